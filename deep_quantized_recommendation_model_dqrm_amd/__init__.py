@@ -1,0 +1,26 @@
+"""MI355X-native (gfx950 / CDNA4) DQRM data-parallel QAT embedding path.
+
+Drop-in for the reference's hot path (YangZhou08/Deep_Quantized_Recommendation_Model_DQRM):
+  * ``quant_modules_not_quantize_grad.QuantEmbeddingBagTwo``  (INT4 fake-quant EmbeddingBag)
+  * ``sgd_quantized_gradients_parallel_comm`` hooks            (INT8 sparse-grad all-reduce + SGD)
+  * ``sgd_quantized_gradients`` simulated-DP buffer helpers
+backed by hand-written HIP kernels behind the C ABI in ``include/dqrm.h`` (libdqrm.so).
+"""
+from . import _lib
+from ._build import LIB_PATH, build
+from .tables import CoalescedGrad, EmbeddingTableSet, LookupBatch, default_caps, reference_scale
+from .comm import SparseGradExchange, get_my_slice, payload_bytes
+
+__all__ = [
+    "LIB_PATH",
+    "build",
+    "_lib",
+    "EmbeddingTableSet",
+    "LookupBatch",
+    "CoalescedGrad",
+    "default_caps",
+    "reference_scale",
+    "SparseGradExchange",
+    "get_my_slice",
+    "payload_bytes",
+]

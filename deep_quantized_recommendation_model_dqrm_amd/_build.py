@@ -1,0 +1,62 @@
+"""Build libdqrm.so (HIP, gfx950) in-tree with hipcc.
+
+The shared library is the product: every hot-path op of this package goes through its
+C ABI (``include/dqrm.h``). It is built in-tree so that it travels with the repository
+snapshot to the GPU box and is the file the Python processes load.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc", "dqrm_kernels.hip")
+HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
+LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    # The reference's `1/s*x + 0`, `(g*s)/s` and `W + (-lr*v)` are separately rounded
+    # operations; contraction would change bits. Intended FMAs are explicit fmaf().
+    "-ffp-contract=off",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libdqrm)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in (CSRC, HEADER, __file__))
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    """Compile csrc/dqrm_kernels.hip into libdqrm.so next to this file."""
+    if not force and not needs_build():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), CSRC, "-o", tmp]
+    if verbose:
+        print("[dqrm] " + " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,148 @@
+"""ctypes binding of libdqrm's C ABI (include/dqrm.h).
+
+This is the same binding a maintainer would add to the reference:
+plain pointers, sizes and an int status per call. There is no CPU fallback: if the
+shared library is missing, importing the compute path raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from ._build import LIB_PATH
+
+DQRM_OK = 0
+DQRM_E_INVALID = -1
+DQRM_E_HIP = -2
+DQRM_E_CAPACITY = -3
+DQRM_E_WORKSPACE = -4
+
+DQRM_ERRF_INDEX = 1
+DQRM_ERRF_OFFSET = 2
+DQRM_ERRF_OVERFLOW = 4
+
+DQRM_BLOCK_ROWS = 256
+DQRM_SBLOCK_ROWS = 65536
+DQRM_MAX_LDS_KEYS = 16384
+
+DQRM_FWD_REFRESH_SCALE = 1
+DQRM_FWD_USE_PACKED = 2
+DQRM_FWD_FULL_PRECISION = 4
+DQRM_FWD_BAG_MAJOR = 8
+
+DQRM_UPD_DP = 0
+DQRM_UPD_SIMULATED = 1
+DQRM_UPD_FP32 = 2
+
+# every symbol include/dqrm.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "dqrm_refresh_absmax",
+    "dqrm_refresh_scale_and_pack",
+    "dqrm_emb_fwd",
+    "dqrm_emb_bwd_sgd",
+    "dqrm_emb_bwd_coalesce",
+    "dqrm_payload_bytes",
+    "dqrm_grad_quant_pack",
+    "dqrm_apply_sparse_update",
+    "dqrm_init_uniform",
+    "dqrm_read_errors",
+    "dqrm_last_error",
+    "dqrm_abi_version",
+)
+
+c_i64p = C.c_void_p  # device pointers are passed as integers
+
+
+class TableSet(C.Structure):
+    """Mirror of ``dqrm_table_set`` (include/dqrm.h)."""
+
+    _fields_ = [
+        ("num_tables", C.c_int32),
+        ("dim", C.c_int32),
+        ("total_rows", C.c_int64),
+        ("total_blocks", C.c_int64),
+        ("total_sblocks", C.c_int64),
+        ("W", C.c_void_p),
+        ("packed", C.c_void_p),
+        ("rowmax", C.c_void_p),
+        ("blkmax", C.c_void_p),
+        ("sblkmax", C.c_void_p),
+        ("tmax", C.c_void_p),
+        ("scale", C.c_void_p),
+        ("pscale", C.c_void_p),
+        ("meta", C.c_void_p),
+        ("err", C.c_void_p),
+        ("tflags", C.c_void_p),
+    ]
+
+
+class Batch(C.Structure):
+    """Mirror of ``dqrm_batch`` (include/dqrm.h)."""
+
+    _fields_ = [
+        ("idx", C.c_void_p),
+        ("off", C.c_void_p),
+        ("idx_base", C.c_void_p),
+        ("num_bags", C.c_int64),
+        ("max_lookups", C.c_int64),
+    ]
+
+
+class DQRMError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libdqrm.so (in-tree). Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise DQRMError(
+            f"libdqrm.so not found at {path}: build it with "
+            "`python -m deep_quantized_recommendation_model_dqrm_amd._build` "
+            "(no CPU fallback exists for the hot path)"
+        )
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    P = C.c_void_p
+    TS = C.POINTER(TableSet)
+    BA = C.POINTER(Batch)
+    sig = {
+        "dqrm_refresh_absmax": (C.c_int, [TS, P]),
+        "dqrm_refresh_scale_and_pack": (C.c_int, [TS, C.c_int, P]),
+        "dqrm_emb_fwd": (C.c_int, [TS, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P]),
+        "dqrm_emb_bwd_sgd": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P]),
+        "dqrm_emb_bwd_coalesce": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, C.c_int, P],
+        ),
+        "dqrm_payload_bytes": (C.c_size_t, [C.c_int, C.c_int64, C.c_int, C.c_int]),
+        "dqrm_grad_quant_pack": (
+            C.c_int,
+            [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, P, P],
+        ),
+        "dqrm_apply_sparse_update": (
+            C.c_int,
+            [TS, P, C.c_int64, P, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
+        ),
+        "dqrm_init_uniform": (C.c_int, [TS, C.c_uint64, P]),
+        "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
+        "dqrm_last_error": (C.c_char_p, []),
+        "dqrm_abi_version": (C.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DQRM_OK:
+        msg = load().dqrm_last_error().decode(errors="replace")
+        raise DQRMError(f"{what} failed ({rc}): {msg}")

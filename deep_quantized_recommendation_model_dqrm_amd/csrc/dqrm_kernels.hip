@@ -1,0 +1,1217 @@
+// dqrm_kernels.hip — CDNA4 (gfx950) kernels and the C ABI of libdqrm.
+//
+// Hot path: DQRM's data-parallel QAT step for embedding tables
+// (reference YangZhou08/Deep_Quantized_Recommendation_Model_DQRM @ 2024-10-24):
+//   fwd   QuantEmbeddingBagTwo.forward      quantization_supp/quant_modules_not_quantize_grad.py:317-398
+//   bwd   SymmetricQuantFunction.backward   quantization_supp/quant_utils.py:349-363
+//   sgd   torch.optim.SGD (sparse)          dlrm_s_pytorch_single_gpu.py:1736-1750,1943-1950
+//   dp    quantize_emb_grad / grad_update_parallel_comm / weight_update_parallel_comm
+//                                           sgd_quantized_gradients_parallel_comm.py:257-317,601-628,850-890
+//
+// Everything here is integer/byte/gather work: HBM- or latency-bound, no MFMA.
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (see build.py). fp-contract must
+// stay off: the reference's `1/s*x + 0`, `(g*s)/s`, `W + (-lr*v)` are separately rounded;
+// the one fused multiply-add the reference does perform (torch CPU's sparse SGD axpy) is
+// written as an explicit fmaf.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+#include <string.h>
+#include <math.h>
+
+#include "../../include/dqrm.h"
+
+#define DQRM_INLINE __device__ __forceinline__
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// error reporting (host)
+// ------------------------------------------------------------------------------------
+thread_local char g_last_error[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return set_error(DQRM_E_HIP, "HIP error: %s (%d)", hipGetErrorString(e_), (int)e_);                                           \
+    } while (0)
+
+#define LAUNCH_CHECK() HIP_TRY(hipGetLastError())
+
+constexpr int WAVE = 64;
+constexpr int BLK = DQRM_BLOCK_ROWS;     // 256
+constexpr int SBLK_BLOCKS = 256;         // blocks per superblock
+constexpr int TABLE_WG = 1024;           // threads of a per-table workgroup
+constexpr int MAX_LDS_KEYS = 16384;      // per-table on-chip sort capacity (128 KiB of keys)
+constexpr int MAX_TABLES = 256;
+
+// ------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------
+struct Meta {
+    const int64_t* row_base;
+    const int64_t* num_rows;
+    const int64_t* blk_base;
+    const int64_t* sblk_base;
+};
+
+DQRM_INLINE Meta make_meta(const int64_t* m, int T) {
+    return Meta{m, m + T, m + 2 * T, m + 3 * T};
+}
+
+DQRM_INLINE int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// largest t with base[t] <= x (base ascending, base[0] == 0)
+DQRM_INLINE int find_table(const int64_t* base, int T, int64_t x) {
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (base[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// symmetric scale: clamp(absmax, min=1e-8) / (2^(bits-1)-1)      quant_utils.py:189-192
+DQRM_INLINE float sym_scale(float absmax, int bits) {
+    const float n = (float)((1 << (bits - 1)) - 1);
+    float a = absmax < 1e-8f ? 1e-8f : absmax;
+    return a / n;
+}
+
+// linear_quantize + clamp: clamp(round(1/s * x + 0), -n-1, n)  quant_utils.py:101,343
+// r = 1/s is precomputed by the caller with an IEEE division (torch: reciprocal(s)*1.0).
+DQRM_INLINE float fake_quant(float x, float r, float lo, float hi) {
+    float t = r * x;
+    t = t + 0.0f;          // `+ zero_point` (zero_point = 0): turns -0 products into +0
+    t = rintf(t);          // torch.round: half to even
+    t = fmaxf(t, lo);      // torch.clamp(min) then (max)
+    t = fminf(t, hi);
+    return t;
+}
+
+DQRM_INLINE float abs_max4(float4 v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
+// max over a group of `G` consecutive lanes (G power of two <= 64)
+template <int G>
+DQRM_INLINE float group_max(float v) {
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, WAVE));
+    return v;
+}
+
+DQRM_INLINE float wave_max(float v) { return group_max<WAVE>(v); }
+
+// pack 4 quantized values (ints in [-8,7] held as float) into 2 offset-binary bytes
+DQRM_INLINE uint16_t pack4_int4(float q0, float q1, float q2, float q3) {
+    uint32_t n0 = (uint32_t)((int)q0 + 8), n1 = (uint32_t)((int)q1 + 8);
+    uint32_t n2 = (uint32_t)((int)q2 + 8), n3 = (uint32_t)((int)q3 + 8);
+    return (uint16_t)(n0 | (n1 << 4) | (n2 << 8) | (n3 << 12));
+}
+
+DQRM_INLINE void flag_error(uint32_t* err, uint32_t f) { atomicOr(err, f); }
+
+// ------------------------------------------------------------------------------------
+// K0: synthetic init, U(-sqrt(1/n), sqrt(1/n)) per table (q_m_n_q_g.py:273-275 distribution)
+// ------------------------------------------------------------------------------------
+DQRM_INLINE uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ void k_init_uniform(float* __restrict__ W, const int64_t* __restrict__ meta, int T,
+                               int D, int64_t total_rows, uint64_t seed) {
+    Meta m = make_meta(meta, T);
+    const int64_t n4 = total_rows * (D / 4);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        int64_t row = q / (D / 4);
+        int t = find_table(m.row_base, T, row);
+        float bound = sqrtf(1.0f / (float)m.num_rows[t]);
+        uint64_t h0 = splitmix64(seed ^ ((uint64_t)q * 2ull));
+        uint64_t h1 = splitmix64(seed ^ ((uint64_t)q * 2ull + 1ull));
+        float4 v;
+        v.x = ((float)(uint32_t)(h0 >> 40) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+        v.y = ((float)(uint32_t)((h0 >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+        v.z = ((float)(uint32_t)(h1 >> 40) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+        v.w = ((float)(uint32_t)((h1 >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+        v.x *= bound; v.y *= bound; v.z *= bound; v.w *= bound;
+        reinterpret_cast<float4*>(W)[q] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K1: absolute-max hierarchy  rowmax -> blkmax -> sblkmax -> tmax
+// (exact replacement of the full-table min/max, quant_utils.py:177-178)
+// ------------------------------------------------------------------------------------
+template <int LPR>  // lanes per row = D/4
+__global__ void k_rowmax_all(const float* __restrict__ W, float* __restrict__ rowmax,
+                             int64_t total_rows) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
+    const int lane = threadIdx.x % LPR;
+    for (int64_t row = gid / LPR; row < total_rows; row += ngrp) {
+        float4 v = reinterpret_cast<const float4*>(W + row * (LPR * 4))[lane];
+        float m = group_max<LPR>(abs_max4(v));
+        if (lane == 0) rowmax[row] = m;
+    }
+}
+
+// one wave per output: out[ob_t + j] = max(in[ib_t + j*256 .. min(+256, nin_t)])
+// level 1: in = rowmax (ib = row_base, nin = num_rows), out = blkmax (ob = blk_base)
+// level 2: in = blkmax (ib = blk_base, nin = nblk),     out = sblkmax (ob = sblk_base)
+__global__ void k_level_max(const float* __restrict__ in, float* __restrict__ out,
+                            const int64_t* __restrict__ meta, int T, int level,
+                            int64_t total_out) {
+    Meta m = make_meta(meta, T);
+    const int lane = threadIdx.x % WAVE;
+    const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
+    const int64_t* ob = level == 1 ? m.blk_base : m.sblk_base;
+    for (int64_t o = wid; o < total_out; o += nw) {
+        int t = find_table(ob, T, o);
+        int64_t j = o - ob[t];
+        int64_t ib = level == 1 ? m.row_base[t] : m.blk_base[t];
+        int64_t nin = level == 1 ? m.num_rows[t] : ceil_div(m.num_rows[t], BLK);
+        int64_t s0 = j * 256, s1 = s0 + 256 < nin ? s0 + 256 : nin;
+        float v = 0.0f;
+        for (int64_t k = s0 + lane; k < s1; k += WAVE) v = fmaxf(v, in[ib + k]);
+        v = wave_max(v);
+        if (lane == 0) out[o] = v;
+    }
+}
+
+// one workgroup per table: tmax[t] = max(sblkmax of t)
+__global__ void k_table_max(const float* __restrict__ sblkmax, float* __restrict__ tmax,
+                            const int64_t* __restrict__ meta, int T) {
+    Meta m = make_meta(meta, T);
+    __shared__ float red[16];
+    const int t = blockIdx.x;
+    const int64_t ns = ceil_div(ceil_div(m.num_rows[t], BLK), SBLK_BLOCKS);
+    float v = 0.0f;
+    for (int64_t k = threadIdx.x; k < ns; k += blockDim.x) v = fmaxf(v, sblkmax[m.sblk_base[t] + k]);
+    v = wave_max(v);
+    if ((threadIdx.x % WAVE) == 0) red[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = 0.0f;
+        for (int w = 0; w < (int)(blockDim.x / WAVE); ++w) r = fmaxf(r, red[w]);
+        tmax[t] = r;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K2: periodic scale refresh + conditional INT4 repack
+// ------------------------------------------------------------------------------------
+__global__ void k_refresh_scale(const float* __restrict__ tmax, float* __restrict__ scale,
+                                float* __restrict__ pscale, uint32_t* __restrict__ tflags,
+                                int T, int bits, int has_packed) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    float s = sym_scale(tmax[t], bits);
+    scale[t] = s;
+    uint32_t need = 0;
+    if (has_packed) {
+        float ps = pscale[t];
+        need = !(ps == s);  // NaN pscale (never packed) -> repack
+        pscale[t] = s;
+    }
+    tflags[t] = need;
+}
+
+template <int LPR>
+DQRM_INLINE void pack_row_int4(const float4 w, uint8_t* __restrict__ packed, int64_t grow,
+                               int lane, float r) {
+    float q0 = fake_quant(w.x, r, -8.0f, 7.0f), q1 = fake_quant(w.y, r, -8.0f, 7.0f);
+    float q2 = fake_quant(w.z, r, -8.0f, 7.0f), q3 = fake_quant(w.w, r, -8.0f, 7.0f);
+    reinterpret_cast<uint16_t*>(packed + grow * (LPR * 2))[lane] = pack4_int4(q0, q1, q2, q3);
+}
+
+template <int LPR>
+__global__ void k_repack_flagged(const float* __restrict__ W, uint8_t* __restrict__ packed,
+                                 const float* __restrict__ scale,
+                                 const uint32_t* __restrict__ tflags,
+                                 const int64_t* __restrict__ meta, int T, int64_t total_rows) {
+    Meta m = make_meta(meta, T);
+    const int lane = threadIdx.x % LPR;
+    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
+    const int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    for (int t = 0; t < T; ++t) {
+        if (!tflags[t]) continue;  // scale unchanged since the last pack: rows still exact
+        const float r = 1.0f / scale[t];
+        const int64_t r0 = m.row_base[t], r1 = r0 + m.num_rows[t];
+        for (int64_t row = r0 + g0; row < r1; row += ngrp) {
+            float4 w = reinterpret_cast<const float4*>(W + row * (LPR * 4))[lane];
+            pack_row_int4<LPR>(w, packed, row, lane, r);
+        }
+    }
+    (void)total_rows;
+}
+
+// ------------------------------------------------------------------------------------
+// K3: fused multi-table fake-quant EmbeddingBag forward
+// One group of LPR = D/4 lanes per bag, float4 per lane; UNR bags in flight per group.
+// Per-table scale / reciprocal / bounds staged in LDS once per workgroup.
+// ------------------------------------------------------------------------------------
+struct FwdArgs {
+    const float* W;
+    const uint8_t* packed;
+    const float* tmax;
+    float* scale;
+    const int64_t* meta;
+    uint32_t* err;
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    float* out;
+    int64_t B;
+    int64_t ost_t, ost_b;
+    int T;
+    int bits;
+    uint32_t flags;
+};
+
+template <int LPR, int UNR>
+__global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
+    __shared__ float s_scale[MAX_TABLES];
+    __shared__ float s_rcp[MAX_TABLES];
+    __shared__ int64_t s_rowbase[MAX_TABLES];
+    __shared__ int64_t s_nrows[MAX_TABLES];
+    __shared__ int64_t s_ibase[MAX_TABLES + 1];
+    const int T = a.T;
+    const bool full_precision = (a.flags & DQRM_FWD_FULL_PRECISION) != 0;
+    const bool refresh = (a.flags & DQRM_FWD_REFRESH_SCALE) != 0;
+    const bool use_packed = (a.flags & DQRM_FWD_USE_PACKED) != 0 && !full_precision;
+    const bool bag_major = (a.flags & DQRM_FWD_BAG_MAJOR) != 0;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        float s = 1.0f;
+        if (!full_precision) s = refresh ? sym_scale(a.tmax[t], a.bits) : a.scale[t];
+        s_scale[t] = s;
+        s_rcp[t] = 1.0f / s;
+        s_rowbase[t] = a.meta[t];
+        s_nrows[t] = a.meta[T + t];
+        s_ibase[t] = a.idx_base[t];
+        if (refresh && !full_precision && blockIdx.x == 0) a.scale[t] = s;
+    }
+    if (threadIdx.x == 0) s_ibase[T] = a.idx_base[T];
+    __syncthreads();
+
+    const float qlo = -(float)(1 << (a.bits - 1));
+    const float qhi = (float)((1 << (a.bits - 1)) - 1);
+    const int lane = threadIdx.x % LPR;
+    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
+    const int64_t total = (int64_t)T * a.B;
+    const int D = LPR * 4;
+
+    for (int64_t u0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; u0 < total;
+         u0 += ngrp * UNR) {
+        int tt[UNR];
+        int64_t bb[UNR], beg[UNR], len[UNR], row[UNR];
+        bool valid[UNR];
+        // phase 1: offsets
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            int64_t u = u0 + (int64_t)k * ngrp;
+            valid[k] = u < total;
+            if (!valid[k]) u = 0;
+            int t; int64_t b;
+            if (bag_major) { b = u / T; t = (int)(u - b * T); }
+            else { t = (int)(u / a.B); b = u - (int64_t)t * a.B; }
+            tt[k] = t; bb[k] = b;
+            const int64_t L = s_ibase[t + 1] - s_ibase[t];
+            int64_t s0 = a.off[(int64_t)t * a.B + b];
+            int64_t s1 = (b + 1 < a.B) ? a.off[(int64_t)t * a.B + b + 1] : L;
+            if (s0 < 0 || s1 > L || s1 < s0) {
+                if (valid[k] && lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
+                s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+                s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+            }
+            beg[k] = s0; len[k] = valid[k] ? s1 - s0 : 0;
+        }
+        // phase 2: single-lookup indices
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            row[k] = -1;
+            if (len[k] == 1) {
+                int64_t r = a.idx[s_ibase[tt[k]] + beg[k]];
+                if (r < 0 || r >= s_nrows[tt[k]]) {
+                    if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+                    r = -1;
+                }
+                row[k] = r;
+            }
+        }
+        // phase 3: row loads for single-lookup bags
+        float4 acc[UNR];
+        uint32_t pk[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            pk[k] = 0x8888u;  // q = 0
+            if (row[k] >= 0) {
+                const int64_t grow = s_rowbase[tt[k]] + row[k];
+                if (use_packed)
+                    pk[k] = reinterpret_cast<const uint16_t*>(a.packed + grow * (D / 2))[lane];
+                else
+                    acc[k] = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
+            }
+        }
+        // phase 4: pooled sums for multi-lookup bags (bag order, FP32), quantize, store
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            if (!valid[k]) continue;
+            const int t = tt[k];
+            const float s = s_scale[t], r = s_rcp[t];
+            float4 y;
+            if (len[k] == 1 && use_packed) {
+                const uint32_t p = pk[k];
+                y.x = (float)((int)(p & 15u) - 8) * s;
+                y.y = (float)((int)((p >> 4) & 15u) - 8) * s;
+                y.z = (float)((int)((p >> 8) & 15u) - 8) * s;
+                y.w = (float)((int)((p >> 12) & 15u) - 8) * s;
+            } else {
+                float4 v = acc[k];
+                if (len[k] > 1) {
+                    const int64_t ib = s_ibase[t] + beg[k];
+                    const int64_t nr = s_nrows[t], rb = s_rowbase[t];
+                    v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (int64_t i = 0; i < len[k]; ++i) {
+                        int64_t rr = a.idx[ib + i];
+                        if (rr < 0 || rr >= nr) {
+                            if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+                            continue;
+                        }
+                        float4 w = reinterpret_cast<const float4*>(a.W + (rb + rr) * D)[lane];
+                        v.x = v.x + w.x; v.y = v.y + w.y; v.z = v.z + w.z; v.w = v.w + w.w;
+                    }
+                }
+                if (full_precision) {
+                    y = v;
+                } else {
+                    y.x = fake_quant(v.x, r, qlo, qhi) * s;
+                    y.y = fake_quant(v.y, r, qlo, qhi) * s;
+                    y.z = fake_quant(v.z, r, qlo, qhi) * s;
+                    y.w = fake_quant(v.w, r, qlo, qhi) * s;
+                }
+            }
+            float* o = a.out + (int64_t)t * a.ost_t + bb[k] * a.ost_b;
+            reinterpret_cast<float4*>(o)[lane] = y;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Per-table workgroup machinery (backward / coalesce / apply):
+// keys = (local_row << 32) | tag sorted in LDS (bitonic), segments = equal rows.
+// ------------------------------------------------------------------------------------
+DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
+
+DQRM_INLINE void bitonic_sort_lds(uint64_t* keys, int n_pow2) {
+    for (int k = 2; k <= n_pow2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int p = threadIdx.x; p < (n_pow2 >> 1); p += blockDim.x) {
+                const int i = ((p / j) * 2 * j) + (p % j);
+                const int l = i + j;
+                uint64_t x = keys[i], y = keys[l];
+                const bool up = (i & k) == 0;
+                if ((x > y) == up) { keys[i] = y; keys[l] = x; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+DQRM_INLINE int next_pow2(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+// block-wide exclusive scan of head flags: returns per-thread chunk base (LDS) so that
+// the unique ordinal of a head at position i = base[i / CH] + heads in [CH*(i/CH), i)
+template <int CH>
+DQRM_INLINE int head_scan(const uint64_t* keys, int n, int* s_base, int* s_wtot) {
+    const int tid = threadIdx.x;
+    int cnt = 0;
+    const int i0 = tid * CH;
+#pragma unroll 4
+    for (int c = 0; c < CH; ++c) {
+        int i = i0 + c;
+        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
+    }
+    // inclusive wave scan
+    int v = cnt;
+    const int lane = tid % WAVE, w = tid / WAVE;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(v, o, WAVE);
+        if (lane >= o) v += y;
+    }
+    if (lane == WAVE - 1) s_wtot[w] = v;
+    __syncthreads();
+    if (tid == 0) {
+        int run = 0;
+        for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wtot[k]; s_wtot[k] = run; run += x; }
+        s_wtot[blockDim.x / WAVE] = run;
+    }
+    __syncthreads();
+    s_base[tid] = s_wtot[w] + v - cnt;
+    __syncthreads();
+    return s_wtot[blockDim.x / WAVE];
+}
+
+template <int CH>
+DQRM_INLINE int head_ordinal(const uint64_t* keys, const int* s_base, int i) {
+    const int c0 = (i / CH) * CH;
+    int u = s_base[i / CH];
+    for (int j = c0; j < i; ++j)
+        if (j == 0 || key_row(keys[j]) != key_row(keys[j - 1])) ++u;
+    return u;
+}
+
+// maintain blkmax/sblkmax/tmax of table t after rows of sorted `keys` changed rowmax.
+DQRM_INLINE void maintain_hierarchy(const Meta& m, int t, const uint64_t* keys, int n,
+                                    const float* rowmax, float* blkmax, float* sblkmax,
+                                    float* tmax, float* s_red) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const int64_t nrows = m.num_rows[t];
+    const int64_t nblk = ceil_div(nrows, BLK);
+    const int64_t nsblk = ceil_div(nblk, SBLK_BLOCKS);
+    // dirty blocks: first key of each distinct (row >> 8)
+    for (int base = w * WAVE; base < n; base += nw * WAVE) {
+        const int i = base + lane;
+        bool head = false;
+        if (i < n) {
+            uint32_t b = key_row(keys[i]) >> 8;
+            head = (i == 0) || (key_row(keys[i - 1]) >> 8) != b;
+        }
+        uint64_t msk = __ballot(head);
+        while (msk) {
+            const int l = __ffsll((long long)msk) - 1;
+            msk &= msk - 1;
+            const int64_t b = key_row(keys[base + l]) >> 8;
+            const int64_t r0 = b * BLK;
+            const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
+            float v = 0.0f;
+            for (int64_t r = r0 + lane; r < r1; r += WAVE) v = fmaxf(v, rowmax[m.row_base[t] + r]);
+            v = wave_max(v);
+            if (lane == 0) blkmax[m.blk_base[t] + b] = v;
+        }
+    }
+    __syncthreads();
+    for (int base = w * WAVE; base < n; base += nw * WAVE) {
+        const int i = base + lane;
+        bool head = false;
+        if (i < n) {
+            uint32_t sb = key_row(keys[i]) >> 16;
+            head = (i == 0) || (key_row(keys[i - 1]) >> 16) != sb;
+        }
+        uint64_t msk = __ballot(head);
+        while (msk) {
+            const int l = __ffsll((long long)msk) - 1;
+            msk &= msk - 1;
+            const int64_t sb = key_row(keys[base + l]) >> 16;
+            const int64_t b0 = sb * SBLK_BLOCKS;
+            const int64_t b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+            float v = 0.0f;
+            for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[m.blk_base[t] + b]);
+            v = wave_max(v);
+            if (lane == 0) sblkmax[m.sblk_base[t] + sb] = v;
+        }
+    }
+    __syncthreads();
+    float v = 0.0f;
+    for (int64_t k = threadIdx.x; k < nsblk; k += blockDim.x) v = fmaxf(v, sblkmax[m.sblk_base[t] + k]);
+    v = wave_max(v);
+    if (lane == 0) s_red[w] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float r = 0.0f;
+        for (int k = 0; k < nw; ++k) r = fmaxf(r, s_red[k]);
+        tmax[t] = r;
+    }
+    __syncthreads();
+}
+
+// build sorted (row << 32 | bag) keys of table t in LDS; returns L (0..), -1 on capacity
+DQRM_INLINE int build_lookup_keys(uint64_t* keys, int key_cap, const int64_t* idx,
+                                  const int64_t* off, const int64_t* idx_base, int64_t B, int t,
+                                  int64_t nrows, uint32_t* err) {
+    const int64_t ib = idx_base[t];
+    const int64_t L = idx_base[t + 1] - ib;
+    if (L < 0 || next_pow2(L < 2 ? 2 : (int)(L > (1 << 30) ? (1 << 30) : L)) > key_cap) {
+        if (threadIdx.x == 0) flag_error(err, DQRM_ERRF_OVERFLOW);
+        return -1;  // uniform across the workgroup
+    }
+    const int n = (int)L;
+    const int np2 = next_pow2(n < 2 ? 2 : n);
+    for (int i = threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
+    __syncthreads();
+    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
+        int64_t s0 = off[(int64_t)t * B + b];
+        int64_t s1 = (b + 1 < B) ? off[(int64_t)t * B + b + 1] : L;
+        if (s0 < 0 || s1 > L || s1 < s0) {
+            flag_error(err, DQRM_ERRF_OFFSET);
+            s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+            s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+        }
+        for (int64_t p = s0; p < s1; ++p) {
+            int64_t r = idx[ib + p];
+            if (r < 0 || r >= nrows) { flag_error(err, DQRM_ERRF_INDEX); continue; }
+            keys[p] = ((uint64_t)r << 32) | (uint64_t)b;
+        }
+    }
+    __syncthreads();
+    bitonic_sort_lds(keys, np2);
+    // positions whose index was invalid (or not covered by any bag) stay ~0 and sort last
+    int valid = 0;
+    // count valid keys: first position with row == 0xFFFFFFFF
+    // (binary search on sorted keys)
+    {
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1;
+        }
+        valid = lo;
+    }
+    return valid;
+}
+
+struct BwdArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    float* tmax;
+    const float* scale;
+    const float* pscale;
+    const int64_t* meta;
+    uint32_t* err;
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    const float* dy;
+    int64_t B;
+    int64_t dst_t, dst_b;
+    int T;
+    int ste;
+    float nlr;          // -lr (f32)
+    int repack;         // repack touched INT4 rows with pscale
+    // coalesce mode outputs
+    const int64_t* cap_base;
+    int32_t* rows_out;
+    float* vals_out;
+    int32_t* counts_out;
+    float* s_loc;
+    int grad_bits;
+    int key_cap;        // dynamic-LDS key capacity (power of two)
+};
+
+// MODE 0: fused SGD (single GPU);  MODE 1: coalesce + local grad scale (DP)
+template <int LPR, int MODE>
+__global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
+    // static LDS kept a multiple of 16 bytes (Guideline 17: dynamic base alignment)
+    __shared__ int s_base[TABLE_WG];
+    __shared__ int s_wtot[TABLE_WG / WAVE + 4];
+    __shared__ float s_red[TABLE_WG / WAVE];
+    __shared__ unsigned int s_absmax_arr[4];
+    unsigned int& s_absmax = s_absmax_arr[0];
+
+    const int t = blockIdx.x;
+    const int T = a.T;
+    Meta m = make_meta(a.meta, T);
+    const int64_t nrows = m.num_rows[t];
+    const int64_t rb = m.row_base[t];
+    const int D = LPR * 4;
+    const int L = (int)(a.idx_base[t + 1] - a.idx_base[t]);
+    if (threadIdx.x == 0) s_absmax = 0u;
+
+    const int n = build_lookup_keys(keys, a.key_cap, a.idx, a.off, a.idx_base, a.B, t, nrows, a.err);
+    if (n < 0) {
+        if (MODE == 1 && threadIdx.x == 0) { a.counts_out[t] = 0; a.s_loc[t] = 0.0f; }
+        return;
+    }
+    const int U = head_scan<MAX_LDS_KEYS / TABLE_WG>(keys, n, s_base, s_wtot);
+
+    const float s = a.scale[t];
+    const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+    const int lane = threadIdx.x % LPR;
+    const int grp = threadIdx.x / LPR;
+    const int ngrp = blockDim.x / LPR;
+    int64_t cap = 0;
+    if (MODE == 1) cap = a.cap_base[t + 1] - a.cap_base[t];
+    float local_absmax = 0.0f;
+
+    for (int i = grp; i < n; i += ngrp) {
+        const uint32_t row = key_row(keys[i]);
+        if (i > 0 && key_row(keys[i - 1]) == row) continue;  // not a segment head
+        const int64_t grow = rb + row;
+        float4 w;
+        if (MODE == 0) w = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool first = true;
+        for (int j = i; j < n; ++j) {
+            const uint64_t kk = keys[j];
+            if (key_row(kk) != row) break;
+            const int64_t bag = (int64_t)(uint32_t)kk;
+            float4 g = reinterpret_cast<const float4*>(a.dy + (int64_t)t * a.dst_t + bag * a.dst_b)[lane];
+            if (a.ste) {  // SymmetricQuantFunction.backward of q*s: (g*s)/s
+                g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
+            }
+            if (MODE == 0) {  // torch CPU sparse SGD: per entry, in lookup order, w = fma(v, -lr, w)
+                w.x = fmaf(g.x, a.nlr, w.x); w.y = fmaf(g.y, a.nlr, w.y);
+                w.z = fmaf(g.z, a.nlr, w.z); w.w = fmaf(g.w, a.nlr, w.w);
+            } else {          // coalesce(): first value, then += in ascending position order
+                if (first) { acc = g; first = false; }
+                else { acc.x = acc.x + g.x; acc.y = acc.y + g.y; acc.z = acc.z + g.z; acc.w = acc.w + g.w; }
+            }
+        }
+        if (MODE == 0) {
+            reinterpret_cast<float4*>(a.W + grow * D)[lane] = w;
+            const float rm = group_max<LPR>(abs_max4(w));
+            if (lane == 0) a.rowmax[grow] = rm;
+            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, lane, r_pack);
+        } else {
+            const int u = head_ordinal<MAX_LDS_KEYS / TABLE_WG>(keys, s_base, i);
+            if (u < cap) {
+                const int64_t e = a.cap_base[t] + u;
+                reinterpret_cast<float4*>(a.vals_out + e * D)[lane] = acc;
+                if (lane == 0) a.rows_out[e] = (int32_t)row;
+            }
+            local_absmax = fmaxf(local_absmax, abs_max4(acc));
+        }
+    }
+    if (MODE == 1) {
+        local_absmax = wave_max(local_absmax);
+        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_absmax, __float_as_uint(local_absmax));
+    }
+    __syncthreads();
+    if (MODE == 0) {
+        maintain_hierarchy(m, t, keys, n, a.rowmax, a.blkmax, a.sblkmax, a.tmax, s_red);
+    } else if (threadIdx.x == 0) {
+        if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        a.counts_out[t] = U < cap ? U : (int32_t)cap;
+        if (a.grad_bits >= 2 && a.grad_bits <= 16)
+            a.s_loc[t] = sym_scale(__uint_as_float(s_absmax), a.grad_bits);
+        else
+            a.s_loc[t] = 0.0f;
+    }
+    (void)L;
+}
+
+// ------------------------------------------------------------------------------------
+// K5: scale average + quantize-pack into the wire payload
+// ------------------------------------------------------------------------------------
+struct PayloadLayout {
+    int64_t rows_off;   // bytes
+    int64_t vals_off;   // bytes
+    int64_t bytes;
+    int elem;           // bytes per value
+};
+
+__host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
+
+__host__ __device__ inline PayloadLayout payload_layout(int T, int64_t cap, int D, int bits) {
+    PayloadLayout p;
+    p.elem = bits <= 8 ? 1 : (bits <= 16 ? 2 : 4);
+    p.rows_off = align16(4 * (int64_t)T);
+    p.vals_off = p.rows_off + align16(4 * cap);
+    p.bytes = p.vals_off + align16(cap * (int64_t)D * p.elem);
+    return p;
+}
+
+// dist.all_reduce(scale, SUM) then scale.mul_(1./N) (s_q_g_p_c.py:865-866). Gloo's
+// allreduce of a one-element tensor accumulates in descending rank order
+// (((s_{N-1} + s_{N-2}) + ...) + s_0) — measured for N = 2..8 with torch 2.10's Gloo;
+// every rank evaluates the same order on the all-gathered scales, so the average is
+// bit-identical across ranks and equal to the reference's.
+DQRM_INLINE float average_scale(const float* s_all, int T, int N, int t, float inv_n) {
+    float acc = s_all[(int64_t)(N - 1) * T + t];
+    for (int r = N - 2; r >= 0; --r) acc = acc + s_all[(int64_t)r * T + t];
+    return acc * inv_n;
+}
+
+template <int LPR>
+__global__ void k_quant_pack(int T, const int64_t* __restrict__ cap_base, int64_t cap_total,
+                             const int32_t* __restrict__ rows, const float* __restrict__ vals,
+                             const int32_t* __restrict__ counts, const float* __restrict__ s_all,
+                             int N, int bits, float* __restrict__ s_avg,
+                             unsigned char* __restrict__ payload) {
+    const int D = LPR * 4;
+    const PayloadLayout pl = payload_layout(T, cap_total, D, bits);
+    const bool quant = bits >= 2 && bits <= 16;
+    const float inv_n = (float)(1.0 / (double)N);
+    if (blockIdx.x == 0) {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            reinterpret_cast<int32_t*>(payload)[t] = counts[t];
+            if (quant) s_avg[t] = average_scale(s_all, T, N, t, inv_n);
+        }
+    }
+    const int lane = threadIdx.x % LPR;
+    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
+    const float qlo = -(float)(1 << (bits - 1)), qhi = (float)((1 << (bits - 1)) - 1);
+    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < cap_total; e += ngrp) {
+        const int t = find_table(cap_base, T, e);
+        if (e - cap_base[t] >= counts[t]) continue;
+        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[e] = rows[e];
+        float4 v = reinterpret_cast<const float4*>(vals + e * D)[lane];
+        if (!quant) {
+            reinterpret_cast<float4*>(payload + pl.vals_off + e * D * 4)[lane] = v;
+            continue;
+        }
+        const float s = average_scale(s_all, T, N, t, inv_n);
+        const float rr = 1.0f / s;
+        const float q0 = fake_quant(v.x, rr, qlo, qhi), q1 = fake_quant(v.y, rr, qlo, qhi);
+        const float q2 = fake_quant(v.z, rr, qlo, qhi), q3 = fake_quant(v.w, rr, qlo, qhi);
+        if (pl.elem == 1) {
+            uint32_t pk = ((uint32_t)(uint8_t)(int8_t)(int)q0) | ((uint32_t)(uint8_t)(int8_t)(int)q1 << 8) |
+                          ((uint32_t)(uint8_t)(int8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int8_t)(int)q3 << 24);
+            reinterpret_cast<uint32_t*>(payload + pl.vals_off + e * D)[lane] = pk;
+        } else {
+            uint2 pk;
+            pk.x = ((uint32_t)(uint16_t)(int16_t)(int)q0) | ((uint32_t)(uint16_t)(int16_t)(int)q1 << 16);
+            pk.y = ((uint32_t)(uint16_t)(int16_t)(int)q2) | ((uint32_t)(uint16_t)(int16_t)(int)q3 << 16);
+            reinterpret_cast<uint2*>(payload + pl.vals_off + e * D * 2)[lane] = pk;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// K6: decode N payloads, union rows, sum, dequantize, SGD update + maintenance
+// keys = (row << 32) | (rank << 24) | entry
+// ------------------------------------------------------------------------------------
+struct ApplyArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    float* tmax;
+    const float* pscale;
+    const int64_t* meta;
+    uint32_t* err;
+    const int64_t* cap_base;
+    int64_t cap_total;
+    const unsigned char* payloads;
+    int64_t payload_bytes;
+    int N;
+    int T;
+    int bits;
+    const float* s_avg;
+    float nlr;
+    int mode;
+    int repack;
+    int key_cap;
+};
+
+template <int LPR>
+DQRM_INLINE float4 load_payload_vals(const unsigned char* p, const PayloadLayout& pl, int64_t e,
+                                     int lane) {
+    const int D = LPR * 4;
+    float4 v;
+    if (pl.elem == 1) {
+        uint32_t x = reinterpret_cast<const uint32_t*>(p + pl.vals_off + e * D)[lane];
+        v.x = (float)(int8_t)(x & 0xFF); v.y = (float)(int8_t)((x >> 8) & 0xFF);
+        v.z = (float)(int8_t)((x >> 16) & 0xFF); v.w = (float)(int8_t)(x >> 24);
+    } else if (pl.elem == 2) {
+        uint2 x = reinterpret_cast<const uint2*>(p + pl.vals_off + e * D * 2)[lane];
+        v.x = (float)(int16_t)(x.x & 0xFFFF); v.y = (float)(int16_t)(x.x >> 16);
+        v.z = (float)(int16_t)(x.y & 0xFFFF); v.w = (float)(int16_t)(x.y >> 16);
+    } else {
+        v = reinterpret_cast<const float4*>(p + pl.vals_off + e * D * 4)[lane];
+    }
+    return v;
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
+    __shared__ int s_cnt[68];
+    __shared__ int s_start[68];
+    __shared__ float s_red[TABLE_WG / WAVE];
+
+    const int t = blockIdx.x;
+    const int T = a.T;
+    const int D = LPR * 4;
+    Meta m = make_meta(a.meta, T);
+    const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
+    const int64_t cap = a.cap_base[t + 1] - a.cap_base[t];
+    const int64_t rb = m.row_base[t];
+    const int64_t nrows = m.num_rows[t];
+    if (threadIdx.x < a.N) {
+        const unsigned char* p = a.payloads + (int64_t)threadIdx.x * a.payload_bytes;
+        int c = reinterpret_cast<const int32_t*>(p)[t];
+        if (c < 0 || c > cap) { flag_error(a.err, DQRM_ERRF_OVERFLOW); c = c < 0 ? 0 : (int)cap; }
+        s_cnt[threadIdx.x] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int r = 0; r < a.N; ++r) { s_start[r] = run; run += s_cnt[r]; }
+        s_start[a.N] = run;
+    }
+    __syncthreads();
+    const int M = s_start[a.N];
+    if (next_pow2(M < 2 ? 2 : M) > a.key_cap) {  // uniform: whole workgroup leaves
+        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        return;
+    }
+    const int np2 = next_pow2(M < 2 ? 2 : M);
+    for (int i = threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
+    __syncthreads();
+    for (int i = threadIdx.x; i < M; i += blockDim.x) {
+        int r = 0;
+        while (i >= s_start[r + 1]) ++r;
+        const int e = i - s_start[r];
+        const unsigned char* p = a.payloads + (int64_t)r * a.payload_bytes;
+        int64_t row = reinterpret_cast<const int32_t*>(p + pl.rows_off)[a.cap_base[t] + e];
+        if (row < 0 || row >= nrows) { flag_error(a.err, DQRM_ERRF_INDEX); continue; }
+        keys[i] = ((uint64_t)row << 32) | ((uint64_t)r << 24) | (uint64_t)e;
+    }
+    __syncthreads();
+    bitonic_sort_lds(keys, np2);
+    int n;
+    {
+        int lo = 0, hi = M;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1; }
+        n = lo;
+    }
+
+    const float s = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const float inv_n = (float)(1.0 / (double)a.N);
+    const float sim_f = (float)((double)s / (double)a.N);
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    const int lane = threadIdx.x % LPR;
+    const int grp = threadIdx.x / LPR;
+    const int ngrp = blockDim.x / LPR;
+    for (int i = grp; i < n; i += ngrp) {
+        const uint32_t row = key_row(keys[i]);
+        if (i > 0 && key_row(keys[i - 1]) == row) continue;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        bool first = true;
+        for (int j = i; j < n; ++j) {
+            const uint64_t kk = keys[j];
+            if (key_row(kk) != row) break;
+            const int r = (int)((kk >> 24) & 0xFF);
+            const int64_t e = a.cap_base[t] + (int64_t)(kk & 0xFFFFFF);
+            float4 v = load_payload_vals<LPR>(a.payloads + (int64_t)r * a.payload_bytes, pl, e, lane);
+            // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
+            // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
+            if (first) { acc = v; first = false; }
+            else { acc.x = acc.x + v.x; acc.y = acc.y + v.y; acc.z = acc.z + v.z; acc.w = acc.w + v.w; }
+        }
+        float4 v;
+        if (a.mode == DQRM_UPD_DP) {          // update.mul_(1/N) ; grad * s.item()
+            v.x = (acc.x * inv_n) * s; v.y = (acc.y * inv_n) * s;
+            v.z = (acc.z * inv_n) * s; v.w = (acc.w * inv_n) * s;
+        } else if (a.mode == DQRM_UPD_SIMULATED) {  // buffer * (s.item()/N)
+            v.x = acc.x * sim_f; v.y = acc.y * sim_f; v.z = acc.z * sim_f; v.w = acc.w * sim_f;
+        } else {                              // FP32 sparse allreduce, mul_(1/N)
+            v.x = acc.x * inv_n; v.y = acc.y * inv_n; v.z = acc.z * inv_n; v.w = acc.w * inv_n;
+        }
+        const int64_t grow = rb + row;
+        float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
+        // weight.data.add_(-lr * grad_update): separately rounded product, then add
+        w.x = w.x + a.nlr * v.x; w.y = w.y + a.nlr * v.y; w.z = w.z + a.nlr * v.z; w.w = w.w + a.nlr * v.w;
+        reinterpret_cast<float4*>(a.W + grow * D)[lane] = w;
+        const float rm = group_max<LPR>(abs_max4(w));
+        if (lane == 0) a.rowmax[grow] = rm;
+        if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, lane, r_pack);
+    }
+    __syncthreads();
+    maintain_hierarchy(m, t, keys, n, a.rowmax, a.blkmax, a.sblkmax, a.tmax, s_red);
+}
+
+// ------------------------------------------------------------------------------------
+// host helpers
+// ------------------------------------------------------------------------------------
+int check_set(const dqrm_table_set* s) {
+    if (!s) return set_error(DQRM_E_INVALID, "dqrm: null table set");
+    if (s->num_tables <= 0 || s->num_tables > MAX_TABLES)
+        return set_error(DQRM_E_INVALID, "dqrm: num_tables out of range (%d)", s->num_tables);
+    const int D = s->dim;
+    if (D < 4 || D > 256 || (D & 3) || ((D / 4) & (D / 4 - 1)))
+        return set_error(DQRM_E_INVALID, "dqrm: dim must be 4*2^k <= 256 (got %d)", D);
+    if (!s->W || !s->rowmax || !s->blkmax || !s->sblkmax || !s->tmax || !s->scale || !s->pscale ||
+        !s->meta || !s->err || !s->tflags)
+        return set_error(DQRM_E_INVALID, "dqrm: null state pointer");
+    if (((uintptr_t)s->W) & 15)
+        return set_error(DQRM_E_INVALID, "dqrm: W must be 16-byte aligned");
+    return DQRM_OK;
+}
+
+int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
+    int64_t b = (work_items + threads - 1) / threads;
+    if (b < 1) b = 1;
+    if (b > max_blocks) b = max_blocks;
+    return (int)b;
+}
+
+#define DISPATCH_LPR(D, ...)                                  \
+    switch ((D) / 4) {                                        \
+        case 1: { constexpr int LPR = 1; __VA_ARGS__; } break;  \
+        case 2: { constexpr int LPR = 2; __VA_ARGS__; } break;  \
+        case 4: { constexpr int LPR = 4; __VA_ARGS__; } break;  \
+        case 8: { constexpr int LPR = 8; __VA_ARGS__; } break;  \
+        case 16: { constexpr int LPR = 16; __VA_ARGS__; } break; \
+        case 32: { constexpr int LPR = 32; __VA_ARGS__; } break; \
+        case 64: { constexpr int LPR = 64; __VA_ARGS__; } break; \
+        default: return set_error(DQRM_E_INVALID, "dqrm: unsupported dim %d", (int)(D)); \
+    }
+
+size_t table_lds_bytes(int64_t max_keys) {
+    int64_t n = 2;
+    while (n < max_keys) n <<= 1;
+    return (size_t)n * sizeof(uint64_t);
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+extern "C" {
+
+const char* dqrm_last_error(void) { return g_last_error; }
+int dqrm_abi_version(void) { return DQRM_ABI_VERSION; }
+
+int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n4 = set->total_rows * (set->dim / 4);
+    hipLaunchKernelGGL(k_init_uniform, dim3(grid_for(n4, 256, 8192)), dim3(256), 0, st, set->W,
+                       set->meta, set->num_tables, set->dim, set->total_rows, seed);
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_refresh_absmax(const dqrm_table_set* set, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        hipLaunchKernelGGL(k_rowmax_all<LPR>, dim3(grid_for(set->total_rows * LPR, 256, 8192)), dim3(256), 0,
+                           st, set->W, set->rowmax, set->total_rows);
+    });
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_level_max, dim3(grid_for(set->total_blocks * WAVE, 256, 8192)), dim3(256), 0, st,
+                       set->rowmax, set->blkmax, set->meta, set->num_tables, 1, set->total_blocks);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_level_max, dim3(grid_for(set->total_sblocks * WAVE, 256, 8192)), dim3(256), 0, st,
+                       set->blkmax, set->sblkmax, set->meta, set->num_tables, 2, set->total_sblocks);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_table_max, dim3(set->num_tables), dim3(256), 0, st, set->sblkmax, set->tmax,
+                       set->meta, set->num_tables);
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_refresh_scale_and_pack(const dqrm_table_set* set, int bits, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if (bits < 2 || bits > 16) return set_error(DQRM_E_INVALID, "%s: bits %d unsupported", "refresh", bits);
+    if (set->packed && bits != 4)
+        return set_error(DQRM_E_INVALID, "%s: packed rows need bits == 4 (got %d)", "refresh", bits);
+    hipStream_t st = (hipStream_t)stream;
+    const int T = set->num_tables;
+    hipLaunchKernelGGL(k_refresh_scale, dim3((T + 255) / 256), dim3(256), 0, st, set->tmax, set->scale,
+                       set->pscale, set->tflags, T, bits, set->packed != nullptr);
+    LAUNCH_CHECK();
+    if (set->packed) {
+        const int D = set->dim;
+        DISPATCH_LPR(D, {
+            hipLaunchKernelGGL(k_repack_flagged<LPR>, dim3(grid_for(set->total_rows * LPR, 256, 8192)),
+                               dim3(256), 0, st, set->W, set->packed, set->scale, set->tflags, set->meta,
+                               T, set->total_rows);
+        });
+        LAUNCH_CHECK();
+    }
+    return DQRM_OK;
+}
+
+int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags,
+                 float* out, int64_t out_stride_t, int64_t out_stride_b, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if (!batch || !batch->idx || !batch->off || !batch->idx_base || !out)
+        return set_error(DQRM_E_INVALID, "%s: null batch/out pointer", "dqrm_emb_fwd");
+    if (!(flags & DQRM_FWD_FULL_PRECISION) && (bits < 2 || bits > 16))
+        return set_error(DQRM_E_INVALID, "%s: embedding_bit %d unsupported", "dqrm_emb_fwd", bits);
+    if ((flags & DQRM_FWD_USE_PACKED) && (!set->packed || bits != 4))
+        return set_error(DQRM_E_INVALID, "%s: packed path needs packed rows and bits == 4", "dqrm_emb_fwd");
+    if ((((uintptr_t)out) & 15) || (out_stride_t & 3) || (out_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: out must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_fwd");
+    if (batch->num_bags <= 0) return DQRM_OK;
+    FwdArgs a;
+    a.W = set->W; a.packed = set->packed; a.tmax = set->tmax; a.scale = set->scale;
+    a.meta = set->meta; a.err = set->err;
+    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base;
+    a.out = out; a.B = batch->num_bags; a.ost_t = out_stride_t; a.ost_b = out_stride_b;
+    a.T = set->num_tables; a.bits = bits; a.flags = flags;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t total = (int64_t)a.T * a.B;
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        constexpr int UNR = 4;
+        int blocks = grid_for(total * LPR, 256 * UNR, 4096);
+        hipLaunchKernelGGL((k_emb_fwd<LPR, UNR>), dim3(blocks), dim3(256), 0, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+static int check_batch_capacity(const dqrm_batch* batch, const char* who) {
+    if (!batch || !batch->idx || !batch->off || !batch->idx_base)
+        return set_error(DQRM_E_INVALID, "%s: null batch pointer", who);
+    if (batch->max_lookups > MAX_LDS_KEYS || batch->num_bags > 0xFFFFFFFFll)
+        return set_error(DQRM_E_CAPACITY, "%s: per-table lookups %lld exceed the on-chip sort capacity (16384)",
+                         who, (long long)batch->max_lookups);
+    return DQRM_OK;
+}
+
+int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                     int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, int repack_bits,
+                     void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch_capacity(batch, "dqrm_emb_bwd_sgd"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_sgd");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_emb_bwd_sgd", repack_bits);
+    if (batch->num_bags <= 0) return DQRM_OK;
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
+    a.sblkmax = set->sblkmax; a.tmax = set->tmax; a.scale = set->scale; a.pscale = set->pscale;
+    a.meta = set->meta; a.err = set->err;
+    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
+    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
+    a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t lds = table_lds_bytes(batch->max_lookups);
+    a.key_cap = (int)(lds / sizeof(uint64_t));
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        hipLaunchKernelGGL((k_table_bwd<LPR, 0>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                          int64_t dy_stride_t, int64_t dy_stride_b, int ste,
+                          const int64_t* cap_base, int32_t* rows, float* vals, int32_t* counts,
+                          float* s_loc, int grad_bits, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch_capacity(batch, "dqrm_emb_bwd_coalesce"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_coalesce");
+    if (!cap_base || !rows || !vals || !counts || !s_loc || (((uintptr_t)vals) & 15))
+        return set_error(DQRM_E_INVALID, "%s: null/unaligned output", "dqrm_emb_bwd_coalesce");
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.W = set->W; a.scale = set->scale; a.meta = set->meta; a.err = set->err;
+    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
+    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables; a.ste = ste;
+    a.cap_base = cap_base; a.rows_out = rows; a.vals_out = vals; a.counts_out = counts; a.s_loc = s_loc;
+    a.grad_bits = grad_bits;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t lds = table_lds_bytes(batch->max_lookups);
+    a.key_cap = (int)(lds / sizeof(uint64_t));
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        hipLaunchKernelGGL((k_table_bwd<LPR, 1>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits) {
+    return (size_t)payload_layout(num_tables, cap_total, dim, grad_bits).bytes;
+}
+
+int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* cap_base, int64_t cap_total,
+                         const int32_t* rows, const float* vals, const int32_t* counts,
+                         const float* s_all, int num_ranks, int grad_bits, float* s_avg,
+                         void* payload, void* stream) {
+    if (num_tables <= 0 || num_tables > MAX_TABLES || num_ranks <= 0 || num_ranks > 64)
+        return set_error(DQRM_E_INVALID, "%s: bad num_tables/num_ranks", "dqrm_grad_quant_pack");
+    if (!(grad_bits == 32 || (grad_bits >= 2 && grad_bits <= 16)))
+        return set_error(DQRM_E_INVALID, "%s: grad bits %d unsupported", "dqrm_grad_quant_pack", grad_bits);
+    if (!cap_base || !rows || !vals || !counts || !payload || (grad_bits != 32 && (!s_all || !s_avg)))
+        return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_grad_quant_pack");
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_LPR(dim, {
+        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(grid_for(cap_total * LPR, 256, 4096)), dim3(256), 0, st,
+                           num_tables, cap_base, cap_total, rows, vals, counts, s_all, num_ranks, grad_bits,
+                           s_avg, (unsigned char*)payload);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                             const void* payloads, size_t payload_bytes, int num_ranks, int grad_bits,
+                             const float* s_avg, float lr, int mode, int repack_bits, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if (num_ranks <= 0 || num_ranks > 64 || !payloads || !cap_base)
+        return set_error(DQRM_E_INVALID, "%s: bad ranks/payloads (%d)", "dqrm_apply_sparse_update", num_ranks);
+    if (mode == DQRM_UPD_FP32 ? grad_bits != 32 : (grad_bits < 2 || grad_bits > 16 || !s_avg))
+        return set_error(DQRM_E_INVALID, "%s: mode/grad_bits mismatch (%d)", "dqrm_apply_sparse_update", grad_bits);
+    if (payload_bytes != dqrm_payload_bytes(set->num_tables, cap_total, set->dim, grad_bits))
+        return set_error(DQRM_E_INVALID, "%s: payload_bytes mismatch", "dqrm_apply_sparse_update");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_apply_sparse_update", repack_bits);
+    ApplyArgs a;
+    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
+    a.sblkmax = set->sblkmax; a.tmax = set->tmax; a.pscale = set->pscale; a.meta = set->meta;
+    a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
+    a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)payload_bytes;
+    a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
+    a.mode = mode; a.repack = repack_bits == 4;
+    // every table's merged entry count must fit the on-chip sort (checked again on device)
+    hipStream_t st = (hipStream_t)stream;
+    a.key_cap = MAX_LDS_KEYS;
+    const size_t lds = table_lds_bytes(MAX_LDS_KEYS);
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T), dim3(TABLE_WG), lds, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {
+    if (!set || !set->err || !flags) return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_read_errors");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(flags, set->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (clear) HIP_TRY(hipMemsetAsync(set->err, 0, sizeof(uint32_t), st));
+    return DQRM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,315 @@
+"""Resident embedding-table state and lookup batches, driven through libdqrm's C ABI.
+
+Memory layout in HBM (one slab per array, all T tables back to back):
+    W       f32 [R, D]      FP32 master rows (table t: rows row_base[t] .. +num_rows[t])
+    packed  u8  [R, D/2]    INT4 rows, offset-binary nibbles, element 2j in the low nibble
+    rowmax  f32 [R]         max_d |W[r, d]|
+    blkmax  f32 [NB]        per 256-row block,   sblkmax f32 [NS] per 65536-row superblock
+    tmax    f32 [T]         max |W_t|  (=> reference scale s_t = max(tmax_t, 1e-8)/7)
+
+Reference semantics: quantization_supp/quant_modules_not_quantize_grad.py:240-398 (module),
+quantization_supp/quant_utils.py:75-101,141-194,316-363 (math).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Sequence
+
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ceil_div(a: int, b: int) -> int:
+    return (a + b - 1) // b
+
+
+class LookupBatch:
+    """All tables' lookups of one batch in the reference's (lS_i, lS_o) form.
+
+    Accepted inputs (dlrm_data_pytorch.py:328-345 Criteo collate, :1099-1157 random bags):
+      * ``indices``: list of T int64 tensors (ragged) or an int64 tensor [T, L];
+      * ``offsets``: list of T int64 tensors [B] or an int64 tensor [T, B].
+    Offsets are nn.EmbeddingBag offsets (bag b = [off[b], off[b+1]), last bag ends at L_t).
+    """
+
+    def __init__(self, indices, offsets, device: torch.device | str | None = None):
+        if isinstance(indices, torch.Tensor):
+            if indices.dim() != 2:
+                raise ValueError("stacked indices must be [T, L]")
+            T = indices.shape[0]
+            lens = [indices.shape[1]] * T
+            idx = indices.reshape(-1)
+        else:
+            T = len(indices)
+            lens = [int(x.numel()) for x in indices]
+            idx = torch.cat([x.reshape(-1) for x in indices]) if T else torch.empty(0, dtype=torch.int64)
+        if isinstance(offsets, torch.Tensor):
+            if offsets.dim() != 2 or offsets.shape[0] != T:
+                raise ValueError("stacked offsets must be [T, B]")
+            off = offsets
+        else:
+            if len(offsets) != T:
+                raise ValueError("need one offsets tensor per table")
+            B0 = int(offsets[0].numel()) if T else 0
+            if any(int(o.numel()) != B0 for o in offsets):
+                raise ValueError("all tables must have the same number of bags")
+            off = torch.stack([o.reshape(-1) for o in offsets]) if T else torch.empty(0, 0, dtype=torch.int64)
+        dev = torch.device(device) if device is not None else idx.device
+        self.num_tables = T
+        self.num_bags = int(off.shape[1]) if T else 0
+        self.lookups = lens
+        self.max_lookups = max(lens) if lens else 0
+        base = [0]
+        for n in lens:
+            base.append(base[-1] + n)
+        self.idx_base_host = base
+        self.idx = idx.to(device=dev, dtype=torch.int64).contiguous()
+        self.off = off.to(device=dev, dtype=torch.int64).contiguous()
+        self.idx_base = torch.tensor(base, dtype=torch.int64, device=dev)
+        self._c = L.Batch(
+            _ptr(self.idx), _ptr(self.off), _ptr(self.idx_base), self.num_bags, self.max_lookups
+        )
+
+    @property
+    def c(self) -> L.Batch:
+        return self._c
+
+    @classmethod
+    def pooling_one(cls, indices: torch.Tensor) -> "LookupBatch":
+        """Criteo form: one index per (table, sample); offsets = arange(B) per table."""
+        T, B = indices.shape
+        off = torch.arange(B, dtype=torch.int64, device=indices.device).expand(T, B)
+        return cls(indices, off.contiguous())
+
+
+class EmbeddingTableSet:
+    """T embedding tables of dim D resident in one set of HBM slabs."""
+
+    def __init__(
+        self,
+        num_rows: Sequence[int],
+        dim: int,
+        device: torch.device | str = "cuda",
+        packed: bool = False,
+        init: str | None = "uniform",
+        seed: int = 123,
+        weights: Sequence[torch.Tensor] | None = None,
+    ):
+        self.lib = L.load()
+        self.num_rows = [int(n) for n in num_rows]
+        self.T = len(self.num_rows)
+        self.D = int(dim)
+        if self.T <= 0 or self.T > 256:
+            raise ValueError("1..256 tables supported")
+        if self.D < 4 or self.D > 256 or self.D % 4 or (self.D // 4) & (self.D // 4 - 1):
+            raise ValueError("embedding dim must be 4*2^k <= 256")
+        self.device = torch.device(device)
+        T, D = self.T, self.D
+        self.row_base = [0]
+        for n in self.num_rows[:-1]:
+            self.row_base.append(self.row_base[-1] + n)
+        nblk = [_ceil_div(n, L.DQRM_BLOCK_ROWS) for n in self.num_rows]
+        nsblk = [_ceil_div(b, L.DQRM_SBLOCK_ROWS // L.DQRM_BLOCK_ROWS) for b in nblk]
+        self.blk_base = [0]
+        for b in nblk[:-1]:
+            self.blk_base.append(self.blk_base[-1] + b)
+        self.sblk_base = [0]
+        for b in nsblk[:-1]:
+            self.sblk_base.append(self.sblk_base[-1] + b)
+        self.R = sum(self.num_rows)
+        NB, NS = sum(nblk), sum(nsblk)
+        dev = self.device
+        f32 = torch.float32
+        self.W = torch.empty(self.R, D, dtype=f32, device=dev)
+        self.packed = torch.empty(self.R, D // 2, dtype=torch.uint8, device=dev) if packed else None
+        self.rowmax = torch.zeros(self.R, dtype=f32, device=dev)
+        self.blkmax = torch.zeros(NB, dtype=f32, device=dev)
+        self.sblkmax = torch.zeros(NS, dtype=f32, device=dev)
+        self.tmax = torch.zeros(T, dtype=f32, device=dev)
+        self.scale = torch.zeros(T, dtype=f32, device=dev)
+        self.pscale = torch.full((T,), float("nan"), dtype=f32, device=dev)
+        self.meta = torch.tensor(
+            [self.row_base, self.num_rows, self.blk_base, self.sblk_base], dtype=torch.int64, device=dev
+        ).contiguous()
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tflags = torch.zeros(T, dtype=torch.int32, device=dev)
+        self._c = L.TableSet(
+            T, D, self.R, NB, NS,
+            _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
+            _ptr(self.tmax), _ptr(self.scale), _ptr(self.pscale), _ptr(self.meta), _ptr(self.err),
+            _ptr(self.tflags),
+        )
+        if weights is not None:
+            if len(weights) != T:
+                raise ValueError("one weight tensor per table")
+            for t, w in enumerate(weights):
+                self.table_weight(t).copy_(w.to(device=dev, dtype=f32))
+        elif init == "uniform":
+            L.check(self.lib.dqrm_init_uniform(C.byref(self._c), seed, _stream_handle()), "dqrm_init_uniform")
+        self.refresh_absmax()
+
+    # ------------------------------------------------------------------ views / state
+    @property
+    def c(self) -> L.TableSet:
+        return self._c
+
+    def table_weight(self, t: int) -> torch.Tensor:
+        b = self.row_base[t]
+        return self.W[b : b + self.num_rows[t]]
+
+    def table_packed(self, t: int) -> torch.Tensor:
+        b = self.row_base[t]
+        return self.packed[b : b + self.num_rows[t]]
+
+    # ------------------------------------------------------------------ maintenance
+    def refresh_absmax(self) -> None:
+        """Recompute the |W| max hierarchy from W (after any external write to W)."""
+        L.check(self.lib.dqrm_refresh_absmax(C.byref(self._c), _stream_handle()), "dqrm_refresh_absmax")
+
+    def refresh_scale_and_pack(self, bits: int = 4) -> None:
+        L.check(
+            self.lib.dqrm_refresh_scale_and_pack(C.byref(self._c), bits, _stream_handle()),
+            "dqrm_refresh_scale_and_pack",
+        )
+
+    def read_errors(self, clear: bool = True) -> int:
+        f = C.c_uint32(0)
+        L.check(self.lib.dqrm_read_errors(C.byref(self._c), C.byref(f), int(clear), _stream_handle()),
+                "dqrm_read_errors")
+        return int(f.value)
+
+    # ------------------------------------------------------------------ forward
+    def forward(
+        self,
+        batch: LookupBatch,
+        bits: int = 4,
+        refresh_scale: bool = True,
+        use_packed: bool = False,
+        full_precision: bool = False,
+        out: torch.Tensor | None = None,
+        layout: str = "tbd",
+    ) -> torch.Tensor:
+        """Fused T-table fake-quant EmbeddingBag (q_m_n_q_g.py:317-398 for every table).
+
+        layout "tbd" -> out [T, B, D]; "btd" -> out [B, T, D] (DLRM interaction order).
+        """
+        if batch.num_tables != self.T:
+            raise ValueError("batch has %d tables, set has %d" % (batch.num_tables, self.T))
+        B, T, D = batch.num_bags, self.T, self.D
+        if out is None:
+            shape = (T, B, D) if layout == "tbd" else (B, T, D)
+            out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        if layout == "tbd":
+            st, sb = B * D, D
+        else:
+            st, sb = D, T * D
+        flags = 0
+        if refresh_scale:
+            flags |= L.DQRM_FWD_REFRESH_SCALE
+        if use_packed:
+            flags |= L.DQRM_FWD_USE_PACKED
+        if full_precision:
+            flags |= L.DQRM_FWD_FULL_PRECISION
+        if layout != "tbd":
+            flags |= L.DQRM_FWD_BAG_MAJOR
+        L.check(
+            self.lib.dqrm_emb_fwd(C.byref(self._c), C.byref(batch.c), bits, flags, _ptr(out), st, sb,
+                                  _stream_handle()),
+            "dqrm_emb_fwd",
+        )
+        return out
+
+    # ------------------------------------------------------------------ backward
+    @staticmethod
+    def _dy_strides(dy: torch.Tensor, layout: str, T: int, B: int, D: int) -> tuple[int, int]:
+        if dy.stride(-1) != 1:
+            raise ValueError("dy must be contiguous in D")
+        if layout == "tbd":
+            if tuple(dy.shape) != (T, B, D):
+                raise ValueError("dy must be [T, B, D]")
+            return dy.stride(0), dy.stride(1)
+        if tuple(dy.shape) != (B, T, D):
+            raise ValueError("dy must be [B, T, D]")
+        return dy.stride(1), dy.stride(0)
+
+    def backward_sgd(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
+                     repack: bool = False, layout: str = "tbd") -> None:
+        """Fused STE + sparse backward + SGD (torch.optim.SGD semantics, in lookup order)."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_sgd(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
+                                      float(lr), 4 if repack else 0, _stream_handle()),
+            "dqrm_emb_bwd_sgd",
+        )
+
+    def backward_coalesce(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad",
+                          ste: bool = True, grad_bits: int = 8, layout: str = "tbd") -> None:
+        """STE + sparse backward + coalesce + local grad scale (s_q_g_p_c.py:850-861)."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_coalesce(
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.cap_base),
+                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.counts), _ptr(ws.s_loc), grad_bits,
+                _stream_handle()),
+            "dqrm_emb_bwd_coalesce",
+        )
+
+
+@dataclass
+class CoalescedGrad:
+    """Fixed-capacity coalesced sparse gradient of all tables (one rank)."""
+
+    caps: list[int]
+    cap_base: torch.Tensor   # i64 [T+1]
+    rows: torch.Tensor       # i32 [CAP]
+    vals: torch.Tensor       # f32 [CAP, D]
+    counts: torch.Tensor     # i32 [T]
+    s_loc: torch.Tensor      # f32 [T]
+
+    @classmethod
+    def allocate(cls, caps: Sequence[int], dim: int, device) -> "CoalescedGrad":
+        caps = [int(c) for c in caps]
+        base = [0]
+        for c in caps:
+            base.append(base[-1] + c)
+        CAP = base[-1]
+        return cls(
+            caps=caps,
+            cap_base=torch.tensor(base, dtype=torch.int64, device=device),
+            rows=torch.zeros(max(CAP, 1), dtype=torch.int32, device=device),
+            vals=torch.zeros(max(CAP, 1), dim, dtype=torch.float32, device=device),
+            counts=torch.zeros(len(caps), dtype=torch.int32, device=device),
+            s_loc=torch.zeros(len(caps), dtype=torch.float32, device=device),
+        )
+
+    @property
+    def cap_total(self) -> int:
+        return sum(self.caps)
+
+
+def default_caps(num_rows: Sequence[int], max_lookups: int) -> list[int]:
+    """cap_t = min(max lookups per table, n_t): the most unique rows a table can touch."""
+    return [min(int(max_lookups), int(n)) for n in num_rows]
+
+
+def reference_scale(absmax: float, bits: int) -> float:
+    """clamp(absmax, 1e-8) / (2^(bits-1)-1) in f32 (quant_utils.py:189-192), host helper."""
+    import numpy as np
+
+    a = np.float32(absmax)
+    a = max(a, np.float32(1e-8))
+    return float(np.float32(a) / np.float32(2 ** (bits - 1) - 1))
+
+
+__all__ = ["LookupBatch", "EmbeddingTableSet", "CoalescedGrad", "default_caps", "reference_scale"]

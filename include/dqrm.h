@@ -1,0 +1,216 @@
+/*
+ * dqrm.h — C ABI of libdqrm, the MI355X-native (gfx950 / CDNA4) implementation of
+ * DQRM's data-parallel QAT step for embedding tables.
+ *
+ * Reference: YangZhou08/Deep_Quantized_Recommendation_Model_DQRM @ 2024-10-24.
+ * Each entry point below names the reference interface it replaces (file:line).
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes, enums. No torch types. Every device pointer is a HIP
+ *    device allocation owned by the caller; the library never allocates or frees
+ *    caller memory and keeps no global device state.
+ *  - Every call is stream-ordered on the hipStream_t passed as `void* stream`
+ *    (NULL = the legacy default stream). No call synchronises the host except
+ *    dqrm_read_errors().
+ *  - Every call returns an int status: 0 = ok, <0 = error (see DQRM_E_*). The message
+ *    of the last failing call on the calling thread is returned by dqrm_last_error().
+ *    No C++ exception crosses the ABI.
+ *  - Shapes: T tables, D = embedding dim (same for all tables, D % 4 == 0, D <= 256),
+ *    B = bags per table per call, L_t = lookups of table t.
+ *
+ * Resident table state (one "table set" = all T tables of a model, one slab each):
+ *    W        f32 [R][D]            FP32 master rows, table t = rows [row_base[t], +num_rows[t])
+ *    packed   u8  [R][D/2]          INT4 rows, offset-binary nibbles (q+8), element 2j in the
+ *                                   low nibble of byte j (FBGEMM/torch 4-bit rowwise order);
+ *                                   nullable when the packed path is unused
+ *    rowmax   f32 [R]               max_d |W[r][d]|
+ *    blkmax   f32 [NB]              max of rowmax over 256-row blocks   (blk_base[t] per table)
+ *    sblkmax  f32 [NS]              max of blkmax over 256-block (65536-row) superblocks
+ *    tmax     f32 [T]               max of sblkmax over the table = max |W_t|
+ *    scale    f32 [T]               embedding scale s_t used by the latest forward
+ *    pscale   f32 [T]               scale the packed rows were built with (NaN = never)
+ *    meta     i64 [4][T]            row_base, num_rows, blk_base, sblk_base (device copy)
+ *
+ *  The max hierarchy makes the reference's per-step full-table min/max
+ *  (quant_utils.py:177-178, called every training forward at
+ *  quant_modules_not_quantize_grad.py:337) exact and O(touched rows).
+ */
+#ifndef DQRM_H_
+#define DQRM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQRM_ABI_VERSION 1
+
+/* status codes */
+#define DQRM_OK            0
+#define DQRM_E_INVALID    -1   /* bad argument (shape, null pointer, unsupported bits) */
+#define DQRM_E_HIP        -2   /* HIP runtime error */
+#define DQRM_E_CAPACITY   -3   /* per-table work exceeds this build's on-chip capacity */
+#define DQRM_E_WORKSPACE  -4   /* workspace too small */
+
+/* device-side error flags accumulated in dqrm_table_set.err (read with dqrm_read_errors) */
+#define DQRM_ERRF_INDEX    1u  /* an index was outside [0, num_rows[t]) (reference: IndexError) */
+#define DQRM_ERRF_OFFSET   2u  /* offsets not non-decreasing / outside [0, L_t] */
+#define DQRM_ERRF_OVERFLOW 4u  /* a coalesced/merged per-table count exceeded its capacity */
+
+#define DQRM_BLOCK_ROWS   256     /* rows per blkmax entry */
+#define DQRM_SBLOCK_ROWS  65536   /* rows per sblkmax entry */
+
+/* Resident state of T tables. All pointers are device pointers. */
+typedef struct dqrm_table_set {
+    int32_t  num_tables;      /* T */
+    int32_t  dim;             /* D */
+    int64_t  total_rows;      /* R = sum num_rows */
+    int64_t  total_blocks;    /* NB */
+    int64_t  total_sblocks;   /* NS */
+    float*   W;
+    uint8_t* packed;          /* nullable */
+    float*   rowmax;
+    float*   blkmax;
+    float*   sblkmax;
+    float*   tmax;
+    float*   scale;
+    float*   pscale;
+    const int64_t* meta;      /* [4][T]: row_base, num_rows, blk_base, sblk_base */
+    uint32_t* err;            /* 1 word, device-side error flags */
+    uint32_t* tflags;         /* [T] scratch (repack decision), library-internal */
+} dqrm_table_set;
+
+/* A batch of lookups for all T tables, in the reference's per-table
+ * (lS_i[t], lS_o[t]) form (dlrm_data_pytorch.py:328-345, 1099-1157), concatenated:
+ *   idx      i64 [sum_t L_t]  table t's indices at [idx_base[t], idx_base[t+1])
+ *   off      i64 [T][B]       bag b of table t = idx_base[t] + [off[t][b], off[t][b+1])
+ *                             (last bag ends at L_t), exactly nn.EmbeddingBag offsets
+ *   idx_base i64 [T+1]        device copy */
+typedef struct dqrm_batch {
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    int64_t  num_bags;        /* B */
+    int64_t  max_lookups;     /* host upper bound on any L_t (capacity planning) */
+} dqrm_batch;
+
+/* forward flags */
+#define DQRM_FWD_REFRESH_SCALE 1u  /* s_t = clamp(tmax_t, 1e-8)/(2^(bits-1)-1), write scale[] */
+#define DQRM_FWD_USE_PACKED    2u  /* single-lookup bags read INT4 rows (valid iff pscale==scale) */
+#define DQRM_FWD_FULL_PRECISION 4u /* full_precision_flag: plain FP32 sum, no fake-quant */
+#define DQRM_FWD_BAG_MAJOR     8u  /* iterate bags b-major (output [B][T][D]) for coalescing */
+
+/* ---------------------------------------------------------------------------------
+ * Table maintenance
+ * ------------------------------------------------------------------------------ */
+
+/* Full recompute of rowmax/blkmax/sblkmax/tmax from W (first forward, after
+ * load_state_dict, after weight_syncc). Replaces the full-table scan of
+ * quant_utils.py:141-194 (symmetric_linear_quantization_param_two). */
+int dqrm_refresh_absmax(const dqrm_table_set* set, void* stream);
+
+/* Periodic scale refresh + conditional repack (the stringified periodic-update path
+ * quant_modules_not_quantize_grad.py:303-315,331-363). For each table:
+ *   s_t = clamp(tmax_t, 1e-8) / (2^(bits-1)-1)   -> scale[t]
+ *   if packed != NULL and pscale[t] != s_t: repack every row of t with s_t, pscale[t] = s_t.
+ * Device-side decision; no host sync. bits must be 4 for repacking. */
+int dqrm_refresh_scale_and_pack(const dqrm_table_set* set, int bits, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Forward: fused multi-table INT4 fake-quant EmbeddingBag
+ * Replaces QuantEmbeddingBagTwo.forward (quant_modules_not_quantize_grad.py:317-398)
+ * called once per table by DLRM_Net.apply_emb (dlrm_s_pytorch_single_gpu.py:609-674):
+ *   out = embedding_bag(idx, off, mode="sum")              (:367)
+ *   q   = clamp(round(1/s * out + 0), -2^(b-1), 2^(b-1)-1)  (quant_utils.py:101,343)
+ *   y   = q * s                                             (:393)
+ * out[t][b][d] is written at out + t*out_stride_t + b*out_stride_b + d (floats).
+ * Bags with one lookup may be served from the INT4 packed rows (bit-identical values
+ * when pscale == scale); every other bag is summed in FP32 in bag order.
+ * ------------------------------------------------------------------------------ */
+int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits,
+                 uint32_t flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                 void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Single-GPU backward + SGD, fused (no sparse gradient materialised).
+ * Replaces: SymmetricQuantFunction.backward (quant_utils.py:349-363) + autograd of q*s,
+ * EmbeddingBag sparse backward, and torch.optim.SGD.step on the sparse grad
+ * (dlrm_s_pytorch_single_gpu.py:1736-1750,1943-1950). Per lookup i of row r, in lookup
+ * order:  g' = (dy[bag(i)] * s) / s ;  W[r] = fma(g', -lr, W[r])   (torch CPU order).
+ * ste = 0 skips the (g*s)/s step (forward ran with full_precision_flag).
+ * Then rowmax/blkmax/sblkmax/tmax of touched rows, and (if packed != NULL and
+ * repack_bits == 4) the touched INT4 rows with pscale.
+ * ------------------------------------------------------------------------------ */
+int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
+                     const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
+                     int ste, float lr, int repack_bits, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Data-parallel gradient path (sgd_quantized_gradients_parallel_comm.py)
+ *
+ * Coalesced-gradient buffer (per rank), fixed capacity per table:
+ *   cap_base i64 [T+1] (device)  table t owns entries [cap_base[t], cap_base[t+1])
+ *   rows     i32 [CAP]           ascending unique local row ids
+ *   vals     f32 [CAP][D]        coalesced sums
+ *   counts   i32 [T]             U_t
+ * ------------------------------------------------------------------------------ */
+
+/* STE backward + EmbeddingBag sparse backward + grad.coalesce() (s_q_g_p_c.py:859) +
+ * local scale s_loc[t] = clamp(max|vals_t|, 1e-8) / (2^(grad_bits-1)-1) (:861,
+ * quant_utils.py:141-194). grad_bits = 0 skips the scale (FP32 gradient path). */
+int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
+                          const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
+                          int ste, const int64_t* cap_base, int32_t* rows, float* vals,
+                          int32_t* counts, float* s_loc, int grad_bits, void* stream);
+
+/* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
+ *   [counts i32 T | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
+ *   int8 (bits<=8) / int16 (bits<=16) / f32 (bits==32, unquantized path)]        */
+size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits);
+
+/* Scale average + quantize-pack (s_q_g_p_c.py:863-869):
+ *   s[t] = (((s_all[N-1][t] + s_all[N-2][t]) + ...) + s_all[0][t]) * (1/N)
+ *          (Gloo's one-element allreduce order; identical on every rank; -> s_avg)
+ *                                                                [bits 2..16 only]
+ *   q    = clamp(round(1/s * v + 0), -2^(bits-1), 2^(bits-1)-1)  (quant_utils.py:101,343)
+ * grad_bits = 32 copies FP32 values (emb_grad_quantized=False path, :319-327). */
+int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* cap_base, int64_t cap_total,
+                         const int32_t* rows, const float* vals, const int32_t* counts,
+                         const float* s_all, int num_ranks, int grad_bits,
+                         float* s_avg, void* payload, void* stream);
+
+/* update modes for dqrm_apply_sparse_update */
+#define DQRM_UPD_DP        0  /* v = ((Q * (1/N)) * s) ; W += -lr * v   (s_q_g_p_c.py:885,618-622) */
+#define DQRM_UPD_SIMULATED 1  /* v = Q * f32((double)s / N) ; W += -lr * v (sgd_quantized_gradients.py:366-371) */
+#define DQRM_UPD_FP32      2  /* v = (sum_r vals_r) * (1/N); W += -lr * v   (s_q_g_p_c.py:319-327,626) */
+
+/* Decode N gathered payloads (contiguous, payload_bytes apart), union rows, integer
+ * (or rank-ordered FP32) sum, dequantize and apply SGD to W; then maintain
+ * rowmax/blkmax/sblkmax/tmax and (packed != NULL && repack_bits == 4) packed rows.
+ * Replaces Gloo sparse all_reduce's coalesce (s_q_g_p_c.py:878) +
+ * weight_update_parallel_comm (:601-628). */
+int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
+                             int64_t cap_total, const void* payloads, size_t payload_bytes,
+                             int num_ranks, int grad_bits, const float* s_avg, float lr,
+                             int mode, int repack_bits, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Misc
+ * ------------------------------------------------------------------------------ */
+/* Synthetic on-device init U(-sqrt(1/n_t), +sqrt(1/n_t)) from a counter-based hash
+ * (same distribution as quant_modules_not_quantize_grad.py:273-275; not numpy's stream). */
+int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream);
+
+/* Synchronises `stream`, returns the accumulated DQRM_ERRF_* flags in *flags and
+ * clears them (if clear != 0). */
+int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream);
+
+const char* dqrm_last_error(void);
+int dqrm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DQRM_H_ */

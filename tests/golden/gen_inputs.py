@@ -1,0 +1,87 @@
+"""Deterministic input generators shared by make_golden.py and the tests.
+
+Inputs are regenerated from seeds (numpy's legacy RandomState / MT19937, whose stream is
+stable across numpy versions); fixtures store the expected outputs plus a checksum of the
+generated inputs so drift in a generator is caught.
+
+Distributions follow the reference:
+  table init   U(-sqrt(1/n), +sqrt(1/n))     quant_modules_not_quantize_grad.py:273-275
+  random bags  generate_dist_input_batch     dlrm_data_pytorch.py:1099-1157 ("uniform")
+  Criteo form  one index per (table, sample), offsets = arange(B)   dlrm_data_pytorch.py:328-345
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194, 27,
+               14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572]
+# reference TB profile at --max-ind-range=10M (python_profiling_script/finding_kaggle_compression_ratio.py:5)
+TERABYTE_ROWS = [9980200, 26095, 17224, 7383, 20152, 3, 7112, 1435, 62, 9756762, 1332128, 314263, 10, 2208,
+                 11168, 122, 4, 971, 14, 9994101, 7267918, 9946670, 415284, 12422, 102, 36]
+
+
+def table_weights(num_rows, dim, seed):
+    out = []
+    for t, n in enumerate(num_rows):
+        rs = np.random.RandomState(seed + 1000 * t)
+        b = np.sqrt(1.0 / n)
+        out.append(rs.uniform(low=-b, high=b, size=(n, dim)).astype(np.float32))
+    return out
+
+
+def random_bags(num_rows, B, seed, num_indices_per_lookup=10, fixed=False):
+    """Per table: (idx int64 [L_t], off int64 [B]) with unique sorted indices per bag."""
+    rs = np.random.RandomState(seed)
+    idxs, offs = [], []
+    for size in num_rows:
+        off, ind, o = [], [], 0
+        for _ in range(B):
+            if fixed:
+                g = np.int64(num_indices_per_lookup)
+            else:
+                r = rs.random_sample(1)
+                g = np.int64(np.round(max([1.0], r[0] * min(size, num_indices_per_lookup))))
+            r = rs.random_sample(int(g))
+            grp = np.unique(np.round(r * (size - 1)).astype(np.int64))
+            off.append(o)
+            ind.extend(grp.tolist())
+            o += grp.size
+        idxs.append(np.asarray(ind, dtype=np.int64))
+        offs.append(np.asarray(off, dtype=np.int64))
+    return idxs, offs
+
+
+def pooling_one(num_rows, B, seed, dist="uniform", alpha=1.05):
+    """[T, B] int64 Criteo-form indices (one lookup per sample and table)."""
+    rs = np.random.RandomState(seed)
+    out = np.empty((len(num_rows), B), dtype=np.int64)
+    for t, n in enumerate(num_rows):
+        if dist == "uniform":
+            out[t] = rs.randint(0, n, size=B)
+        elif dist == "zipf":
+            z = rs.zipf(alpha, size=B) - 1
+            out[t] = np.minimum(z, n - 1)
+        else:
+            raise ValueError(dist)
+    return out
+
+
+def upstream_grad(T, B, D, seed, scale=0.05):
+    rs = np.random.RandomState(seed)
+    return (rs.standard_normal((T, B, D)) * scale).astype(np.float32)
+
+
+def checksum(*arrays) -> str:
+    h = hashlib.sha256()
+
+    def feed(a):
+        if isinstance(a, (list, tuple)):
+            for x in a:
+                feed(x)
+        else:
+            h.update(np.ascontiguousarray(a).tobytes())
+
+    feed(arrays)
+    return h.hexdigest()[:16]
