@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Benchmark: DQRM data-parallel QAT embedding step on MI355X (1..8 GPUs, one process each).
+
+A step = one pass of the hot path over one synthetic batch per rank:
+  forward   26-table fake-quant EmbeddingBag (exact per-step table scale, FP32-row gather)
+  backward  STE + sparse backward + coalesce + local INT8 grad scale        (K4)
+  comm      RCCL all-gather of the [T] scales, quantize-pack to INT8       (K5)
+            RCCL all-gather of the fixed-capacity {rows, int8} payloads
+  update    decode all ranks' payloads, integer union-sum, dequant, SGD    (K6)
+The MLP/interaction layers are outside the north-star path and are not run;
+the upstream gradient dL/dy is a fixed synthetic tensor.
+
+Prints ONE JSON line (rank 0). N=1 by default; N>1 is launched by torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+import deep_quantized_recommendation_model_dqrm_amd as dq  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd import _lib as L  # noqa: E402
+import gen_inputs as G  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # BASELINE.json configs[4]: Criteo-Terabyte shape, D=64, ~773M rows: the reference TB
+    # profile (--max-ind-range=10M) with its six >=1M-row tables scaled x16
+    "terabyte": dict(rows=[n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS], dim=64),
+    # the reference's actual TB run (49.1M rows)
+    "terabyte_ref": dict(rows=G.TERABYTE_ROWS, dim=64),
+    # BASELINE.json configs[2-3]: Criteo-Kaggle, D=16
+    "kaggle": dict(rows=G.KAGGLE_ROWS, dim=16),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="terabyte", choices=sorted(CONFIGS))
+    p.add_argument("--batch-per-gpu", type=int, default=2048,
+                   help="samples per rank per step (reference TB mini-batch 2048)")
+    p.add_argument("--grad-bits", type=int, default=8)
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--index-dist", default="uniform", choices=["uniform", "zipf"])
+    p.add_argument("--num-batches", type=int, default=8, help="distinct resident batches cycled")
+    p.add_argument("--gather-batch", type=int, default=65536,
+                   help="bags per table for the INT4 packed-gather bandwidth phase (0 = skip)")
+    p.add_argument("--gather-iters", type=int, default=50)
+    p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--seed", type=int, default=123)
+    return p.parse_args()
+
+
+def make_batches(rows, B_global, rank, world, count, seed, dist_kind, device):
+    """Global Criteo-form batches [T, B_global] generated identically on every rank, each
+    rank keeping its contiguous slice (get_my_slice, dlrm_s_pytorch_single_gpu.py:989-993)."""
+    g = torch.Generator(device=device)
+    out = []
+    sl = dq.get_my_slice(B_global, world, rank)
+    for k in range(count):
+        g.manual_seed(seed * 1000 + k)
+        cols = []
+        for n in rows:
+            if dist_kind == "uniform":
+                cols.append(torch.randint(0, n, (B_global,), generator=g, device=device, dtype=torch.int64))
+            else:  # Zipf(1.05)-like power law via inverse transform on a log scale
+                u = torch.rand(B_global, generator=g, device=device, dtype=torch.float64)
+                z = torch.floor(torch.exp(u * np.log(float(n)))) - 1
+                cols.append(z.clamp_(0, n - 1).to(torch.int64))
+        P = torch.stack(cols)[:, sl].contiguous()
+        out.append(dq.LookupBatch.pooling_one(P))
+    return out
+
+
+def timed_events(n):
+    return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            print("N>1 must be launched with torch.distributed.run", file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = CONFIGS[a.config]
+    rows, D, B = cfg["rows"], cfg["dim"], a.batch_per_gpu
+    T = len(rows)
+
+    t0 = time.time()
+    ts = dq.EmbeddingTableSet(rows, D, device=dev, packed=a.gather_batch > 0, init="uniform", seed=a.seed)
+    batches = make_batches(rows, B * world, rank, world, a.num_batches, a.seed, a.index_dist, dev)
+    dy = torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + rank)) * 0.05
+    y = torch.empty(T, B, D, device=dev)
+    ex = dq.SparseGradExchange.for_batch_shape(ts, B, grad_bits=a.grad_bits)
+    kern = ex.kernels
+    torch.cuda.synchronize()
+    setup_s = time.time() - t0
+
+    def step(i, ev=None):
+        b = batches[i % len(batches)]
+        if ev is not None:
+            ev[0][0].record()
+        ts.forward(b, bits=4, refresh_scale=True, out=y)
+        if ev is not None:
+            ev[0][1].record()
+            ev[1][0].record()
+        kern.coalesce(b, dy, ex.ws, True, a.grad_bits, "tbd")
+        if ev is not None:
+            ev[1][1].record()
+        ex._all_gather(ex.s_all, ex.ws.s_loc)
+        if ev is not None:
+            ev[2][0].record()
+        kern.quant_pack(ex.ws, ex.s_all, ex.world, a.grad_bits, ex.s_avg, ex.payload)
+        if ev is not None:
+            ev[2][1].record()
+        if ex.world == 1:
+            gathered = ex.payload.view(1, -1)
+        else:
+            ex._all_gather(ex.gathered, ex.payload)
+            gathered = ex.gathered
+        if ev is not None:
+            ev[3][0].record()
+        kern.apply(ex.ws, gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg, a.lr, L.DQRM_UPD_DP, False)
+        if ev is not None:
+            ev[3][1].record()
+
+    for i in range(a.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [timed_events(4) for _ in range(a.steps)]
+    t_start = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i, evs[i])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
+    kms = {n: float(np.mean([evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(a.steps)])) for j, n in enumerate(names)}
+
+    # algorithmic bytes per launch; unique counts from the last step
+    U = int(ex.ws.counts.sum().item())
+    L_tot = T * B
+    alg = {
+        "emb_fwd": L_tot * (D * 4 + 8) + T * B * 8 + T * B * D * 4 + T * 4,
+        "bwd_coalesce": L_tot * 8 + T * B * 8 + L_tot * D * 4 + U * (D * 4 + 4),
+        "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
+        "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4,
+    }
+    dom = max(kms, key=kms.get)
+    achieved = alg[dom] / (kms[dom] * 1e-3) / 1e9
+    err = ts.read_errors()
+
+    # INT4 packed-gather bandwidth phase (north-star gather metric), outside the timed step
+    gather = None
+    if a.gather_batch > 0:
+        ts.refresh_scale_and_pack(4)
+        Bg = a.gather_batch
+        gb = make_batches(rows, Bg, 0, 1, 2, a.seed + 7, a.index_dist, dev)
+        yg = torch.empty(T, Bg, D, device=dev)
+        for i in range(5):
+            ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
+        gev = timed_events(a.gather_iters)
+        for i in range(a.gather_iters):
+            gev[i][0].record()
+            ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
+            gev[i][1].record()
+        torch.cuda.synchronize()
+        g_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in gev]))
+        g_bytes = T * Bg * (D // 2 + 8 + 8 + D * 4) + T * 4
+        g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
+        gather = {"kernel": "k_emb_fwd (INT4 packed, pooling 1)", "bags_per_table": Bg, "ms": round(g_ms, 4),
+                  "alg_bytes": g_bytes, "GBps": round(g_gbs, 1), "frac_of_peak": round(g_gbs / HBM_PEAK_GBS, 4),
+                  "bytes_per_lookup": D // 2 + 8 + 8 + D * 4}
+        del yg, gb
+
+    cpu = None
+    if rank == 0 and a.cpu_baseline:
+        cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
+
+    if rank == 0:
+        value = world * B * a.steps / elapsed
+        line = {
+            "metric": "QAT-step samples/sec (DP embedding QAT step: INT4 fake-quant gather + sparse SGD + INT8 sparse-grad all-reduce)",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (int4 fake-quant activations, int8 gradients)",
+            "data": "synthetic (uniform-random Criteo-form indices, U(+-sqrt(1/n)) tables, N(0,0.05) dL/dy)"
+            if a.index_dist == "uniform" else "synthetic (power-law indices)",
+            "config": {
+                "workload": f"criteo-{a.config} embedding QAT step",
+                "tables": T, "total_rows": sum(rows), "emb_dim": D,
+                "batch_per_gpu": B, "global_batch": B * world, "pooling": 1,
+                "grad_bits": a.grad_bits, "scale_period": 1, "parallelism": f"dp{world} (tables replicated)",
+            },
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": round(kms[dom], 5)},
+            "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+            "int4_gather": gather,
+            "cpu_baseline": cpu,
+            "device_errors": err,
+            "setup_s": round(setup_s, 1),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(rows, D, B, seed):
+    """The oracle (C restatement of the reference path, single thread) on a bounded sample:
+    tables capped at 1M rows (host RAM), a few full QAT steps incl. the reference's per-step
+    full-table |W| scan. kind = "port" (the reference itself cannot run here)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    O.build()
+    cap_rows = [min(n, 1_000_000) for n in rows]
+    rs = np.random.RandomState(seed)
+    Ws = [rs.uniform(-np.sqrt(1 / n), np.sqrt(1 / n), (n, D)).astype(np.float32) for n in cap_rows]
+    T = len(rows)
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        P = np.stack([rs.randint(0, n, B) for n in cap_rows]).astype(np.int64)
+        dyc = (rs.standard_normal((T, B, D)) * 0.05).astype(np.float32)
+        s_fwd = []
+        for t in range(T):
+            s = O.table_scale(Ws[t], 4)
+            O.emb_fwd(Ws[t], P[t], np.arange(B), s)
+            s_fwd.append(s)
+        O.dp_step(Ws, [[(P[t], np.arange(B)) for t in range(T)]], [[dyc[t] for t in range(T)]], s_fwd, 0.1, 8)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el > 10.0 or steps >= 50:
+            break
+    return {"value": round(steps * B / el, 1), "unit": "samples/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} QAT steps, B={B}, {T} tables capped at 1M rows (D={D}), oracle C restatement, 1 thread"}
+
+
+if __name__ == "__main__":
+    main()

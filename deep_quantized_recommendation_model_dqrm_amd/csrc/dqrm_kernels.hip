@@ -419,6 +419,8 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
 // keys = (local_row << 32) | tag sorted in LDS (bitonic), segments = equal rows.
 // ------------------------------------------------------------------------------------
 DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
+DQRM_INLINE uint32_t key_lo(uint64_t k) { return (uint32_t)k; }
+DQRM_INLINE uint64_t with_lo(uint64_t k, uint32_t lo) { return (k & 0xFFFFFFFF00000000ull) | lo; }
 
 DQRM_INLINE void bitonic_sort_lds(uint64_t* keys, int n_pow2) {
     for (int k = 2; k <= n_pow2; k <<= 1) {
@@ -453,7 +455,6 @@ DQRM_INLINE int head_scan(const uint64_t* keys, int n, int* s_base, int* s_wtot)
         int i = i0 + c;
         if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
     }
-    // inclusive wave scan
     int v = cnt;
     const int lane = tid % WAVE, w = tid / WAVE;
 #pragma unroll
@@ -483,59 +484,240 @@ DQRM_INLINE int head_ordinal(const uint64_t* keys, const int* s_base, int i) {
     return u;
 }
 
-// maintain blkmax/sblkmax/tmax of table t after rows of sorted `keys` changed rowmax.
-DQRM_INLINE void maintain_hierarchy(const Meta& m, int t, const uint64_t* keys, int n,
+// ------------------------------------------------------------------------------------
+// Segment reduction in exact sequential order.
+// A segment = the sorted keys of one row; its entries must be combined strictly in key
+// order (ascending lookup position / rank) to reproduce the reference's rounding:
+//   OP_FMA  acc = fma(v, -lr, acc) per entry          (torch CPU sparse SGD axpy)
+//   OP_SUM  acc = v0; acc = acc + v_k                  (coalesce / sparse all_reduce)
+// Short segments: one lane group (LPR lanes x float4), 4 entries in flight per chunk.
+// Long segments (> LONG_SEG entries, tiny hot tables): a whole wave loads WAVE/LPR entries
+// per chunk (next chunk prefetched) and combines them in order through shuffles.
+// Masked entries load the head's own row, so they never address out of bounds and cost
+// no extra memory traffic.
+// ------------------------------------------------------------------------------------
+constexpr int LONG_SEG = 32;
+constexpr int OP_FMA = 0;
+constexpr int OP_SUM = 1;
+
+template <int OP>
+DQRM_INLINE float4 combine(float4 acc, float4 v, bool& first, float nlr) {
+    if (OP == OP_FMA) {
+        acc.x = fmaf(v.x, nlr, acc.x); acc.y = fmaf(v.y, nlr, acc.y);
+        acc.z = fmaf(v.z, nlr, acc.z); acc.w = fmaf(v.w, nlr, acc.w);
+    } else if (first) {
+        acc = v;
+        first = false;
+    } else {
+        acc.x = acc.x + v.x; acc.y = acc.y + v.y; acc.z = acc.z + v.z; acc.w = acc.w + v.w;
+    }
+    return acc;
+}
+
+DQRM_INLINE bool is_head(const uint64_t* keys, int i) {
+    return i == 0 || key_row(keys[i - 1]) != key_row(keys[i]);
+}
+
+DQRM_INLINE bool is_long(const uint64_t* keys, int n, int i, uint32_t row) {
+    return i + LONG_SEG < n && key_row(keys[i + LONG_SEG]) == row;
+}
+
+template <int LPR, int OP, class Src>
+DQRM_INLINE float4 seg_reduce_group(const uint64_t* keys, int n, int i, uint32_t row, float4 acc,
+                                    const Src& src, float nlr, int sub) {
+    const uint32_t head_lo = key_lo(keys[i]);
+    bool first = true;
+    for (int j = i;; j += 4) {
+        float4 v[4];
+        bool m[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int jj = j + c;
+            const uint64_t kk = jj < n ? keys[jj] : ~0ull;
+            m[c] = key_row(kk) == row;
+            v[c] = src.load(m[c] ? key_lo(kk) : head_lo, sub);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (m[c]) acc = combine<OP>(acc, v[c], first, nlr);
+        }
+        if (!m[3]) break;
+    }
+    return acc;
+}
+
+template <int LPR, int OP, class Src>
+DQRM_INLINE float4 seg_reduce_wave(const uint64_t* keys, int n, int i, uint32_t row, float4 acc,
+                                   const Src& src, float nlr) {
+    constexpr int G = WAVE / LPR;
+    const int lane = threadIdx.x % WAVE;
+    const int g = lane / LPR, sub = lane % LPR;
+    const uint32_t head_lo = key_lo(keys[i]);
+    bool first = true;
+    int j = i;
+    auto fetch = [&](int jb, float4& v, bool& ok) {
+        const int jj = jb + g;
+        const uint64_t kk = jj < n ? keys[jj] : ~0ull;
+        ok = key_row(kk) == row;
+        v = src.load(ok ? key_lo(kk) : head_lo, sub);
+    };
+    float4 v0;
+    bool ok0;
+    fetch(j, v0, ok0);
+    for (;;) {
+        float4 v1;
+        bool ok1;
+        fetch(j + G, v1, ok1);  // prefetch the next chunk before combining this one
+        const uint64_t msk = __ballot(ok0);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            if (!((msk >> (k * LPR)) & 1ull)) break;  // wave-uniform
+            float4 x;
+            x.x = __shfl(v0.x, k * LPR + sub, WAVE);
+            x.y = __shfl(v0.y, k * LPR + sub, WAVE);
+            x.z = __shfl(v0.z, k * LPR + sub, WAVE);
+            x.w = __shfl(v0.w, k * LPR + sub, WAVE);
+            acc = combine<OP>(acc, x, first, nlr);
+        }
+        if (!((msk >> ((G - 1) * LPR)) & 1ull)) break;
+        v0 = v1;
+        ok0 = ok1;
+        j += G;
+    }
+    return acc;
+}
+
+// Visit every segment head once: short segments by lane groups (strided), long ones by
+// whole waves. fn(i, row, sub, writer, wave_mode) runs the per-row epilogue; it calls the
+// matching seg_reduce_* itself (so the initial accumulator can be loaded first).
+template <int LPR, class Fn>
+DQRM_INLINE void for_each_segment(const uint64_t* keys, int n, Fn&& fn) {
+    const int sub = threadIdx.x % LPR;
+    const int grp = threadIdx.x / LPR;
+    const int ngrp = blockDim.x / LPR;
+    for (int i = grp; i < n; i += ngrp) {
+        if (!is_head(keys, i)) continue;
+        const uint32_t row = key_row(keys[i]);
+        if (is_long(keys, n, i, row)) continue;
+        fn(i, row, sub, true, false);
+    }
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    for (int base = w * WAVE; base < n; base += nw * WAVE) {
+        const int i = base + lane;
+        bool lh = false;
+        if (i < n && is_head(keys, i)) lh = is_long(keys, n, i, key_row(keys[i]));
+        uint64_t msk = __ballot(lh);
+        while (msk) {
+            const int l = __ffsll((long long)msk) - 1;
+            msk &= msk - 1;
+            const int h = base + l;
+            fn(h, key_row(keys[h]), lane % LPR, lane < LPR, true);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Incremental |W| hierarchy maintenance (exact).
+// Before it runs, every segment head's key carries the row's OLD rowmax in its low bits
+// (the row epilogue swaps it in once the segment has been read). A block's new max is
+// max(old blkmax, new rowmax of its touched rows) unless one of those rows held the old
+// max and shrank; only then the block's 256 rowmax are re-read. Same one level up with
+// the block-start keys carrying the old blkmax. The table max re-reduces its superblocks.
+// ------------------------------------------------------------------------------------
+DQRM_INLINE void maintain_hierarchy(const Meta& m, int t, uint64_t* keys, int n,
                                     const float* rowmax, float* blkmax, float* sblkmax,
                                     float* tmax, float* s_red) {
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
     const int64_t nrows = m.num_rows[t];
     const int64_t nblk = ceil_div(nrows, BLK);
     const int64_t nsblk = ceil_div(nblk, SBLK_BLOCKS);
-    // dirty blocks: first key of each distinct (row >> 8)
+    const int64_t rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    // level 1: blocks
     for (int base = w * WAVE; base < n; base += nw * WAVE) {
         const int i = base + lane;
-        bool head = false;
-        if (i < n) {
-            uint32_t b = key_row(keys[i]) >> 8;
-            head = (i == 0) || (key_row(keys[i - 1]) >> 8) != b;
-        }
-        uint64_t msk = __ballot(head);
+        const bool start = i < n && (i == 0 || (key_row(keys[i - 1]) >> 8) != (key_row(keys[i]) >> 8));
+        uint64_t msk = __ballot(start);
         while (msk) {
             const int l = __ffsll((long long)msk) - 1;
             msk &= msk - 1;
-            const int64_t b = key_row(keys[base + l]) >> 8;
-            const int64_t r0 = b * BLK;
-            const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
-            float v = 0.0f;
-            for (int64_t r = r0 + lane; r < r1; r += WAVE) v = fmaxf(v, rowmax[m.row_base[t] + r]);
-            v = wave_max(v);
-            if (lane == 0) blkmax[m.blk_base[t] + b] = v;
+            const int i0 = base + l;
+            const uint32_t blk = key_row(keys[i0]) >> 8;
+            const float old_blk = blkmax[bb + blk];
+            bool dec = false;
+            float cand = 0.0f;
+            for (int p0 = i0;; p0 += WAVE) {
+                const int p = p0 + lane;
+                const bool in = p < n && (key_row(keys[p]) >> 8) == blk;
+                if (in && (p == i0 || is_head(keys, p))) {
+                    const float old_rm = __uint_as_float(key_lo(keys[p]));
+                    const float new_rm = rowmax[rb + key_row(keys[p])];
+                    dec |= (old_rm == old_blk) && (new_rm < old_rm);
+                    cand = fmaxf(cand, new_rm);
+                }
+                if (!__all(in)) break;
+            }
+            dec = __any(dec);
+            cand = wave_max(cand);
+            float nb;
+            if (dec) {
+                const int64_t r0 = (int64_t)blk * BLK;
+                const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
+                float v = 0.0f;
+                for (int64_t r = r0 + lane; r < r1; r += WAVE) v = fmaxf(v, rowmax[rb + r]);
+                nb = wave_max(v);
+            } else {
+                nb = fmaxf(old_blk, cand);
+            }
+            if (lane == 0) {
+                blkmax[bb + blk] = nb;
+                keys[i0] = with_lo(keys[i0], __float_as_uint(old_blk));
+            }
         }
     }
     __syncthreads();
+    // level 2: superblocks, from the block-start keys (old blkmax in their low bits)
     for (int base = w * WAVE; base < n; base += nw * WAVE) {
         const int i = base + lane;
-        bool head = false;
-        if (i < n) {
-            uint32_t sb = key_row(keys[i]) >> 16;
-            head = (i == 0) || (key_row(keys[i - 1]) >> 16) != sb;
-        }
-        uint64_t msk = __ballot(head);
+        const bool start = i < n && (i == 0 || (key_row(keys[i - 1]) >> 16) != (key_row(keys[i]) >> 16));
+        uint64_t msk = __ballot(start);
         while (msk) {
             const int l = __ffsll((long long)msk) - 1;
             msk &= msk - 1;
-            const int64_t sb = key_row(keys[base + l]) >> 16;
-            const int64_t b0 = sb * SBLK_BLOCKS;
-            const int64_t b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-            float v = 0.0f;
-            for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[m.blk_base[t] + b]);
-            v = wave_max(v);
-            if (lane == 0) sblkmax[m.sblk_base[t] + sb] = v;
+            const int i0 = base + l;
+            const uint32_t sb = key_row(keys[i0]) >> 16;
+            const float old_sb = sblkmax[sbb + sb];
+            bool dec = false;
+            float cand = 0.0f;
+            for (int p0 = i0;; p0 += WAVE) {
+                const int p = p0 + lane;
+                const bool in = p < n && (key_row(keys[p]) >> 16) == sb;
+                if (in && (p == i0 || (key_row(keys[p - 1]) >> 8) != (key_row(keys[p]) >> 8))) {
+                    const uint32_t blk = key_row(keys[p]) >> 8;
+                    const float old_b = __uint_as_float(key_lo(keys[p]));
+                    const float new_b = blkmax[bb + blk];
+                    dec |= (old_b == old_sb) && (new_b < old_b);
+                    cand = fmaxf(cand, new_b);
+                }
+                if (!__all(in)) break;
+            }
+            dec = __any(dec);
+            cand = wave_max(cand);
+            float ns;
+            if (dec) {
+                const int64_t b0 = (int64_t)sb * SBLK_BLOCKS;
+                const int64_t b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+                float v = 0.0f;
+                for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[bb + b]);
+                ns = wave_max(v);
+            } else {
+                ns = fmaxf(old_sb, cand);
+            }
+            if (lane == 0) sblkmax[sbb + sb] = ns;
         }
     }
     __syncthreads();
     float v = 0.0f;
-    for (int64_t k = threadIdx.x; k < nsblk; k += blockDim.x) v = fmaxf(v, sblkmax[m.sblk_base[t] + k]);
+    for (int64_t k = threadIdx.x; k < nsblk; k += blockDim.x) v = fmaxf(v, sblkmax[sbb + k]);
     v = wave_max(v);
     if (lane == 0) s_red[w] = v;
     __syncthreads();
@@ -578,18 +760,12 @@ DQRM_INLINE int build_lookup_keys(uint64_t* keys, int key_cap, const int64_t* id
     __syncthreads();
     bitonic_sort_lds(keys, np2);
     // positions whose index was invalid (or not covered by any bag) stay ~0 and sort last
-    int valid = 0;
-    // count valid keys: first position with row == 0xFFFFFFFF
-    // (binary search on sorted keys)
-    {
-        int lo = 0, hi = n;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1;
-        }
-        valid = lo;
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1;
     }
-    return valid;
+    return lo;
 }
 
 struct BwdArgs {
@@ -623,6 +799,21 @@ struct BwdArgs {
     int key_cap;        // dynamic-LDS key capacity (power of two)
 };
 
+// dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363)
+struct DySource {
+    const float* base;  // dy + t * dst_t
+    int64_t st_b;
+    float s;
+    int ste;
+    DQRM_INLINE float4 load(uint32_t bag, int sub) const {
+        float4 g = reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[sub];
+        if (ste) {
+            g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
+        }
+        return g;
+    }
+};
+
 // MODE 0: fused SGD (single GPU);  MODE 1: coalesce + local grad scale (DP)
 template <int LPR, int MODE>
 __global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
@@ -641,7 +832,6 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
     const int64_t nrows = m.num_rows[t];
     const int64_t rb = m.row_base[t];
     const int D = LPR * 4;
-    const int L = (int)(a.idx_base[t + 1] - a.idx_base[t]);
     if (threadIdx.x == 0) s_absmax = 0u;
 
     const int n = build_lookup_keys(keys, a.key_cap, a.idx, a.off, a.idx_base, a.B, t, nrows, a.err);
@@ -649,56 +839,45 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
         if (MODE == 1 && threadIdx.x == 0) { a.counts_out[t] = 0; a.s_loc[t] = 0.0f; }
         return;
     }
-    const int U = head_scan<MAX_LDS_KEYS / TABLE_WG>(keys, n, s_base, s_wtot);
+    int U = 0;
+    if (MODE == 1) U = head_scan<MAX_LDS_KEYS / TABLE_WG>(keys, n, s_base, s_wtot);
 
-    const float s = a.scale[t];
+    DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste};
     const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
-    const int lane = threadIdx.x % LPR;
-    const int grp = threadIdx.x / LPR;
-    const int ngrp = blockDim.x / LPR;
-    int64_t cap = 0;
-    if (MODE == 1) cap = a.cap_base[t + 1] - a.cap_base[t];
+    const int64_t cap = MODE == 1 ? a.cap_base[t + 1] - a.cap_base[t] : 0;
     float local_absmax = 0.0f;
 
-    for (int i = grp; i < n; i += ngrp) {
-        const uint32_t row = key_row(keys[i]);
-        if (i > 0 && key_row(keys[i - 1]) == row) continue;  // not a segment head
+    for_each_segment<LPR>(keys, n, [&](int i, uint32_t row, int sub, bool writer, bool wave_mode) {
         const int64_t grow = rb + row;
-        float4 w;
-        if (MODE == 0) w = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool first = true;
-        for (int j = i; j < n; ++j) {
-            const uint64_t kk = keys[j];
-            if (key_row(kk) != row) break;
-            const int64_t bag = (int64_t)(uint32_t)kk;
-            float4 g = reinterpret_cast<const float4*>(a.dy + (int64_t)t * a.dst_t + bag * a.dst_b)[lane];
-            if (a.ste) {  // SymmetricQuantFunction.backward of q*s: (g*s)/s
-                g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
-            }
-            if (MODE == 0) {  // torch CPU sparse SGD: per entry, in lookup order, w = fma(v, -lr, w)
-                w.x = fmaf(g.x, a.nlr, w.x); w.y = fmaf(g.y, a.nlr, w.y);
-                w.z = fmaf(g.z, a.nlr, w.z); w.w = fmaf(g.w, a.nlr, w.w);
-            } else {          // coalesce(): first value, then += in ascending position order
-                if (first) { acc = g; first = false; }
-                else { acc.x = acc.x + g.x; acc.y = acc.y + g.y; acc.z = acc.z + g.z; acc.w = acc.w + g.w; }
-            }
-        }
         if (MODE == 0) {
-            reinterpret_cast<float4*>(a.W + grow * D)[lane] = w;
+            float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+            const float old_rm = a.rowmax[grow];
+            w = wave_mode ? seg_reduce_wave<LPR, OP_FMA>(keys, n, i, row, w, src, a.nlr)
+                          : seg_reduce_group<LPR, OP_FMA>(keys, n, i, row, w, src, a.nlr, sub);
             const float rm = group_max<LPR>(abs_max4(w));
-            if (lane == 0) a.rowmax[grow] = rm;
-            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, lane, r_pack);
-        } else {
-            const int u = head_ordinal<MAX_LDS_KEYS / TABLE_WG>(keys, s_base, i);
-            if (u < cap) {
-                const int64_t e = a.cap_base[t] + u;
-                reinterpret_cast<float4*>(a.vals_out + e * D)[lane] = acc;
-                if (lane == 0) a.rows_out[e] = (int32_t)row;
+            if (writer) {
+                reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+                if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
+                if (sub == 0) {
+                    a.rowmax[grow] = rm;
+                    keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+                }
             }
-            local_absmax = fmaxf(local_absmax, abs_max4(acc));
+        } else {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            acc = wave_mode ? seg_reduce_wave<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f)
+                            : seg_reduce_group<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f, sub);
+            if (writer) {
+                const int u = head_ordinal<MAX_LDS_KEYS / TABLE_WG>(keys, s_base, i);
+                if (u < cap) {
+                    const int64_t e = a.cap_base[t] + u;
+                    reinterpret_cast<float4*>(a.vals_out + e * D)[sub] = acc;
+                    if (sub == 0) a.rows_out[e] = (int32_t)row;
+                }
+                local_absmax = fmaxf(local_absmax, abs_max4(acc));
+            }
         }
-    }
+    });
     if (MODE == 1) {
         local_absmax = wave_max(local_absmax);
         if ((threadIdx.x % WAVE) == 0) atomicMax(&s_absmax, __float_as_uint(local_absmax));
@@ -714,7 +893,6 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
         else
             a.s_loc[t] = 0.0f;
     }
-    (void)L;
 }
 
 // ------------------------------------------------------------------------------------
@@ -822,24 +1000,32 @@ struct ApplyArgs {
     int key_cap;
 };
 
+// one payload entry (rank = lo >> 24, entry = lo & 0xFFFFFF) widened to f32
 template <int LPR>
-DQRM_INLINE float4 load_payload_vals(const unsigned char* p, const PayloadLayout& pl, int64_t e,
-                                     int lane) {
-    const int D = LPR * 4;
-    float4 v;
-    if (pl.elem == 1) {
-        uint32_t x = reinterpret_cast<const uint32_t*>(p + pl.vals_off + e * D)[lane];
-        v.x = (float)(int8_t)(x & 0xFF); v.y = (float)(int8_t)((x >> 8) & 0xFF);
-        v.z = (float)(int8_t)((x >> 16) & 0xFF); v.w = (float)(int8_t)(x >> 24);
-    } else if (pl.elem == 2) {
-        uint2 x = reinterpret_cast<const uint2*>(p + pl.vals_off + e * D * 2)[lane];
-        v.x = (float)(int16_t)(x.x & 0xFFFF); v.y = (float)(int16_t)(x.x >> 16);
-        v.z = (float)(int16_t)(x.y & 0xFFFF); v.w = (float)(int16_t)(x.y >> 16);
-    } else {
-        v = reinterpret_cast<const float4*>(p + pl.vals_off + e * D * 4)[lane];
+struct PayloadSource {
+    const unsigned char* payloads;
+    int64_t payload_bytes;
+    PayloadLayout pl;
+    int64_t cap_base_t;
+    DQRM_INLINE float4 load(uint32_t lo, int sub) const {
+        constexpr int D = LPR * 4;
+        const unsigned char* p = payloads + (int64_t)(lo >> 24) * payload_bytes;
+        const int64_t e = cap_base_t + (int64_t)(lo & 0xFFFFFF);
+        float4 v;
+        if (pl.elem == 1) {
+            uint32_t x = reinterpret_cast<const uint32_t*>(p + pl.vals_off + e * D)[sub];
+            v.x = (float)(int8_t)(x & 0xFF); v.y = (float)(int8_t)((x >> 8) & 0xFF);
+            v.z = (float)(int8_t)((x >> 16) & 0xFF); v.w = (float)(int8_t)(x >> 24);
+        } else if (pl.elem == 2) {
+            uint2 x = reinterpret_cast<const uint2*>(p + pl.vals_off + e * D * 2)[sub];
+            v.x = (float)(int16_t)(x.x & 0xFFFF); v.y = (float)(int16_t)(x.x >> 16);
+            v.z = (float)(int16_t)(x.y & 0xFFFF); v.w = (float)(int16_t)(x.y >> 16);
+        } else {
+            v = reinterpret_cast<const float4*>(p + pl.vals_off + e * D * 4)[sub];
+        }
+        return v;
     }
-    return v;
-}
+};
 
 template <int LPR>
 __global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
@@ -900,25 +1086,17 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
     const float inv_n = (float)(1.0 / (double)a.N);
     const float sim_f = (float)((double)s / (double)a.N);
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
-    const int lane = threadIdx.x % LPR;
-    const int grp = threadIdx.x / LPR;
-    const int ngrp = blockDim.x / LPR;
-    for (int i = grp; i < n; i += ngrp) {
-        const uint32_t row = key_row(keys[i]);
-        if (i > 0 && key_row(keys[i - 1]) == row) continue;
+    PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, a.cap_base[t]};
+
+    for_each_segment<LPR>(keys, n, [&](int i, uint32_t row, int sub, bool writer, bool wave_mode) {
+        const int64_t grow = rb + row;
+        float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+        const float old_rm = a.rowmax[grow];
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool first = true;
-        for (int j = i; j < n; ++j) {
-            const uint64_t kk = keys[j];
-            if (key_row(kk) != row) break;
-            const int r = (int)((kk >> 24) & 0xFF);
-            const int64_t e = a.cap_base[t] + (int64_t)(kk & 0xFFFFFF);
-            float4 v = load_payload_vals<LPR>(a.payloads + (int64_t)r * a.payload_bytes, pl, e, lane);
-            // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
-            // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
-            if (first) { acc = v; first = false; }
-            else { acc.x = acc.x + v.x; acc.y = acc.y + v.y; acc.z = acc.z + v.z; acc.w = acc.w + v.w; }
-        }
+        // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
+        // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
+        acc = wave_mode ? seg_reduce_wave<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f)
+                        : seg_reduce_group<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f, sub);
         float4 v;
         if (a.mode == DQRM_UPD_DP) {          // update.mul_(1/N) ; grad * s.item()
             v.x = (acc.x * inv_n) * s; v.y = (acc.y * inv_n) * s;
@@ -928,15 +1106,18 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
         } else {                              // FP32 sparse allreduce, mul_(1/N)
             v.x = acc.x * inv_n; v.y = acc.y * inv_n; v.z = acc.z * inv_n; v.w = acc.w * inv_n;
         }
-        const int64_t grow = rb + row;
-        float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
         // weight.data.add_(-lr * grad_update): separately rounded product, then add
         w.x = w.x + a.nlr * v.x; w.y = w.y + a.nlr * v.y; w.z = w.z + a.nlr * v.z; w.w = w.w + a.nlr * v.w;
-        reinterpret_cast<float4*>(a.W + grow * D)[lane] = w;
         const float rm = group_max<LPR>(abs_max4(w));
-        if (lane == 0) a.rowmax[grow] = rm;
-        if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, lane, r_pack);
-    }
+        if (writer) {
+            reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
+            if (sub == 0) {
+                a.rowmax[grow] = rm;
+                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+            }
+        }
+    });
     __syncthreads();
     maintain_hierarchy(m, t, keys, n, a.rowmax, a.blkmax, a.sblkmax, a.tmax, s_red);
 }
@@ -977,6 +1158,15 @@ int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
         case 64: { constexpr int LPR = 64; __VA_ARGS__; } break; \
         default: return set_error(DQRM_E_INVALID, "dqrm: unsupported dim %d", (int)(D)); \
     }
+
+// allow the per-table kernels more than the default 64 KiB of dynamic LDS (gfx950: 160 KiB/CU)
+template <typename K>
+int allow_lds(K kernel, size_t bytes) {
+    if (bytes <= 65536) return DQRM_OK;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    return DQRM_OK;
+}
 
 size_t table_lds_bytes(int64_t max_keys) {
     int64_t n = 2;
@@ -1114,6 +1304,7 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     a.key_cap = (int)(lds / sizeof(uint64_t));
     const int D = set->dim;
     DISPATCH_LPR(D, {
+        if ((rc = allow_lds(k_table_bwd<LPR, 0>, lds))) return rc;
         hipLaunchKernelGGL((k_table_bwd<LPR, 0>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
     });
     LAUNCH_CHECK();
@@ -1143,6 +1334,7 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
     a.key_cap = (int)(lds / sizeof(uint64_t));
     const int D = set->dim;
     DISPATCH_LPR(D, {
+        if ((rc = allow_lds(k_table_bwd<LPR, 1>, lds))) return rc;
         hipLaunchKernelGGL((k_table_bwd<LPR, 1>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
     });
     LAUNCH_CHECK();
@@ -1199,6 +1391,7 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
     const size_t lds = table_lds_bytes(MAX_LDS_KEYS);
     const int D = set->dim;
     DISPATCH_LPR(D, {
+        if ((rc = allow_lds(k_table_apply<LPR>, lds))) return rc;
         hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T), dim3(TABLE_WG), lds, st, a);
     });
     LAUNCH_CHECK();

@@ -42,7 +42,7 @@ def random_bags(num_rows, B, seed, num_indices_per_lookup=10, fixed=False):
                 g = np.int64(num_indices_per_lookup)
             else:
                 r = rs.random_sample(1)
-                g = np.int64(np.round(max([1.0], r[0] * min(size, num_indices_per_lookup))))
+                g = np.int64(np.round(max(1.0, float(r[0]) * min(size, num_indices_per_lookup))))
             r = rs.random_sample(int(g))
             grp = np.unique(np.round(r * (size - 1)).astype(np.int64))
             off.append(o)

@@ -1,0 +1,63 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/dqrm.h declares,
+and rejects bad arguments without touching a device."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import deep_quantized_recommendation_model_dqrm_amd as dq
+from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+from deep_quantized_recommendation_model_dqrm_amd.comm import payload_bytes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    dq.build(verbose=False)
+    return L.load()
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "dqrm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dqrm_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_what_binding_expects():
+    assert header_functions() == sorted(L.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_header_symbol(lib):
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.dqrm_abi_version() == 1
+
+
+def test_payload_bytes_agree(lib):
+    for T, cap, D, bits in [(26, 3328, 16, 8), (26, 53248, 64, 8), (4, 7, 4, 16), (3, 0, 32, 32), (1, 1, 256, 2)]:
+        assert lib.dqrm_payload_bytes(T, cap, D, bits) == payload_bytes(T, cap, D, bits)
+
+
+def test_struct_layouts():
+    # dqrm_table_set: 2 x i32 + 3 x i64 + 11 pointers; dqrm_batch: 3 pointers + 2 x i64
+    assert C.sizeof(L.TableSet) == 8 + 24 + 11 * 8
+    assert C.sizeof(L.Batch) == 5 * 8
+
+
+def test_invalid_arguments_rejected_without_device(lib):
+    assert lib.dqrm_refresh_absmax(None, None) == L.DQRM_E_INVALID
+    assert b"null table set" in lib.dqrm_last_error()
+    ts = L.TableSet()
+    ts.num_tables, ts.dim = 2, 12  # dim must be 4 * 2^k
+    assert lib.dqrm_emb_fwd(C.byref(ts), None, 4, 0, None, 0, 0, None) == L.DQRM_E_INVALID
+    assert b"dim" in lib.dqrm_last_error()
+    assert lib.dqrm_grad_quant_pack(0, 16, None, 0, None, None, None, None, 1, 8, None, None, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_grad_quant_pack(2, 16, None, 0, None, None, None, None, 1, 7 + 30, None, None, None) == L.DQRM_E_INVALID
+
+
+def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(L.DQRMError):
+        L.load(str(tmp_path / "missing.so"))

@@ -1,0 +1,300 @@
+"""GPU parity: libdqrm (HIP, via the C ABI) against the CPU oracle and golden fixtures.
+
+Bar: bit-exact on indices, packing, counts and quantized integers; forward outputs and
+updated weights are compared exactly too (the kernels reproduce the reference's f32
+rounding); the north-star tolerance (1e-5) is only used against torch-CPU-native fixtures.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gen_inputs as G
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def dq():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import deep_quantized_recommendation_model_dqrm_amd as d
+
+    d.build(verbose=False)
+    d._lib.load()
+    return d
+
+
+def load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name)))
+
+
+def make_set(dq, Ws, packed=False):
+    return dq.EmbeddingTableSet([w.shape[0] for w in Ws], Ws[0].shape[1], device="cuda", packed=packed,
+                                init=None, weights=[torch.from_numpy(w) for w in Ws])
+
+
+def to_batch(dq, idxs, offs):
+    return dq.LookupBatch([torch.from_numpy(np.ascontiguousarray(i)) for i in idxs],
+                          [torch.from_numpy(np.ascontiguousarray(o)) for o in offs], device="cuda")
+
+
+from test_oracle_golden import SINGLE, regen_single, dp_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("name", SINGLE)
+def test_single_gpu_qat_steps_bitexact(dq, golden_dir, name):
+    fx = load(golden_dir, name)
+    Ws, batches, dys = regen_single(fx)
+    bits, lr = int(fx["bits"]), float(fx["lr"])
+    ts = make_set(dq, Ws)
+    for k, ((idxs, offs), dy) in enumerate(zip(batches, dys)):
+        b = to_batch(dq, idxs, offs)
+        y = ts.forward(b, bits=bits, refresh_scale=True)
+        np.testing.assert_array_equal(ts.scale.cpu().numpy(), fx[f"s{k}"])
+        np.testing.assert_array_equal(y.cpu().numpy(), fx[f"y{k}"])
+        ts.backward_sgd(b, torch.from_numpy(dy).cuda(), lr=lr, ste=True)
+    assert ts.read_errors() == 0
+    for t in range(len(Ws)):
+        rows = torch.from_numpy(fx[f"rows_t{t}"]).cuda()
+        np.testing.assert_array_equal(ts.table_weight(t)[rows].cpu().numpy(), fx[f"w_t{t}"])
+    # the incrementally maintained |W| hierarchy equals a full recompute
+    tmax_inc = ts.tmax.clone()
+    ts.refresh_absmax()
+    torch.testing.assert_close(tmax_inc, ts.tmax, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("bits", [2, 4, 8, 16])
+@pytest.mark.parametrize("case", ["tie", "zero"])
+def test_edge_cases_bitexact(dq, golden_dir, bits, case):
+    fx = load(golden_dir, "edge.npz")
+    ts = make_set(dq, [fx[f"W_{case}"]])
+    b = to_batch(dq, [fx[f"idx_{case}"]], [fx[f"off_{case}"]])
+    y = ts.forward(b, bits=bits)
+    assert ts.scale.item() == fx[f"{case}_b{bits}_s"]
+    np.testing.assert_array_equal(y[0].cpu().numpy(), fx[f"{case}_b{bits}_y"])
+    ts.backward_sgd(b, torch.from_numpy(fx[f"{case}_b{bits}_dy"][None]).cuda(), lr=0.1)
+    np.testing.assert_array_equal(ts.W.cpu().numpy(), fx[f"{case}_b{bits}_w"])
+
+
+def test_full_precision_flag(dq, golden_dir):
+    fx = load(golden_dir, "edge.npz")
+    ts = make_set(dq, [fx["W_tie"]])
+    b = to_batch(dq, [fx["idx_tie"]], [fx["off_tie"]])
+    y = ts.forward(b, full_precision=True)
+    np.testing.assert_array_equal(y[0].cpu().numpy(), fx["fp_y"])
+    ts.backward_sgd(b, torch.from_numpy(fx["fp_dy"][None]).cuda(), lr=0.1, ste=False)
+    np.testing.assert_array_equal(ts.W.cpu().numpy(), fx["fp_w"])
+
+
+def test_bag_major_layout_matches(dq):
+    rows = [1000, 7, 50000]
+    Ws = G.table_weights(rows, 32, 5)
+    P = G.pooling_one(rows, 96, 6)
+    ts = make_set(dq, Ws)
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+    y_tbd = ts.forward(b)
+    y_btd = ts.forward(b, layout="btd")
+    torch.testing.assert_close(y_tbd.permute(1, 0, 2), y_btd, rtol=0, atol=0)
+
+
+def test_packed_int4_path_bitexact(dq, golden_dir):
+    """Packed rows equal the oracle's packing; the INT4 gather equals the FP32 fake-quant
+    path; touched rows are repacked with the frozen scale after SGD."""
+    fx = load(golden_dir, "kaggle_pool1.npz")
+    Ws, batches, dys = regen_single(fx)
+    ts = make_set(dq, Ws, packed=True)
+    ts.refresh_scale_and_pack(4)
+    s = ts.scale.cpu().numpy()
+    np.testing.assert_array_equal(s, fx["s0"])
+    for t in range(len(Ws)):
+        np.testing.assert_array_equal(ts.table_packed(t).cpu().numpy(), O.pack_int4(Ws[t], s[t]))
+    (idxs, offs), dy = batches[0], dys[0]
+    b = to_batch(dq, idxs, offs)
+    y_packed = ts.forward(b, refresh_scale=False, use_packed=True)
+    np.testing.assert_array_equal(y_packed.cpu().numpy(), fx["y0"])
+    ts.backward_sgd(b, torch.from_numpy(dy).cuda(), lr=0.1, repack=True)
+    W_host = ts.W.cpu().numpy()
+    P_host = ts.packed.cpu().numpy()
+    for t in range(len(Ws)):
+        base, n = ts.row_base[t], ts.num_rows[t]
+        np.testing.assert_array_equal(P_host[base:base + n], O.pack_int4(W_host[base:base + n], s[t]))
+    # scale refresh: tables whose max moved are fully repacked, the rest keep their rows
+    ts.refresh_scale_and_pack(4)
+    s2 = ts.scale.cpu().numpy()
+    P2 = ts.packed.cpu().numpy()
+    for t in range(len(Ws)):
+        base, n = ts.row_base[t], ts.num_rows[t]
+        assert s2[t] == O.table_scale(W_host[base:base + n], 4)
+        np.testing.assert_array_equal(P2[base:base + n], O.pack_int4(W_host[base:base + n], s2[t]))
+
+
+def _emulate_ranks(dq, ts, caps, rank_batches, rank_dys, grad_bits, lr, mode=None, repack=False):
+    """Run the exchange's three device steps for N ranks on one GPU (the all-gathers become
+    stacking), exactly as SparseGradExchange does on each rank."""
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels, payload_bytes
+
+    N = len(rank_batches)
+    k = HipExchangeKernels(ts)
+    wss = []
+    for r in range(N):
+        ws = dq.CoalescedGrad.allocate(caps, ts.D, "cuda")
+        k.coalesce(rank_batches[r], rank_dys[r], ws, True, grad_bits, "tbd")
+        wss.append(ws)
+    s_all = torch.stack([ws.s_loc for ws in wss])
+    P = payload_bytes(ts.T, wss[0].cap_total, ts.D, grad_bits)
+    payloads = torch.zeros(N, P, dtype=torch.uint8, device="cuda")
+    s_avg = torch.zeros(ts.T, dtype=torch.float32, device="cuda")
+    for r in range(N):
+        k.quant_pack(wss[r], s_all, N, grad_bits, s_avg, payloads[r])
+    if mode is None:
+        mode = L.DQRM_UPD_FP32 if grad_bits == 32 else L.DQRM_UPD_DP
+    k.apply(wss[0], payloads, P, N, grad_bits, s_avg, lr, mode, repack)
+    return wss, payloads, s_avg
+
+
+def _decode_payload(p, T, cap_base, D, bits, t):
+    p = p.cpu().numpy()
+    a16 = lambda x: (x + 15) & ~15  # noqa: E731
+    CAP = int(cap_base[-1])
+    cnt = p[: 4 * T].view(np.int32)[t]
+    rows_off = a16(4 * T)
+    vals_off = rows_off + a16(4 * CAP)
+    rows = p[rows_off: rows_off + 4 * CAP].view(np.int32)[cap_base[t]: cap_base[t] + cnt]
+    dt = np.int8 if bits <= 8 else np.int16
+    vals = p[vals_off: vals_off + CAP * D * np.dtype(dt).itemsize].view(dt).reshape(CAP, D)
+    return rows, vals[cap_base[t]: cap_base[t] + cnt].astype(f32)
+
+
+DP = ["dp_n2.npz", "dp_n4.npz", "dp_n4_zipf.npz", "dp_n2_fp32.npz", "dp_n2_b16.npz"]
+
+
+@pytest.mark.parametrize("name", DP)
+def test_data_parallel_exchange_bitexact(dq, golden_dir, name):
+    fx = load(golden_dir, name)
+    num_rows = fx["num_rows"].tolist()
+    D, seed, N, bits = int(fx["D"]), int(fx["seed"]), int(fx["N"]), int(fx["bits"])
+    quantized = bool(fx["quantized"])
+    gb = bits if quantized else 32
+    Ws = G.table_weights(num_rows, D, seed)
+    ts = make_set(dq, Ws)
+    for k in range(int(fx["steps"])):
+        b, dys = dp_inputs(fx, k)
+        rank_batches = [to_batch(dq, [x[0] for x in b[r]], [x[1] for x in b[r]]) for r in range(N)]
+        rank_dys = [torch.from_numpy(np.stack(dys[r])).cuda() for r in range(N)]
+        for rb in rank_batches:  # each rank's forward refreshes the same scale
+            ts.forward(rb, refresh_scale=True)
+        caps = dq.default_caps(num_rows, max(rb.max_lookups for rb in rank_batches))
+        wss, payloads, s_avg = _emulate_ranks(dq, ts, caps, rank_batches, rank_dys, gb, float(fx["lr"]))
+        if quantized:
+            cb = wss[0].cap_base.cpu().numpy()
+            for t in range(len(num_rows)):
+                assert s_avg[t].item() == fx[f"k{k}_t{t}_s_avg"]
+                for r in range(N):
+                    assert wss[r].s_loc[t].item() == fx[f"k{k}_t{t}_r{r}_s_loc"]
+                    rows, q = _decode_payload(payloads[r], len(num_rows), cb, D, bits, t)
+                    np.testing.assert_array_equal(rows, fx[f"k{k}_t{t}_r{r}_rows"])
+                    np.testing.assert_array_equal(q, fx[f"k{k}_t{t}_r{r}_q"])
+    assert ts.read_errors() == 0
+    for t in range(len(num_rows)):
+        rows = torch.from_numpy(fx[f"rows_t{t}"]).cuda()
+        np.testing.assert_array_equal(ts.table_weight(t)[rows].cpu().numpy(), fx[f"w_t{t}"])
+
+
+def test_simulated_dp_bitexact(dq, golden_dir):
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+
+    fx = load(golden_dir, "sim_dp.npz")
+    num_rows = fx["num_rows"].tolist()
+    D, B, seed, N = int(fx["D"]), int(fx["B"]), int(fx["seed"]), int(fx["N"])
+    Ws = G.table_weights(num_rows, D, seed)
+    ts = make_set(dq, Ws)
+    batches, dys = [], []
+    for k in range(N):
+        P = G.pooling_one(num_rows, B, seed + 17 * (k + 1))
+        batches.append(dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()))
+        dys.append(torch.from_numpy(G.upstream_grad(len(num_rows), B, D, seed + 31 * (k + 1))).cuda())
+    ts.forward(batches[0])
+    # micro-step scales: the FIRST micro-step's local scale is used for every micro-step
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels, payload_bytes
+    kern = HipExchangeKernels(ts)
+    caps = dq.default_caps(num_rows, B)
+    wss = []
+    for k in range(N):
+        ws = dq.CoalescedGrad.allocate(caps, D, "cuda")
+        kern.coalesce(batches[k], dys[k], ws, True, 8, "tbd")
+        wss.append(ws)
+    s_first = wss[0].s_loc.clone()
+    Pb = payload_bytes(len(num_rows), wss[0].cap_total, D, 8)
+    payloads = torch.zeros(N, Pb, dtype=torch.uint8, device="cuda")
+    s_avg = torch.zeros(len(num_rows), dtype=torch.float32, device="cuda")
+    for k in range(N):
+        kern.quant_pack(wss[k], s_first.view(1, -1), 1, 8, s_avg, payloads[k])
+    kern.apply(wss[0], payloads, Pb, N, 8, s_first, 0.1, L.DQRM_UPD_SIMULATED, False)
+    for t in range(len(num_rows)):
+        assert s_first[t].item() == fx[f"s_t{t}"]
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), fx[f"w_t{t}"])
+
+
+def test_invalid_indices_flag_not_fault(dq):
+    Ws = G.table_weights([100, 10], 16, 3)
+    ts = make_set(dq, Ws)
+    idx = [np.array([5, 100, -1, 3], np.int64), np.array([0, 9, 12, 1], np.int64)]
+    off = [np.arange(4, dtype=np.int64), np.array([0, 1, 1, 3], np.int64)]
+    b = to_batch(dq, idx, off)
+    y = ts.forward(b)
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    assert ts.read_errors() & L.DQRM_ERRF_INDEX
+    y0, _ = O.emb_fwd(Ws[0], idx[0], off[0], O.table_scale(Ws[0], 4))
+    np.testing.assert_array_equal(y[0].cpu().numpy(), y0)
+    ts.backward_sgd(b, torch.zeros(2, 4, 16, device="cuda"), lr=0.1)
+    assert ts.read_errors() & L.DQRM_ERRF_INDEX
+
+
+def test_capacity_error_is_reported(dq):
+    ts = make_set(dq, G.table_weights([100], 16, 3))
+    b = dq.LookupBatch.pooling_one(torch.zeros(1, 20000, dtype=torch.int64, device="cuda"))
+    with pytest.raises(dq._lib.DQRMError):
+        ts.backward_sgd(b, torch.zeros(1, 20000, 16, device="cuda"), lr=0.1)
+
+
+def test_kaggle_full_size_forward_and_step(dq):
+    """Full Criteo-Kaggle tables (33.8M rows, D=16): forward of every table equals the
+    oracle; after 3 SGD steps the scales still equal a full-table oracle scan."""
+    rows = G.KAGGLE_ROWS
+    ts = dq.EmbeddingTableSet(rows, 16, device="cuda", init="uniform", seed=11)
+    B = 2048
+    for k in range(3):
+        P = G.pooling_one(rows, B, 40 + k, dist="zipf" if k % 2 else "uniform")
+        b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+        y = ts.forward(b).cpu().numpy()
+        W = ts.W.cpu().numpy()
+        s = ts.scale.cpu().numpy()
+        for t in range(len(rows)):
+            Wt = W[ts.row_base[t]: ts.row_base[t] + rows[t]]
+            assert s[t] == O.table_scale(Wt, 4)
+            yo, _ = O.emb_fwd(Wt, P[t], np.arange(B), s[t])
+            np.testing.assert_array_equal(y[t], yo)
+        dy = torch.from_numpy(G.upstream_grad(len(rows), B, 16, 50 + k)).cuda()
+        ts.backward_sgd(b, dy, lr=0.1)
+    assert ts.read_errors() == 0
+
+
+def test_determinism_bitwise(dq):
+    rows = [3, 1000, 200000]
+    P = G.pooling_one(rows, 4096, 8, dist="zipf")
+    dy = torch.from_numpy(G.upstream_grad(3, 4096, 64, 9)).cuda()
+    outs = []
+    for _ in range(2):
+        ts = dq.EmbeddingTableSet(rows, 64, device="cuda", seed=4)
+        b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+        for _ in range(3):
+            ts.forward(b)
+            ts.backward_sgd(b, dy, lr=0.1)
+        outs.append(ts.W.clone())
+    assert torch.equal(outs[0], outs[1])
