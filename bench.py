@@ -112,7 +112,7 @@ def main():
     batches = make_batches(rows, B * world, rank, world, a.num_batches, a.seed, a.index_dist, dev)
     dy = torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + rank)) * 0.05
     y = torch.empty(T, B, D, device=dev)
-    ex = dq.SparseGradExchange.for_batch_shape(ts, B, grad_bits=a.grad_bits)
+    ex = dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits)
     kern = ex.kernels
     torch.cuda.synchronize()
     setup_s = time.time() - t0
@@ -125,13 +125,17 @@ def main():
         if ev is not None:
             ev[0][1].record()
             ev[1][0].record()
-        kern.coalesce(b, dy, ex.ws, True, a.grad_bits, "tbd")
+        kern.coalesce(b, dy, ex.ws, True, "tbd")
         if ev is not None:
             ev[1][1].record()
-        ex._all_gather(ex.s_all, ex.ws.s_loc)
+        if ex.world == 1:
+            absmax_all = ex.ws.absmax.view(1, -1)
+        else:
+            ex._all_gather(ex.absmax_all, ex.ws.absmax)
+            absmax_all = ex.absmax_all
         if ev is not None:
             ev[2][0].record()
-        kern.quant_pack(ex.ws, ex.s_all, ex.world, a.grad_bits, ex.s_avg, ex.payload)
+        kern.quant_pack(ex.ws, absmax_all, ex.world, a.grad_bits, ex.cap_base, ex.cap_total, ex.s_avg, ex.payload)
         if ev is not None:
             ev[2][1].record()
         if ex.world == 1:
@@ -141,7 +145,8 @@ def main():
             gathered = ex.gathered
         if ev is not None:
             ev[3][0].record()
-        kern.apply(ex.ws, gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg, a.lr, L.DQRM_UPD_DP, False)
+        kern.apply(ex.cap_base, ex.cap_total, gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg, a.lr,
+                   L.DQRM_UPD_DP, False)
         if ev is not None:
             ev[3][1].record()
 
@@ -166,7 +171,7 @@ def main():
     kms = {n: float(np.mean([evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(a.steps)])) for j, n in enumerate(names)}
 
     # algorithmic bytes per launch; unique counts from the last step
-    U = int(ex.ws.counts.sum().item())
+    U = int(ex.ws.ucount.sum().item())
     L_tot = T * B
     alg = {
         "emb_fwd": L_tot * (D * 4 + 8) + T * B * 8 + T * B * D * 4 + T * 4,

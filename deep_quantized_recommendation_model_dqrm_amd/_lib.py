@@ -23,12 +23,13 @@ DQRM_ERRF_OVERFLOW = 4
 
 DQRM_BLOCK_ROWS = 256
 DQRM_SBLOCK_ROWS = 65536
-DQRM_MAX_LDS_KEYS = 16384
+DQRM_TABLE_SPLIT = 8
+DQRM_SLOT_KEYS = 8192
 
 DQRM_FWD_REFRESH_SCALE = 1
 DQRM_FWD_USE_PACKED = 2
 DQRM_FWD_FULL_PRECISION = 4
-DQRM_FWD_BAG_MAJOR = 8
+DQRM_FWD_NT_STORE = 16
 
 DQRM_UPD_DP = 0
 DQRM_UPD_SIMULATED = 1
@@ -40,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_refresh_scale_and_pack",
     "dqrm_emb_fwd",
     "dqrm_emb_bwd_sgd",
+    "dqrm_coalesce_slot_caps",
     "dqrm_emb_bwd_coalesce",
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
@@ -73,6 +75,7 @@ class TableSet(C.Structure):
         ("meta", C.c_void_p),
         ("err", C.c_void_p),
         ("tflags", C.c_void_p),
+        ("sdirty", C.c_void_p),
     ]
 
 
@@ -100,7 +103,7 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("DQRM_LIB_PATH") or LIB_PATH
     if not os.path.exists(path):
         raise DQRMError(
             f"libdqrm.so not found at {path}: build it with "
@@ -116,14 +119,15 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_refresh_scale_and_pack": (C.c_int, [TS, C.c_int, P]),
         "dqrm_emb_fwd": (C.c_int, [TS, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P]),
         "dqrm_emb_bwd_sgd": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P]),
+        "dqrm_coalesce_slot_caps": (C.c_int64, [P, C.c_int, C.c_int64, P]),
         "dqrm_emb_bwd_coalesce": (
             C.c_int,
-            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, C.c_int, P],
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, P],
         ),
         "dqrm_payload_bytes": (C.c_size_t, [C.c_int, C.c_int64, C.c_int, C.c_int]),
         "dqrm_grad_quant_pack": (
             C.c_int,
-            [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, P, P],
+            [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, C.c_int64, P, P, P],
         ),
         "dqrm_apply_sparse_update": (
             C.c_int,

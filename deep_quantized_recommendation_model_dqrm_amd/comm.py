@@ -9,8 +9,8 @@ Reference: sgd_quantized_gradients_parallel_comm.py
 MI355X design: the 52 per-table Gloo collectives of the reference become TWO collectives
 per step for all tables together, both all-gathers over RCCL (torch.distributed "nccl"
 on ROCm, xGMI point-to-point):
-  1. all_gather of the [T] local scales  -> every rank sums them in rank order (the
-     average is bit-identical on every rank);
+  1. all_gather of the per-slot max|grad| [T*8] -> every rank derives each rank's
+     local scale and averages them in Gloo's order (bit-identical on every rank);
   2. all_gather of one fixed-capacity payload per rank  {counts i32[T], rows i32[CAP],
      q int8[CAP, D]} -> every rank decodes all N payloads, unions rows and sums the
      integers exactly (= Gloo sparse all_reduce, torch-internal: coalesce, allgather,
@@ -33,13 +33,13 @@ class ExchangeKernels(Protocol):
     """The three device steps of the exchange (HIP by default; tests may inject a checker)."""
 
     def coalesce(self, batch: LookupBatch, dy: torch.Tensor, ws: CoalescedGrad, ste: bool,
-                 grad_bits: int, layout: str) -> None: ...
+                 layout: str) -> None: ...
 
-    def quant_pack(self, ws: CoalescedGrad, s_all: torch.Tensor, num_ranks: int, grad_bits: int,
-                   s_avg: torch.Tensor, payload: torch.Tensor) -> None: ...
+    def quant_pack(self, ws: CoalescedGrad, absmax_all: torch.Tensor, num_ranks: int, grad_bits: int,
+                   cap_base: torch.Tensor, cap_total: int, s_avg: torch.Tensor, payload: torch.Tensor) -> None: ...
 
-    def apply(self, ws: CoalescedGrad, gathered: torch.Tensor, payload_bytes: int, num_ranks: int,
-              grad_bits: int, s_avg: torch.Tensor, lr: float, mode: int, repack: bool) -> None: ...
+    def apply(self, cap_base: torch.Tensor, cap_total: int, gathered: torch.Tensor, payload_bytes: int,
+              num_ranks: int, grad_bits: int, s_avg: torch.Tensor, lr: float, mode: int, repack: bool) -> None: ...
 
 
 class HipExchangeKernels:
@@ -49,24 +49,24 @@ class HipExchangeKernels:
         self.tables = tables
         self.lib = tables.lib
 
-    def coalesce(self, batch, dy, ws, ste, grad_bits, layout):
-        self.tables.backward_coalesce(batch, dy, ws, ste=ste, grad_bits=grad_bits if grad_bits <= 16 else 0,
-                                      layout=layout)
+    def coalesce(self, batch, dy, ws, ste, layout):
+        self.tables.backward_coalesce(batch, dy, ws, ste=ste, layout=layout)
 
-    def quant_pack(self, ws, s_all, num_ranks, grad_bits, s_avg, payload):
+    def quant_pack(self, ws, absmax_all, num_ranks, grad_bits, cap_base, cap_total, s_avg, payload):
         t = self.tables
         L.check(
             self.lib.dqrm_grad_quant_pack(
-                t.T, t.D, _ptr(ws.cap_base), ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.counts),
-                _ptr(s_all), num_ranks, grad_bits, _ptr(s_avg), _ptr(payload), _stream_handle()),
+                t.T, t.D, _ptr(ws.slot_cap_base), ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount),
+                _ptr(absmax_all), num_ranks, grad_bits, _ptr(cap_base), cap_total, _ptr(s_avg), _ptr(payload),
+                _stream_handle()),
             "dqrm_grad_quant_pack",
         )
 
-    def apply(self, ws, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack):
+    def apply(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack):
         t = self.tables
         L.check(
             self.lib.dqrm_apply_sparse_update(
-                C.byref(t.c), _ptr(ws.cap_base), ws.cap_total, _ptr(gathered), payload_bytes, num_ranks,
+                C.byref(t.c), _ptr(cap_base), cap_total, _ptr(gathered), payload_bytes, num_ranks,
                 grad_bits, _ptr(s_avg), float(lr), mode, 4 if repack else 0, _stream_handle()),
             "dqrm_apply_sparse_update",
         )
@@ -80,14 +80,16 @@ def payload_bytes(num_tables: int, cap_total: int, dim: int, grad_bits: int) -> 
 
 
 class SparseGradExchange:
-    """Per-step DP embedding update: coalesce -> scale all-gather -> quantize-pack ->
-    payload all-gather -> decode + SGD.  One instance per rank, buffers reused every step.
+    """Per-step DP embedding update: coalesce -> all-gather of per-slot max|grad| ->
+    scale average + quantize-pack -> payload all-gather -> decode + SGD.
+    One instance per rank, buffers reused every step.
 
     grad_bits: 8 (scripts' --embedding_bag_gradient_bit_num=8), 2..16, or 32 for the
     unquantized sparse path (emb_grad_quantized=False, s_q_g_p_c.py:319-327).
+    max_lookups: upper bound of any table's lookups per rank per step (B x pooling).
     """
 
-    def __init__(self, tables: EmbeddingTableSet, caps, grad_bits: int = 8, group=None,
+    def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None,
                  kernels: ExchangeKernels | None = None, device=None):
         if not (grad_bits == 32 or 2 <= grad_bits <= 16):
             raise ValueError("grad_bits must be 2..16 or 32")
@@ -96,20 +98,22 @@ class SparseGradExchange:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
-        dev = device if device is not None else tables.device
-        self.device = torch.device(dev)
+        dev = torch.device(device if device is not None else tables.device)
+        self.device = dev
         self.kernels = kernels if kernels is not None else HipExchangeKernels(tables)
-        self.ws = CoalescedGrad.allocate(caps, tables.D, self.device)
         T = tables.T
-        self.payload_bytes = payload_bytes(T, self.ws.cap_total, tables.D, grad_bits)
-        self.s_all = torch.zeros(self.world, T, dtype=torch.float32, device=self.device)
-        self.s_avg = torch.zeros(T, dtype=torch.float32, device=self.device)
-        self.payload = torch.zeros(self.payload_bytes, dtype=torch.uint8, device=self.device)
-        self.gathered = torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8, device=self.device)
-
-    @classmethod
-    def for_batch_shape(cls, tables: EmbeddingTableSet, max_lookups_per_table: int, **kw):
-        return cls(tables, default_caps(tables.num_rows, max_lookups_per_table), **kw)
+        self.ws = CoalescedGrad.allocate(tables.num_rows, max_lookups, tables.D, dev)
+        self.caps = default_caps(tables.num_rows, max_lookups)
+        base = [0]
+        for c in self.caps:
+            base.append(base[-1] + c)
+        self.cap_total = base[-1]
+        self.cap_base = torch.tensor(base, dtype=torch.int64, device=dev)
+        self.payload_bytes = payload_bytes(T, self.cap_total, tables.D, grad_bits)
+        self.absmax_all = torch.zeros(self.world, T * L.DQRM_TABLE_SPLIT, dtype=torch.float32, device=dev)
+        self.s_avg = torch.zeros(T, dtype=torch.float32, device=dev)
+        self.payload = torch.zeros(self.payload_bytes, dtype=torch.uint8, device=dev)
+        self.gathered = torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8, device=dev)
 
     # -------------------------------------------------------------- collectives
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
@@ -123,22 +127,45 @@ class SparseGradExchange:
             dist.all_gather(list(out.unbind(0)), inp, group=self.group)
 
     # -------------------------------------------------------------- the step
-    def step(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
-             mode: int | None = None, repack: bool = False, layout: str = "tbd") -> None:
-        """grad_update_parallel_comm + weight_update_parallel_comm for all tables."""
+    def exchange(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True, layout: str = "tbd") -> torch.Tensor:
+        """grad_update_parallel_comm's embedding branch (s_q_g_p_c.py:278-315 via :850-890):
+        coalesce, all-gather the scale inputs, quantize-pack, all-gather the payloads.
+        Returns the per-table averaged gradient scale (emb_scaling_factor)."""
+        gb = self.grad_bits
+        k = self.kernels
+        k.coalesce(batch, dy, self.ws, ste, layout)
+        if gb != 32 and self.world > 1:
+            self._all_gather(self.absmax_all, self.ws.absmax)
+            absmax_all = self.absmax_all
+        else:
+            absmax_all = self.ws.absmax.view(1, -1)
+        k.quant_pack(self.ws, absmax_all, self.world, gb, self.cap_base, self.cap_total, self.s_avg, self.payload)
+        if self.world > 1:
+            self._all_gather(self.gathered, self.payload)
+        return self.s_avg
+
+    def apply(self, lr: float, mode: int | None = None, repack: bool = False) -> None:
+        """weight_update_parallel_comm's embedding branch (s_q_g_p_c.py:601-628)."""
         gb = self.grad_bits
         if mode is None:
             mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
-        self.kernels.coalesce(batch, dy, self.ws, ste, gb, layout)
-        if gb != 32:
-            self._all_gather(self.s_all, self.ws.s_loc)
-        self.kernels.quant_pack(self.ws, self.s_all, self.world, gb, self.s_avg, self.payload)
-        if self.world == 1:
-            gathered = self.payload.view(1, -1)
-        else:
-            self._all_gather(self.gathered, self.payload)
-            gathered = self.gathered
-        self.kernels.apply(self.ws, gathered, self.payload_bytes, self.world, gb, self.s_avg, lr, mode, repack)
+        gathered = self.payload.view(1, -1) if self.world == 1 else self.gathered
+        self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, gb, self.s_avg,
+                           lr, mode, repack)
+
+    def step(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
+             mode: int | None = None, repack: bool = False, layout: str = "tbd") -> None:
+        """grad_update_parallel_comm + weight_update_parallel_comm for all tables."""
+        self.exchange(batch, dy, ste=ste, layout=layout)
+        self.apply(lr, mode=mode, repack=repack)
+
+    def local_scales(self) -> torch.Tensor:
+        """This rank's per-table gradient scale s_loc (host-side view for inspection)."""
+        import numpy as np
+
+        a = self.ws.absmax.view(self.tables.T, L.DQRM_TABLE_SPLIT).max(dim=1).values.cpu().numpy()
+        a = np.maximum(a.astype(np.float32), np.float32(1e-8))
+        return torch.from_numpy(a / np.float32(2 ** (self.grad_bits - 1) - 1))
 
 
 def get_my_slice(n: int, my_size: int, my_rank: int) -> slice:

@@ -52,8 +52,6 @@ int set_error(int code, const char* fmt, ...) {
 constexpr int WAVE = 64;
 constexpr int BLK = DQRM_BLOCK_ROWS;     // 256
 constexpr int SBLK_BLOCKS = 256;         // blocks per superblock
-constexpr int TABLE_WG = 1024;           // threads of a per-table workgroup
-constexpr int MAX_LDS_KEYS = 16384;      // per-table on-chip sort capacity (128 KiB of keys)
 constexpr int MAX_TABLES = 256;
 
 // ------------------------------------------------------------------------------------
@@ -287,72 +285,59 @@ struct FwdArgs {
 
 template <int LPR, int UNR>
 __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
-    __shared__ float s_scale[MAX_TABLES];
-    __shared__ float s_rcp[MAX_TABLES];
-    __shared__ int64_t s_rowbase[MAX_TABLES];
-    __shared__ int64_t s_nrows[MAX_TABLES];
-    __shared__ int64_t s_ibase[MAX_TABLES + 1];
-    const int T = a.T;
+    // grid = (bag chunks, tables): the table index is blockIdx.y, so every per-table value
+    // below is wave-uniform (scalar registers) and no 64-bit division is needed per bag.
+    const int t = blockIdx.y;
     const bool full_precision = (a.flags & DQRM_FWD_FULL_PRECISION) != 0;
     const bool refresh = (a.flags & DQRM_FWD_REFRESH_SCALE) != 0;
     const bool use_packed = (a.flags & DQRM_FWD_USE_PACKED) != 0 && !full_precision;
-    const bool bag_major = (a.flags & DQRM_FWD_BAG_MAJOR) != 0;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        float s = 1.0f;
-        if (!full_precision) s = refresh ? sym_scale(a.tmax[t], a.bits) : a.scale[t];
-        s_scale[t] = s;
-        s_rcp[t] = 1.0f / s;
-        s_rowbase[t] = a.meta[t];
-        s_nrows[t] = a.meta[T + t];
-        s_ibase[t] = a.idx_base[t];
-        if (refresh && !full_precision && blockIdx.x == 0) a.scale[t] = s;
-    }
-    if (threadIdx.x == 0) s_ibase[T] = a.idx_base[T];
-    __syncthreads();
+    float s = 1.0f;
+    if (!full_precision) s = refresh ? sym_scale(a.tmax[t], a.bits) : a.scale[t];
+    const float r = 1.0f / s;
+    if (refresh && !full_precision && blockIdx.x == 0 && threadIdx.x == 0) a.scale[t] = s;
+    const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
+    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    const int64_t B = a.B;
+    const int64_t* __restrict__ off = a.off + (int64_t)t * B;
+    const int64_t* __restrict__ idx = a.idx + ibase;
+    float* __restrict__ out = a.out + (int64_t)t * a.ost_t;
 
     const float qlo = -(float)(1 << (a.bits - 1));
     const float qhi = (float)((1 << (a.bits - 1)) - 1);
+    constexpr int G = 256 / LPR;  // bags per workgroup pass
     const int lane = threadIdx.x % LPR;
-    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
-    const int64_t total = (int64_t)T * a.B;
+    const int grp = threadIdx.x / LPR;
     const int D = LPR * 4;
 
-    for (int64_t u0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; u0 < total;
-         u0 += ngrp * UNR) {
-        int tt[UNR];
-        int64_t bb[UNR], beg[UNR], len[UNR], row[UNR];
-        bool valid[UNR];
+    for (int64_t b0 = (int64_t)blockIdx.x * (G * UNR); b0 < B; b0 += (int64_t)gridDim.x * (G * UNR)) {
+        int64_t beg[UNR], len[UNR], row[UNR];
         // phase 1: offsets
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
-            int64_t u = u0 + (int64_t)k * ngrp;
-            valid[k] = u < total;
-            if (!valid[k]) u = 0;
-            int t; int64_t b;
-            if (bag_major) { b = u / T; t = (int)(u - b * T); }
-            else { t = (int)(u / a.B); b = u - (int64_t)t * a.B; }
-            tt[k] = t; bb[k] = b;
-            const int64_t L = s_ibase[t + 1] - s_ibase[t];
-            int64_t s0 = a.off[(int64_t)t * a.B + b];
-            int64_t s1 = (b + 1 < a.B) ? a.off[(int64_t)t * a.B + b + 1] : L;
+            const int64_t b = b0 + k * G + grp;
+            const bool valid = b < B;
+            const int64_t bb = valid ? b : 0;
+            int64_t s0 = off[bb];
+            int64_t s1 = (bb + 1 < B) ? off[bb + 1] : L;
             if (s0 < 0 || s1 > L || s1 < s0) {
-                if (valid[k] && lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
+                if (valid && lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
                 s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
                 s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
             }
-            beg[k] = s0; len[k] = valid[k] ? s1 - s0 : 0;
+            beg[k] = s0;
+            len[k] = valid ? s1 - s0 : -1;  // -1: no such bag
         }
         // phase 2: single-lookup indices
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
             row[k] = -1;
             if (len[k] == 1) {
-                int64_t r = a.idx[s_ibase[tt[k]] + beg[k]];
-                if (r < 0 || r >= s_nrows[tt[k]]) {
+                int64_t rr = idx[beg[k]];
+                if (rr < 0 || rr >= nrows) {
                     if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
-                    r = -1;
+                    rr = -1;
                 }
-                row[k] = r;
+                row[k] = rr;
             }
         }
         // phase 3: row loads for single-lookup bags
@@ -363,7 +348,7 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             pk[k] = 0x8888u;  // q = 0
             if (row[k] >= 0) {
-                const int64_t grow = s_rowbase[tt[k]] + row[k];
+                const int64_t grow = rowbase + row[k];
                 if (use_packed)
                     pk[k] = reinterpret_cast<const uint16_t*>(a.packed + grow * (D / 2))[lane];
                 else
@@ -373,9 +358,7 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
         // phase 4: pooled sums for multi-lookup bags (bag order, FP32), quantize, store
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
-            if (!valid[k]) continue;
-            const int t = tt[k];
-            const float s = s_scale[t], r = s_rcp[t];
+            if (len[k] < 0) continue;
             float4 y;
             if (len[k] == 1 && use_packed) {
                 const uint32_t p = pk[k];
@@ -386,16 +369,14 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
             } else {
                 float4 v = acc[k];
                 if (len[k] > 1) {
-                    const int64_t ib = s_ibase[t] + beg[k];
-                    const int64_t nr = s_nrows[t], rb = s_rowbase[t];
                     v = make_float4(0.f, 0.f, 0.f, 0.f);
                     for (int64_t i = 0; i < len[k]; ++i) {
-                        int64_t rr = a.idx[ib + i];
-                        if (rr < 0 || rr >= nr) {
+                        const int64_t rr = idx[beg[k] + i];
+                        if (rr < 0 || rr >= nrows) {
                             if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
                             continue;
                         }
-                        float4 w = reinterpret_cast<const float4*>(a.W + (rb + rr) * D)[lane];
+                        const float4 w = reinterpret_cast<const float4*>(a.W + (rowbase + rr) * D)[lane];
                         v.x = v.x + w.x; v.y = v.y + w.y; v.z = v.z + w.z; v.w = v.w + w.w;
                     }
                 }
@@ -408,25 +389,164 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
                     y.w = fake_quant(v.w, r, qlo, qhi) * s;
                 }
             }
-            float* o = a.out + (int64_t)t * a.ost_t + bb[k] * a.ost_b;
-            reinterpret_cast<float4*>(o)[lane] = y;
+            const int64_t b = b0 + k * G + grp;
+            reinterpret_cast<float4*>(out + b * a.ost_b)[lane] = y;
         }
     }
 }
 
 // ------------------------------------------------------------------------------------
-// Per-table workgroup machinery (backward / coalesce / apply):
-// keys = (local_row << 32) | tag sorted in LDS (bitonic), segments = equal rows.
+// K3p: INT4 packed forward, one bag per thread, three lane-parallel phases per 256 bags:
+//   (1) offsets + single-lookup index for 256 consecutive bags (coalesced),
+//   (2) 256 independent packed-row loads (D/2 bytes, lane per bag) staged in LDS,
+//   (3) dequantize + store: LPR lanes x float4 per output row (full-line, coalesced).
+// Bags that do not hold exactly one valid lookup take the exact FP32 fake-quant path in
+// phase 3. The row loads no longer sit behind a per-group dependent chain, so the kernel
+// runs at the output-write stream rate.
 // ------------------------------------------------------------------------------------
+template <int LPR, bool NT>
+__global__ void __launch_bounds__(256) k_emb_fwd_packed(FwdArgs a) {
+    constexpr int D = LPR * 4;
+    constexpr int PB = D / 2;                 // packed bytes per row
+    constexpr int PW = PB / 4 > 0 ? PB / 4 : 1;  // dwords per packed row (D >= 8)
+    __shared__ __attribute__((aligned(16))) uint32_t s_pk[256 * PW + 4];
+    __shared__ int64_t s_beg[256];
+    __shared__ int s_len[256];
+    const int t = blockIdx.y;
+    const float s = a.scale[t];               // frozen scale the rows were packed with
+    const float r = 1.0f / s;
+    const float qlo = -(float)(1 << (a.bits - 1)), qhi = (float)((1 << (a.bits - 1)) - 1);
+    const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
+    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    const int64_t B = a.B;
+    const int64_t* __restrict__ off = a.off + (int64_t)t * B;
+    const int64_t* __restrict__ idx = a.idx + ibase;
+    float* __restrict__ out = a.out + (int64_t)t * a.ost_t;
+    const int tid = threadIdx.x;
+
+    for (int64_t b0 = (int64_t)blockIdx.x * 256; b0 < B; b0 += (int64_t)gridDim.x * 256) {
+        // phase 1: one bag per thread
+        const int64_t b = b0 + tid;
+        int64_t s0 = 0, s1 = 0;
+        int len = -1;
+        int64_t row = -1;
+        if (b < B) {
+            s0 = off[b];
+            s1 = (b + 1 < B) ? off[b + 1] : L;
+            if (s0 < 0 || s1 > L || s1 < s0) {
+                flag_error(a.err, DQRM_ERRF_OFFSET);
+                s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+                s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+            }
+            len = (int)(s1 - s0 > 0x7fffffff ? 0x7fffffff : s1 - s0);
+            if (len == 1) {
+                row = idx[s0];
+                if (row < 0 || row >= nrows) {
+                    flag_error(a.err, DQRM_ERRF_INDEX);
+                    row = -1;
+                    len = 0;  // an invalid lookup contributes nothing (zero row)
+                }
+            }
+        }
+        // phase 2: packed row -> LDS
+        uint32_t pk[PW];
+        if (len == 1) {
+            const uint8_t* src = a.packed + (rowbase + row) * PB;
+            if constexpr (PB >= 16) {
+#pragma unroll
+                for (int q = 0; q < PB / 16; ++q) {
+                    const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+                    pk[4 * q] = v.x; pk[4 * q + 1] = v.y; pk[4 * q + 2] = v.z; pk[4 * q + 3] = v.w;
+                }
+            } else if constexpr (PB == 8) {
+                const uint2 v = *reinterpret_cast<const uint2*>(src);
+                pk[0] = v.x; pk[1] = v.y;
+            } else {
+                pk[0] = *reinterpret_cast<const uint32_t*>(src);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < PW; ++q) pk[q] = 0x88888888u;
+        }
+        __syncthreads();  // previous pass's phase 3 is done with the LDS
+#pragma unroll
+        for (int q = 0; q < PW; ++q) s_pk[tid * PW + q] = pk[q];
+        s_len[tid] = len;
+        s_beg[tid] = s0;
+        __syncthreads();
+        // phase 3: LPR lanes per bag, float4 each
+        constexpr int G = 256 / LPR;
+        const int lane = tid % LPR, grp = tid / LPR;
+        for (int j = grp; j < 256; j += G) {
+            const int64_t bb = b0 + j;
+            const int ln = s_len[j];
+            if (ln < 0) break;  // past the last bag (uniform per group: bags are in order)
+            float4 y;
+            if (ln == 1 || ln == 0) {
+                const uint32_t w = reinterpret_cast<const uint16_t*>(s_pk + j * PW)[lane];
+                y.x = (float)((int)(w & 15u) - 8) * s;
+                y.y = (float)((int)((w >> 4) & 15u) - 8) * s;
+                y.z = (float)((int)((w >> 8) & 15u) - 8) * s;
+                y.w = (float)((int)((w >> 12) & 15u) - 8) * s;
+            } else {  // multi-lookup bag: exact FP32 sum in bag order, then fake-quant
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                const int64_t sb = s_beg[j];
+                for (int i = 0; i < ln; ++i) {
+                    const int64_t rr = idx[sb + i];
+                    if (rr < 0 || rr >= nrows) {
+                        if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+                        continue;
+                    }
+                    const float4 w = reinterpret_cast<const float4*>(a.W + (rowbase + rr) * D)[lane];
+                    v.x = v.x + w.x; v.y = v.y + w.y; v.z = v.z + w.z; v.w = v.w + w.w;
+                }
+                y.x = fake_quant(v.x, r, qlo, qhi) * s;
+                y.y = fake_quant(v.y, r, qlo, qhi) * s;
+                y.z = fake_quant(v.z, r, qlo, qhi) * s;
+                y.w = fake_quant(v.w, r, qlo, qhi) * s;
+            }
+            float4* dst = reinterpret_cast<float4*>(out + bb * a.ost_b) + lane;
+            if (NT) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                v4f yv = {y.x, y.y, y.z, y.w};
+                __builtin_nontemporal_store(yv, reinterpret_cast<v4f*>(dst));
+            } else {
+                *dst = y;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Per-table workgroup machinery (backward / coalesce / apply).
+// Each table is split into DQRM_TABLE_SPLIT row-range slots (block-aligned); one
+// 512-thread workgroup per (table, slot) gathers the lookups (or payload entries) of its
+// rows as keys (row << 32 | tag) in LDS, sorts them (bitonic), compacts the segment heads
+// (= unique rows) and processes every segment in exact sequential order.
+// ------------------------------------------------------------------------------------
+constexpr int SPLIT = DQRM_TABLE_SPLIT;
+constexpr int TWG = 512;                       // threads per (table, slot) workgroup
+constexpr int SLOT_KEYS = DQRM_SLOT_KEYS;      // keys one slot sorts on chip (64 KiB)
+constexpr int TILE_FLOATS = 2048;              // per-wave LDS tile for long segments (8 KiB)
+// dynamic LDS of a slot workgroup: keys u64 | heads u16 | one tile per wave  (144 KiB)
+constexpr int SLOT_LDS = SLOT_KEYS * 8 + SLOT_KEYS * 2 + (TWG / WAVE) * TILE_FLOATS * 4;
+
 DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
 DQRM_INLINE uint32_t key_lo(uint64_t k) { return (uint32_t)k; }
 DQRM_INLINE uint64_t with_lo(uint64_t k, uint32_t lo) { return (k & 0xFFFFFFFF00000000ull) | lo; }
 
+DQRM_INLINE int next_pow2(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
 DQRM_INLINE void bitonic_sort_lds(uint64_t* keys, int n_pow2) {
     for (int k = 2; k <= n_pow2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
+            const int lj = __builtin_ctz(j);
             for (int p = threadIdx.x; p < (n_pow2 >> 1); p += blockDim.x) {
-                const int i = ((p / j) * 2 * j) + (p % j);
+                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1));  // j is a power of two
                 const int l = i + j;
                 uint64_t x = keys[i], y = keys[l];
                 const bool up = (i & k) == 0;
@@ -437,64 +557,67 @@ DQRM_INLINE void bitonic_sort_lds(uint64_t* keys, int n_pow2) {
     }
 }
 
-DQRM_INLINE int next_pow2(int n) {
-    int p = 1;
-    while (p < n) p <<= 1;
-    return p;
+// rows [r0, r1) of slot s of a table with nrows rows (block-aligned split)
+DQRM_INLINE void slot_rows(int64_t nrows, int s, int64_t& r0, int64_t& r1) {
+    const int64_t nblk = ceil_div(nrows, BLK);
+    const int64_t b0 = nblk * s / SPLIT, b1 = nblk * (s + 1) / SPLIT;
+    r0 = b0 * BLK;
+    r1 = b1 * BLK < nrows ? b1 * BLK : nrows;
 }
 
-// block-wide exclusive scan of head flags: returns per-thread chunk base (LDS) so that
-// the unique ordinal of a head at position i = base[i / CH] + heads in [CH*(i/CH), i)
-template <int CH>
-DQRM_INLINE int head_scan(const uint64_t* keys, int n, int* s_base, int* s_wtot) {
-    const int tid = threadIdx.x;
-    int cnt = 0;
+// sort the n keys already in LDS, then compact segment heads: heads[u] = first key of the
+// u-th distinct row. Returns U. (heads are u16: n <= SLOT_KEYS <= 65536)
+DQRM_INLINE int sort_and_heads(uint64_t* keys, uint16_t* heads, int n, int* s_wsum) {
+    const int np2 = next_pow2(n < 2 ? 2 : n);
+    for (int i = n + threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_lds(keys, np2);
+    // compact heads with a block-wide scan over chunks of CH keys per thread
+    constexpr int CH = SLOT_KEYS / TWG;
+    const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
     const int i0 = tid * CH;
-#pragma unroll 4
+    int cnt = 0;
     for (int c = 0; c < CH; ++c) {
-        int i = i0 + c;
+        const int i = i0 + c;
         if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
     }
     int v = cnt;
-    const int lane = tid % WAVE, w = tid / WAVE;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
         int y = __shfl_up(v, o, WAVE);
         if (lane >= o) v += y;
     }
-    if (lane == WAVE - 1) s_wtot[w] = v;
+    if (lane == WAVE - 1) s_wsum[w] = v;
     __syncthreads();
     if (tid == 0) {
         int run = 0;
-        for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wtot[k]; s_wtot[k] = run; run += x; }
-        s_wtot[blockDim.x / WAVE] = run;
+        for (int k = 0; k < TWG / WAVE; ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
+        s_wsum[TWG / WAVE] = run;
     }
     __syncthreads();
-    s_base[tid] = s_wtot[w] + v - cnt;
+    int u = s_wsum[w] + v - cnt;
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) heads[u++] = (uint16_t)i;
+    }
     __syncthreads();
-    return s_wtot[blockDim.x / WAVE];
+    return s_wsum[TWG / WAVE];
 }
 
-template <int CH>
-DQRM_INLINE int head_ordinal(const uint64_t* keys, const int* s_base, int i) {
-    const int c0 = (i / CH) * CH;
-    int u = s_base[i / CH];
-    for (int j = c0; j < i; ++j)
-        if (j == 0 || key_row(keys[j]) != key_row(keys[j - 1])) ++u;
-    return u;
+DQRM_INLINE int seg_end(const uint16_t* heads, int U, int n, int u) {
+    return u + 1 < U ? (int)heads[u + 1] : n;
 }
 
 // ------------------------------------------------------------------------------------
 // Segment reduction in exact sequential order.
-// A segment = the sorted keys of one row; its entries must be combined strictly in key
-// order (ascending lookup position / rank) to reproduce the reference's rounding:
+// A segment = the sorted keys of one row; its entries are combined strictly in key order
+// (ascending lookup position, or ascending rank) to reproduce the reference's rounding:
 //   OP_FMA  acc = fma(v, -lr, acc) per entry          (torch CPU sparse SGD axpy)
 //   OP_SUM  acc = v0; acc = acc + v_k                  (coalesce / sparse all_reduce)
 // Short segments: one lane group (LPR lanes x float4), 4 entries in flight per chunk.
-// Long segments (> LONG_SEG entries, tiny hot tables): a whole wave loads WAVE/LPR entries
-// per chunk (next chunk prefetched) and combines them in order through shuffles.
-// Masked entries load the head's own row, so they never address out of bounds and cost
-// no extra memory traffic.
+// Long segments (> LONG_SEG entries, tiny hot tables): a whole wave loads 4*WAVE/LPR
+// entries per chunk (the next chunk prefetched) and combines them in order via shuffles.
+// Masked entries re-load the head's own entry, so they never address out of bounds.
 // ------------------------------------------------------------------------------------
 constexpr int LONG_SEG = 32;
 constexpr int OP_FMA = 0;
@@ -514,258 +637,342 @@ DQRM_INLINE float4 combine(float4 acc, float4 v, bool& first, float nlr) {
     return acc;
 }
 
-DQRM_INLINE bool is_head(const uint64_t* keys, int i) {
-    return i == 0 || key_row(keys[i - 1]) != key_row(keys[i]);
-}
-
-DQRM_INLINE bool is_long(const uint64_t* keys, int n, int i, uint32_t row) {
-    return i + LONG_SEG < n && key_row(keys[i + LONG_SEG]) == row;
-}
-
 template <int LPR, int OP, class Src>
-DQRM_INLINE float4 seg_reduce_group(const uint64_t* keys, int n, int i, uint32_t row, float4 acc,
-                                    const Src& src, float nlr, int sub) {
+DQRM_INLINE float4 seg_reduce_group(const uint64_t* keys, int i, int len, float4 acc, const Src& src,
+                                    float nlr, int sub) {
     const uint32_t head_lo = key_lo(keys[i]);
     bool first = true;
-    for (int j = i;; j += 4) {
+    for (int j = 0; j < len; j += 4) {
         float4 v[4];
-        bool m[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int jj = j + c;
-            const uint64_t kk = jj < n ? keys[jj] : ~0ull;
-            m[c] = key_row(kk) == row;
-            v[c] = src.load(m[c] ? key_lo(kk) : head_lo, sub);
+            v[c] = src.load(jj < len ? key_lo(keys[i + jj]) : head_lo, sub);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (m[c]) acc = combine<OP>(acc, v[c], first, nlr);
-        }
-        if (!m[3]) break;
+        for (int c = 0; c < 4; ++c)
+            if (j + c < len) acc = combine<OP>(acc, v[c], first, nlr);
     }
     return acc;
+}
+
+// Long segments: lane-owned dimensions. Lane l owns dims l, l+64, ... of the row; the wave
+// stages CH = TILE_FLOATS/D entries at a time in its LDS tile (8 float4 loads per lane,
+// coalesced, the next chunk in flight while the current one is reduced) and every lane
+// walks the tile's entries in order for its own dims: no shuffles, no per-entry branches.
+template <int LPR>
+struct LaneRow {
+    static constexpr int D = LPR * 4;
+    static constexpr int NDL = (D + WAVE - 1) / WAVE;
+    float v[NDL];
+};
+
+// Order one wave's LDS writes before its own later LDS reads (and vice versa). A wave's
+// DS instructions execute in order, so only the compiler must be stopped from moving
+// them; no s_waitcnt on the vector-memory counter is wanted here (it would drain the
+// prefetched global loads).
+DQRM_INLINE void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+template <int OP>
+DQRM_INLINE float combine1(float acc, float v, bool first, float nlr) {
+    if (OP == OP_FMA) return fmaf(v, nlr, acc);
+    return first ? v : acc + v;
 }
 
 template <int LPR, int OP, class Src>
-DQRM_INLINE float4 seg_reduce_wave(const uint64_t* keys, int n, int i, uint32_t row, float4 acc,
-                                   const Src& src, float nlr) {
-    constexpr int G = WAVE / LPR;
+DQRM_INLINE LaneRow<LPR> seg_reduce_tile(const uint64_t* keys, int i, int len, LaneRow<LPR> acc,
+                                         const Src& src, float nlr, float* tile) {
+    constexpr int D = LPR * 4;
+    constexpr int CH = TILE_FLOATS / D;             // entries per chunk
+    constexpr int F4 = TILE_FLOATS / 4 / WAVE;      // float4 loads per lane per chunk (8)
+    constexpr int NDL = LaneRow<LPR>::NDL;
     const int lane = threadIdx.x % WAVE;
-    const int g = lane / LPR, sub = lane % LPR;
     const uint32_t head_lo = key_lo(keys[i]);
-    bool first = true;
-    int j = i;
-    auto fetch = [&](int jb, float4& v, bool& ok) {
-        const int jj = jb + g;
-        const uint64_t kk = jj < n ? keys[jj] : ~0ull;
-        ok = key_row(kk) == row;
-        v = src.load(ok ? key_lo(kk) : head_lo, sub);
-    };
-    float4 v0;
-    bool ok0;
-    fetch(j, v0, ok0);
-    for (;;) {
-        float4 v1;
-        bool ok1;
-        fetch(j + G, v1, ok1);  // prefetch the next chunk before combining this one
-        const uint64_t msk = __ballot(ok0);
+    float4 buf[F4];
+    auto load_chunk = [&](int j0) {
 #pragma unroll
-        for (int k = 0; k < G; ++k) {
-            if (!((msk >> (k * LPR)) & 1ull)) break;  // wave-uniform
-            float4 x;
-            x.x = __shfl(v0.x, k * LPR + sub, WAVE);
-            x.y = __shfl(v0.y, k * LPR + sub, WAVE);
-            x.z = __shfl(v0.z, k * LPR + sub, WAVE);
-            x.w = __shfl(v0.w, k * LPR + sub, WAVE);
-            acc = combine<OP>(acc, x, first, nlr);
+        for (int f = 0; f < F4; ++f) {
+            const int flat = f * WAVE + lane;        // float4 index in the tile = e * LPR + q
+            const int e = flat / LPR, q = flat % LPR;
+            const int jj = j0 + e;
+            buf[f] = src.load(jj < len ? key_lo(keys[i + jj]) : head_lo, q);
         }
-        if (!((msk >> ((G - 1) * LPR)) & 1ull)) break;
-        v0 = v1;
-        ok0 = ok1;
-        j += G;
+    };
+    load_chunk(0);
+    bool first = true;
+    for (int j = 0; j < len; j += CH) {
+        wave_lds_sync();  // previous chunk fully read before it is overwritten
+#pragma unroll
+        for (int f = 0; f < F4; ++f) reinterpret_cast<float4*>(tile)[f * WAVE + lane] = buf[f];
+        wave_lds_sync();
+        if (j + CH < len) load_chunk(j + CH);      // wave-uniform; overlaps the walk below
+        const int cnt = len - j < CH ? len - j : CH;
+        for (int e = 0; e < cnt; e += 8) {
+#pragma unroll
+            for (int d = 0; d < NDL; ++d) {
+                const int dim = lane + WAVE * d;
+                if (dim >= D) continue;
+                float v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = tile[((e + k) % CH) * D + dim];  // 8 reads in flight
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (e + k < cnt) acc.v[d] = combine1<OP>(acc.v[d], v[k], first && k == 0 && e == 0, nlr);
+            }
+            first = false;
+        }
     }
+    wave_lds_sync();
     return acc;
 }
 
-// Visit every segment head once: short segments by lane groups (strided), long ones by
-// whole waves. fn(i, row, sub, writer, wave_mode) runs the per-row epilogue; it calls the
-// matching seg_reduce_* itself (so the initial accumulator can be loaded first).
-template <int LPR, class Fn>
-DQRM_INLINE void for_each_segment(const uint64_t* keys, int n, Fn&& fn) {
+template <int LPR>
+DQRM_INLINE LaneRow<LPR> load_lane_row(const float* row) {
+    LaneRow<LPR> r;
+    const int lane = threadIdx.x % WAVE;
+#pragma unroll
+    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) {
+        const int dim = lane + WAVE * d;
+        r.v[d] = dim < LPR * 4 ? row[dim] : 0.0f;
+    }
+    return r;
+}
+
+template <int LPR>
+DQRM_INLINE void store_lane_row(float* row, const LaneRow<LPR>& r) {
+    const int lane = threadIdx.x % WAVE;
+#pragma unroll
+    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) {
+        const int dim = lane + WAVE * d;
+        if (dim < LPR * 4) row[dim] = r.v[d];
+    }
+}
+
+template <int LPR>
+DQRM_INLINE float lane_row_absmax(const LaneRow<LPR>& r) {
+    float m = 0.0f;
+#pragma unroll
+    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) m = fmaxf(m, fabsf(r.v[d]));
+    return wave_max(m);
+}
+
+// repack a lane-owned row: stage it in the wave's tile, lanes 0..LPR-1 pack float4 slices
+template <int LPR>
+DQRM_INLINE void pack_lane_row(const LaneRow<LPR>& r, float* tile, uint8_t* packed, int64_t grow, float rcp) {
+    const int lane = threadIdx.x % WAVE;
+    wave_lds_sync();
+    store_lane_row<LPR>(tile, r);
+    wave_lds_sync();
+    if (lane < LPR) pack_row_int4<LPR>(reinterpret_cast<const float4*>(tile)[lane], packed, grow, lane, rcp);
+    wave_lds_sync();
+}
+
+// Visit every segment once: short ones by lane groups (strided over heads) through
+// fg(u, i, len, sub); long ones by whole waves through fw(u, i, len) (all 64 lanes).
+constexpr int LONG_SEGS_MAX = SLOT_KEYS / (LONG_SEG + 1) + 1;
+
+template <int LPR, class FG, class FW>
+DQRM_INLINE void for_each_segment(const uint16_t* heads, int U, int n, uint16_t* s_long, int* s_nlong,
+                                  FG&& fg, FW&& fw) {
     const int sub = threadIdx.x % LPR;
     const int grp = threadIdx.x / LPR;
     const int ngrp = blockDim.x / LPR;
-    for (int i = grp; i < n; i += ngrp) {
-        if (!is_head(keys, i)) continue;
-        const uint32_t row = key_row(keys[i]);
-        if (is_long(keys, n, i, row)) continue;
-        fn(i, row, sub, true, false);
+    for (int u = grp; u < U; u += ngrp) {
+        const int i = heads[u];
+        const int len = seg_end(heads, U, n, u) - i;
+        if (len > LONG_SEG) continue;
+        fg(u, i, len, sub);
     }
+    // long segments: compact their head ordinals, then deal them round-robin to the waves
+    // (a segment > LONG_SEG entries long means at most n / (LONG_SEG+1) <= LONG_SEGS_MAX of them)
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    for (int base = w * WAVE; base < n; base += nw * WAVE) {
-        const int i = base + lane;
-        bool lh = false;
-        if (i < n && is_head(keys, i)) lh = is_long(keys, n, i, key_row(keys[i]));
-        uint64_t msk = __ballot(lh);
-        while (msk) {
-            const int l = __ffsll((long long)msk) - 1;
-            msk &= msk - 1;
-            const int h = base + l;
-            fn(h, key_row(keys[h]), lane % LPR, lane < LPR, true);
-        }
+    if (threadIdx.x == 0) *s_nlong = 0;
+    __syncthreads();
+    for (int base = w * WAVE; base < U; base += nw * WAVE) {
+        const int u = base + lane;
+        const bool lg = u < U && (seg_end(heads, U, n, u) - (int)heads[u]) > LONG_SEG;
+        const uint64_t msk = __ballot(lg);
+        int off = 0;
+        if (lane == 0 && msk) off = atomicAdd(s_nlong, __popcll(msk));
+        off = __shfl(off, 0, WAVE);
+        if (lg) s_long[off + __popcll(msk & ((1ull << lane) - 1))] = (uint16_t)u;
+    }
+    __syncthreads();
+    const int nlong = *s_nlong;
+    for (int k = w; k < nlong; k += nw) {
+        const int uu = s_long[k];
+        const int i = heads[uu];
+        fw(uu, i, seg_end(heads, U, n, uu) - i);
     }
 }
 
 // ------------------------------------------------------------------------------------
-// Incremental |W| hierarchy maintenance (exact).
-// Before it runs, every segment head's key carries the row's OLD rowmax in its low bits
-// (the row epilogue swaps it in once the segment has been read). A block's new max is
-// max(old blkmax, new rowmax of its touched rows) unless one of those rows held the old
-// max and shrank; only then the block's 256 rowmax are re-read. Same one level up with
-// the block-start keys carrying the old blkmax. The table max re-reduces its superblocks.
+// Incremental |W| hierarchy maintenance (exact), per slot.
+// Before it runs, every head key carries its row's OLD rowmax in the low bits. A block's
+// new max is max(old blkmax, new rowmax of its touched rows) unless one of those rows held
+// the old max and shrank (then the block's 256 rowmax are re-read). The slot owns its
+// blocks; superblocks can be shared between slots: increases go in with an order-free
+// atomicMax on the (non-negative) float bits, a holder that shrank flags the superblock,
+// and k_table_finalize re-reduces flagged superblocks and the table max.
 // ------------------------------------------------------------------------------------
-DQRM_INLINE void maintain_hierarchy(const Meta& m, int t, uint64_t* keys, int n,
-                                    const float* rowmax, float* blkmax, float* sblkmax,
-                                    float* tmax, float* s_red) {
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+DQRM_INLINE void maintain_blocks(const Meta& m, int t, const uint64_t* keys, const uint16_t* heads,
+                                 int U, const float* rowmax, float* blkmax, float* sblkmax,
+                                 uint8_t* sdirty) {
     const int64_t nrows = m.num_rows[t];
-    const int64_t nblk = ceil_div(nrows, BLK);
-    const int64_t nsblk = ceil_div(nblk, SBLK_BLOCKS);
     const int64_t rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
-    // level 1: blocks
-    for (int base = w * WAVE; base < n; base += nw * WAVE) {
-        const int i = base + lane;
-        const bool start = i < n && (i == 0 || (key_row(keys[i - 1]) >> 8) != (key_row(keys[i]) >> 8));
-        uint64_t msk = __ballot(start);
-        while (msk) {
-            const int l = __ffsll((long long)msk) - 1;
-            msk &= msk - 1;
-            const int i0 = base + l;
-            const uint32_t blk = key_row(keys[i0]) >> 8;
-            const float old_blk = blkmax[bb + blk];
-            bool dec = false;
-            float cand = 0.0f;
-            for (int p0 = i0;; p0 += WAVE) {
-                const int p = p0 + lane;
-                const bool in = p < n && (key_row(keys[p]) >> 8) == blk;
-                if (in && (p == i0 || is_head(keys, p))) {
-                    const float old_rm = __uint_as_float(key_lo(keys[p]));
-                    const float new_rm = rowmax[rb + key_row(keys[p])];
-                    dec |= (old_rm == old_blk) && (new_rm < old_rm);
-                    cand = fmaxf(cand, new_rm);
-                }
-                if (!__all(in)) break;
-            }
-            dec = __any(dec);
-            cand = wave_max(cand);
-            float nb;
-            if (dec) {
-                const int64_t r0 = (int64_t)blk * BLK;
-                const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
-                float v = 0.0f;
-                for (int64_t r = r0 + lane; r < r1; r += WAVE) v = fmaxf(v, rowmax[rb + r]);
-                nb = wave_max(v);
-            } else {
-                nb = fmaxf(old_blk, cand);
-            }
-            if (lane == 0) {
-                blkmax[bb + blk] = nb;
-                keys[i0] = with_lo(keys[i0], __float_as_uint(old_blk));
-            }
+    for (int u = threadIdx.x; u < U; u += blockDim.x) {
+        const uint32_t blk = key_row(keys[heads[u]]) >> 8;
+        if (u > 0 && (key_row(keys[heads[u - 1]]) >> 8) == blk) continue;  // not a block start
+        // end of the block's heads: first head whose row is in a later block
+        int lo = u + 1, hi = U;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((key_row(keys[heads[mid]]) >> 8) == blk) lo = mid + 1; else hi = mid;
         }
+        const int cnt = lo - u;
+        const float old_blk = blkmax[bb + blk];
+        bool dec = false;
+        float cand = 0.0f;
+        if (cnt <= 32) {
+            for (int k = u; k < lo; ++k) {
+                const uint64_t kk = keys[heads[k]];
+                const float old_rm = __uint_as_float(key_lo(kk));
+                const float new_rm = rowmax[rb + key_row(kk)];
+                dec |= (old_rm == old_blk) && (new_rm < old_rm);
+                cand = fmaxf(cand, new_rm);
+            }
+        } else {
+            dec = true;  // many touched rows: re-reading the block is cheaper than walking
+        }
+        float nb;
+        if (dec) {
+            const int64_t r0 = (int64_t)blk * BLK;
+            const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
+            float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+            int64_t r = r0;
+            for (; r + 4 <= r1; r += 4) {
+                v0 = fmaxf(v0, rowmax[rb + r]); v1 = fmaxf(v1, rowmax[rb + r + 1]);
+                v2 = fmaxf(v2, rowmax[rb + r + 2]); v3 = fmaxf(v3, rowmax[rb + r + 3]);
+            }
+            for (; r < r1; ++r) v0 = fmaxf(v0, rowmax[rb + r]);
+            nb = fmaxf(fmaxf(v0, v1), fmaxf(v2, v3));
+        } else {
+            nb = fmaxf(old_blk, cand);
+        }
+        blkmax[bb + blk] = nb;
+        const int64_t sb = sbb + (blk >> 8);
+        const float old_sb = sblkmax[sb];
+        if (old_blk == old_sb && nb < old_blk) sdirty[sb] = 1;
+        if (nb > old_sb) atomicMax(reinterpret_cast<unsigned int*>(sblkmax) + sb, __float_as_uint(nb));
     }
-    __syncthreads();
-    // level 2: superblocks, from the block-start keys (old blkmax in their low bits)
-    for (int base = w * WAVE; base < n; base += nw * WAVE) {
-        const int i = base + lane;
-        const bool start = i < n && (i == 0 || (key_row(keys[i - 1]) >> 16) != (key_row(keys[i]) >> 16));
-        uint64_t msk = __ballot(start);
-        while (msk) {
+}
+
+// one workgroup per table: re-reduce flagged superblocks, then tmax over all superblocks
+__global__ void k_table_finalize(const float* __restrict__ blkmax, float* __restrict__ sblkmax,
+                                 uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
+                                 const int64_t* __restrict__ meta, int T) {
+    Meta m = make_meta(meta, T);
+    __shared__ float red[16];
+    const int t = blockIdx.x;
+    const int64_t nblk = ceil_div(m.num_rows[t], BLK);
+    const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
+    const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    for (int64_t k0 = (int64_t)w * WAVE; k0 < ns; k0 += (int64_t)nw * WAVE) {
+        const int64_t k = k0 + lane;
+        const bool d = k < ns && sdirty[sbb + k];
+        uint64_t msk = __ballot(d);
+        while (msk) {  // rare: a superblock's max holder shrank
             const int l = __ffsll((long long)msk) - 1;
             msk &= msk - 1;
-            const int i0 = base + l;
-            const uint32_t sb = key_row(keys[i0]) >> 16;
-            const float old_sb = sblkmax[sbb + sb];
-            bool dec = false;
-            float cand = 0.0f;
-            for (int p0 = i0;; p0 += WAVE) {
-                const int p = p0 + lane;
-                const bool in = p < n && (key_row(keys[p]) >> 16) == sb;
-                if (in && (p == i0 || (key_row(keys[p - 1]) >> 8) != (key_row(keys[p]) >> 8))) {
-                    const uint32_t blk = key_row(keys[p]) >> 8;
-                    const float old_b = __uint_as_float(key_lo(keys[p]));
-                    const float new_b = blkmax[bb + blk];
-                    dec |= (old_b == old_sb) && (new_b < old_b);
-                    cand = fmaxf(cand, new_b);
-                }
-                if (!__all(in)) break;
-            }
-            dec = __any(dec);
-            cand = wave_max(cand);
-            float ns;
-            if (dec) {
-                const int64_t b0 = (int64_t)sb * SBLK_BLOCKS;
-                const int64_t b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-                float v = 0.0f;
-                for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[bb + b]);
-                ns = wave_max(v);
-            } else {
-                ns = fmaxf(old_sb, cand);
-            }
-            if (lane == 0) sblkmax[sbb + sb] = ns;
+            const int64_t sb = k0 + l;
+            const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+            float v = 0.0f;
+            for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[bb + b]);
+            v = wave_max(v);
+            if (lane == 0) { sblkmax[sbb + sb] = v; sdirty[sbb + sb] = 0; }
         }
     }
     __syncthreads();
     float v = 0.0f;
-    for (int64_t k = threadIdx.x; k < nsblk; k += blockDim.x) v = fmaxf(v, sblkmax[sbb + k]);
+    for (int64_t k = threadIdx.x; k < ns; k += blockDim.x) v = fmaxf(v, sblkmax[sbb + k]);
     v = wave_max(v);
-    if (lane == 0) s_red[w] = v;
+    if (lane == 0) red[w] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
         float r = 0.0f;
-        for (int k = 0; k < nw; ++k) r = fmaxf(r, s_red[k]);
+        for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
         tmax[t] = r;
     }
-    __syncthreads();
 }
 
-// build sorted (row << 32 | bag) keys of table t in LDS; returns L (0..), -1 on capacity
-DQRM_INLINE int build_lookup_keys(uint64_t* keys, int key_cap, const int64_t* idx,
-                                  const int64_t* off, const int64_t* idx_base, int64_t B, int t,
-                                  int64_t nrows, uint32_t* err) {
+// gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
+// deterministic placement (count, block-scan, write); returns the key count, or -1
+// (uniform) when the slot overflows SLOT_KEYS.
+DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* idx, const int64_t* off,
+                                   const int64_t* idx_base, int64_t B, int t, int64_t nrows,
+                                   int64_t r0, int64_t r1, bool report, uint32_t* err) {
     const int64_t ib = idx_base[t];
     const int64_t L = idx_base[t + 1] - ib;
-    if (L < 0 || next_pow2(L < 2 ? 2 : (int)(L > (1 << 30) ? (1 << 30) : L)) > key_cap) {
-        if (threadIdx.x == 0) flag_error(err, DQRM_ERRF_OVERFLOW);
-        return -1;  // uniform across the workgroup
-    }
-    const int n = (int)L;
-    const int np2 = next_pow2(n < 2 ? 2 : n);
-    for (int i = threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
-    __syncthreads();
-    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) {
-        int64_t s0 = off[(int64_t)t * B + b];
-        int64_t s1 = (b + 1 < B) ? off[(int64_t)t * B + b + 1] : L;
+    const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
+    // each thread owns a contiguous run of bags
+    const int64_t per = (B + blockDim.x - 1) / blockDim.x;
+    const int64_t b0 = (int64_t)tid * per, b1 = b0 + per < B ? b0 + per : B;
+    auto bag_range = [&](int64_t b, int64_t& s0, int64_t& s1) {
+        s0 = off[(int64_t)t * B + b];
+        s1 = (b + 1 < B) ? off[(int64_t)t * B + b + 1] : L;
         if (s0 < 0 || s1 > L || s1 < s0) {
-            flag_error(err, DQRM_ERRF_OFFSET);
+            if (report) flag_error(err, DQRM_ERRF_OFFSET);
             s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
             s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
         }
+    };
+    int cnt = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+        int64_t s0, s1;
+        bag_range(b, s0, s1);
         for (int64_t p = s0; p < s1; ++p) {
-            int64_t r = idx[ib + p];
-            if (r < 0 || r >= nrows) { flag_error(err, DQRM_ERRF_INDEX); continue; }
-            keys[p] = ((uint64_t)r << 32) | (uint64_t)b;
+            const int64_t r = idx[ib + p];
+            if (r < 0 || r >= nrows) {
+                if (report) flag_error(err, DQRM_ERRF_INDEX);
+                continue;
+            }
+            cnt += (r >= r0 && r < r1);
+        }
+    }
+    int v = cnt;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        int y = __shfl_up(v, o, WAVE);
+        if (lane >= o) v += y;
+    }
+    if (lane == WAVE - 1) s_wsum[w] = v;
+    __syncthreads();
+    if (tid == 0) {
+        int run = 0;
+        for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
+        s_wsum[blockDim.x / WAVE] = run;
+    }
+    __syncthreads();
+    const int n = s_wsum[blockDim.x / WAVE];
+    if (n > SLOT_KEYS) {
+        if (tid == 0) flag_error(err, DQRM_ERRF_OVERFLOW);
+        return -1;
+    }
+    int pos = s_wsum[w] + v - cnt;
+    for (int64_t b = b0; b < b1 && cnt > 0; ++b) {
+        int64_t s0, s1;
+        bag_range(b, s0, s1);
+        for (int64_t p = s0; p < s1; ++p) {
+            const int64_t r = idx[ib + p];
+            if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
         }
     }
     __syncthreads();
-    bitonic_sort_lds(keys, np2);
-    // positions whose index was invalid (or not covered by any bag) stay ~0 and sort last
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        int mid = (lo + hi) >> 1;
-        if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1;
-    }
-    return lo;
+    return n;
 }
 
 struct BwdArgs {
@@ -774,7 +981,7 @@ struct BwdArgs {
     float* rowmax;
     float* blkmax;
     float* sblkmax;
-    float* tmax;
+    uint8_t* sdirty;
     const float* scale;
     const float* pscale;
     const int64_t* meta;
@@ -789,14 +996,12 @@ struct BwdArgs {
     int ste;
     float nlr;          // -lr (f32)
     int repack;         // repack touched INT4 rows with pscale
-    // coalesce mode outputs
-    const int64_t* cap_base;
-    int32_t* rows_out;
-    float* vals_out;
-    int32_t* counts_out;
-    float* s_loc;
-    int grad_bits;
-    int key_cap;        // dynamic-LDS key capacity (power of two)
+    // coalesce mode outputs (slot workspace)
+    const int64_t* ws_cap_base;
+    int32_t* ws_rows;
+    float* ws_vals;
+    int32_t* ws_ucount;
+    float* ws_absmax;
 };
 
 // dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363)
@@ -814,89 +1019,116 @@ struct DySource {
     }
 };
 
-// MODE 0: fused SGD (single GPU);  MODE 1: coalesce + local grad scale (DP)
+// MODE 0: fused SGD (single GPU);  MODE 1: coalesce + per-slot max |grad| (DP)
 template <int LPR, int MODE>
-__global__ void __launch_bounds__(TABLE_WG) k_table_bwd(BwdArgs a) {
+__global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
-    // static LDS kept a multiple of 16 bytes (Guideline 17: dynamic base alignment)
-    __shared__ int s_base[TABLE_WG];
-    __shared__ int s_wtot[TABLE_WG / WAVE + 4];
-    __shared__ float s_red[TABLE_WG / WAVE];
-    __shared__ unsigned int s_absmax_arr[4];
-    unsigned int& s_absmax = s_absmax_arr[0];
+    uint16_t* heads = reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8);
+    __shared__ int s_wsum[TWG / WAVE + 8];   // 64 B: static LDS stays a multiple of 16
+    __shared__ unsigned int s_misc[4];
+    __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
+    int* s_nlong = reinterpret_cast<int*>(&s_misc[2]);
 
-    const int t = blockIdx.x;
+    const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
     const int T = a.T;
     Meta m = make_meta(a.meta, T);
     const int64_t nrows = m.num_rows[t];
     const int64_t rb = m.row_base[t];
     const int D = LPR * 4;
-    if (threadIdx.x == 0) s_absmax = 0u;
+    int64_t r0, r1;
+    slot_rows(nrows, s, r0, r1);
+    const int slot = t * SPLIT + s;
+    if (threadIdx.x == 1) s_misc[1] = 0u;
 
-    const int n = build_lookup_keys(keys, a.key_cap, a.idx, a.off, a.idx_base, a.B, t, nrows, a.err);
+    const int n = gather_lookup_keys(keys, s_wsum, a.idx, a.off, a.idx_base, a.B, t, nrows, r0, r1, s == 0,
+                                     a.err);
     if (n < 0) {
-        if (MODE == 1 && threadIdx.x == 0) { a.counts_out[t] = 0; a.s_loc[t] = 0.0f; }
+        if (MODE == 1 && threadIdx.x == 0) { a.ws_ucount[slot] = 0; a.ws_absmax[slot] = 0.0f; }
         return;
     }
-    int U = 0;
-    if (MODE == 1) U = head_scan<MAX_LDS_KEYS / TABLE_WG>(keys, n, s_base, s_wtot);
+#if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 1
+    if (n >= 0) return;  // diagnostic build: gather only
+#endif
+    const int U = sort_and_heads(keys, heads, n, s_wsum);
+#if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 2
+    if (U >= 0) return;  // diagnostic build: gather + sort + heads
+#endif
 
     DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste};
     const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
-    const int64_t cap = MODE == 1 ? a.cap_base[t + 1] - a.cap_base[t] : 0;
+    const int64_t cap = MODE == 1 ? a.ws_cap_base[slot + 1] - a.ws_cap_base[slot] : 0;
     float local_absmax = 0.0f;
+    float* tile = reinterpret_cast<float*>(lds + SLOT_KEYS * 10) + (threadIdx.x / WAVE) * TILE_FLOATS;
 
-    for_each_segment<LPR>(keys, n, [&](int i, uint32_t row, int sub, bool writer, bool wave_mode) {
+    auto group_fn = [&](int u, int i, int len, int sub) {
+        const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
         if (MODE == 0) {
             float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
             const float old_rm = a.rowmax[grow];
-            w = wave_mode ? seg_reduce_wave<LPR, OP_FMA>(keys, n, i, row, w, src, a.nlr)
-                          : seg_reduce_group<LPR, OP_FMA>(keys, n, i, row, w, src, a.nlr, sub);
+            w = seg_reduce_group<LPR, OP_FMA>(keys, i, len, w, src, a.nlr, sub);
             const float rm = group_max<LPR>(abs_max4(w));
-            if (writer) {
-                reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
-                if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
-                if (sub == 0) {
-                    a.rowmax[grow] = rm;
-                    keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-                }
+            reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
+            if (sub == 0) {
+                a.rowmax[grow] = rm;
+                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
             }
         } else {
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            acc = wave_mode ? seg_reduce_wave<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f)
-                            : seg_reduce_group<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f, sub);
-            if (writer) {
-                const int u = head_ordinal<MAX_LDS_KEYS / TABLE_WG>(keys, s_base, i);
-                if (u < cap) {
-                    const int64_t e = a.cap_base[t] + u;
-                    reinterpret_cast<float4*>(a.vals_out + e * D)[sub] = acc;
-                    if (sub == 0) a.rows_out[e] = (int32_t)row;
-                }
-                local_absmax = fmaxf(local_absmax, abs_max4(acc));
+            acc = seg_reduce_group<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, sub);
+            if (u < cap) {
+                const int64_t e = a.ws_cap_base[slot] + u;
+                reinterpret_cast<float4*>(a.ws_vals + e * D)[sub] = acc;
+                if (sub == 0) a.ws_rows[e] = (int32_t)row;
             }
+            local_absmax = fmaxf(local_absmax, abs_max4(acc));
         }
-    });
+    };
+    auto wave_fn = [&](int u, int i, int len) {
+        const uint32_t row = key_row(keys[i]);
+        const int64_t grow = rb + row;
+        const int lane = threadIdx.x % WAVE;
+        if (MODE == 0) {
+            LaneRow<LPR> w = load_lane_row<LPR>(a.W + grow * D);
+            const float old_rm = a.rowmax[grow];
+            w = seg_reduce_tile<LPR, OP_FMA>(keys, i, len, w, src, a.nlr, tile);
+            const float rm = lane_row_absmax<LPR>(w);
+            store_lane_row<LPR>(a.W + grow * D, w);
+            if (a.repack) pack_lane_row<LPR>(w, tile, a.packed, grow, r_pack);
+            if (lane == 0) {
+                a.rowmax[grow] = rm;
+                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+            }
+        } else {
+            LaneRow<LPR> acc{};
+            acc = seg_reduce_tile<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, tile);
+            if (u < cap) {
+                const int64_t e = a.ws_cap_base[slot] + u;
+                store_lane_row<LPR>(a.ws_vals + e * D, acc);
+                if (lane == 0) a.ws_rows[e] = (int32_t)row;
+            }
+            local_absmax = fmaxf(local_absmax, lane_row_absmax<LPR>(acc));
+        }
+    };
+    for_each_segment<LPR>(heads, U, n, s_long, s_nlong, group_fn, wave_fn);
     if (MODE == 1) {
         local_absmax = wave_max(local_absmax);
-        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_absmax, __float_as_uint(local_absmax));
+        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
     }
     __syncthreads();
     if (MODE == 0) {
-        maintain_hierarchy(m, t, keys, n, a.rowmax, a.blkmax, a.sblkmax, a.tmax, s_red);
+        maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
     } else if (threadIdx.x == 0) {
         if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        a.counts_out[t] = U < cap ? U : (int32_t)cap;
-        if (a.grad_bits >= 2 && a.grad_bits <= 16)
-            a.s_loc[t] = sym_scale(__uint_as_float(s_absmax), a.grad_bits);
-        else
-            a.s_loc[t] = 0.0f;
+        a.ws_ucount[slot] = U < cap ? U : (int32_t)cap;
+        a.ws_absmax[slot] = __uint_as_float(s_misc[1]);
     }
 }
 
 // ------------------------------------------------------------------------------------
-// K5: scale average + quantize-pack into the wire payload
+// K5: scale average + quantize-pack (slot workspace -> dense wire payload)
 // ------------------------------------------------------------------------------------
 struct PayloadLayout {
     int64_t rows_off;   // bytes
@@ -916,65 +1148,84 @@ __host__ __device__ inline PayloadLayout payload_layout(int T, int64_t cap, int 
     return p;
 }
 
-// dist.all_reduce(scale, SUM) then scale.mul_(1./N) (s_q_g_p_c.py:865-866). Gloo's
-// allreduce of a one-element tensor accumulates in descending rank order
+// rank r's local scale from its slots' max |grad| (quant_utils.py:141-194 on the coalesced
+// values), then dist.all_reduce(SUM) + mul_(1./N) (s_q_g_p_c.py:861-866). Gloo's allreduce
+// of a one-element tensor accumulates in descending rank order
 // (((s_{N-1} + s_{N-2}) + ...) + s_0) — measured for N = 2..8 with torch 2.10's Gloo;
-// every rank evaluates the same order on the all-gathered scales, so the average is
+// every rank evaluates the same order on the all-gathered values, so the average is
 // bit-identical across ranks and equal to the reference's.
-DQRM_INLINE float average_scale(const float* s_all, int T, int N, int t, float inv_n) {
-    float acc = s_all[(int64_t)(N - 1) * T + t];
-    for (int r = N - 2; r >= 0; --r) acc = acc + s_all[(int64_t)r * T + t];
+DQRM_INLINE float rank_scale(const float* absmax_all, int T, int r, int t, int bits) {
+    float a = 0.0f;
+    for (int s = 0; s < SPLIT; ++s) a = fmaxf(a, absmax_all[((int64_t)r * T + t) * SPLIT + s]);
+    return sym_scale(a, bits);
+}
+
+DQRM_INLINE float average_scale(const float* absmax_all, int T, int N, int t, int bits) {
+    const float inv_n = (float)(1.0 / (double)N);
+    float acc = rank_scale(absmax_all, T, N - 1, t, bits);
+    for (int r = N - 2; r >= 0; --r) acc = acc + rank_scale(absmax_all, T, r, t, bits);
     return acc * inv_n;
 }
 
 template <int LPR>
-__global__ void k_quant_pack(int T, const int64_t* __restrict__ cap_base, int64_t cap_total,
-                             const int32_t* __restrict__ rows, const float* __restrict__ vals,
-                             const int32_t* __restrict__ counts, const float* __restrict__ s_all,
-                             int N, int bits, float* __restrict__ s_avg,
-                             unsigned char* __restrict__ payload) {
+__global__ void k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base, int64_t ws_cap_total,
+                             const int32_t* __restrict__ ws_rows, const float* __restrict__ ws_vals,
+                             const int32_t* __restrict__ ws_ucount, const float* __restrict__ absmax_all,
+                             int N, int bits, const int64_t* __restrict__ cap_base, int64_t cap_total,
+                             float* __restrict__ s_avg, unsigned char* __restrict__ payload) {
+    __shared__ int s_pre[MAX_TABLES * SPLIT];   // exclusive prefix of ucount within each table
+    __shared__ float s_sc[MAX_TABLES];
     const int D = LPR * 4;
     const PayloadLayout pl = payload_layout(T, cap_total, D, bits);
     const bool quant = bits >= 2 && bits <= 16;
-    const float inv_n = (float)(1.0 / (double)N);
-    if (blockIdx.x == 0) {
-        for (int t = threadIdx.x; t < T; t += blockDim.x) {
-            reinterpret_cast<int32_t*>(payload)[t] = counts[t];
-            if (quant) s_avg[t] = average_scale(s_all, T, N, t, inv_n);
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        int run = 0;
+        for (int s = 0; s < SPLIT; ++s) { s_pre[t * SPLIT + s] = run; run += ws_ucount[t * SPLIT + s]; }
+        const int cap = (int)(cap_base[t + 1] - cap_base[t]);
+        if (blockIdx.x == 0) reinterpret_cast<int32_t*>(payload)[t] = run < cap ? run : cap;
+        if (quant) {
+            const float sv = average_scale(absmax_all, T, N, t, bits);
+            s_sc[t] = sv;
+            if (blockIdx.x == 0) s_avg[t] = sv;
         }
     }
+    __syncthreads();
     const int lane = threadIdx.x % LPR;
     const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
     const float qlo = -(float)(1 << (bits - 1)), qhi = (float)((1 << (bits - 1)) - 1);
-    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < cap_total; e += ngrp) {
-        const int t = find_table(cap_base, T, e);
-        if (e - cap_base[t] >= counts[t]) continue;
-        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[e] = rows[e];
-        float4 v = reinterpret_cast<const float4*>(vals + e * D)[lane];
+    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < ws_cap_total; e += ngrp) {
+        const int slot = find_table(ws_cap_base, T * SPLIT, e);
+        const int64_t u = e - ws_cap_base[slot];
+        if (u >= ws_ucount[slot]) continue;
+        const int t = slot / SPLIT;
+        const int64_t q = cap_base[t] + s_pre[slot] + u;  // dense payload entry
+        if (q >= cap_base[t + 1]) continue;
+        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = ws_rows[e];
+        float4 v = reinterpret_cast<const float4*>(ws_vals + e * D)[lane];
         if (!quant) {
-            reinterpret_cast<float4*>(payload + pl.vals_off + e * D * 4)[lane] = v;
+            reinterpret_cast<float4*>(payload + pl.vals_off + q * D * 4)[lane] = v;
             continue;
         }
-        const float s = average_scale(s_all, T, N, t, inv_n);
-        const float rr = 1.0f / s;
+        const float rr = 1.0f / s_sc[t];
         const float q0 = fake_quant(v.x, rr, qlo, qhi), q1 = fake_quant(v.y, rr, qlo, qhi);
         const float q2 = fake_quant(v.z, rr, qlo, qhi), q3 = fake_quant(v.w, rr, qlo, qhi);
         if (pl.elem == 1) {
             uint32_t pk = ((uint32_t)(uint8_t)(int8_t)(int)q0) | ((uint32_t)(uint8_t)(int8_t)(int)q1 << 8) |
                           ((uint32_t)(uint8_t)(int8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int8_t)(int)q3 << 24);
-            reinterpret_cast<uint32_t*>(payload + pl.vals_off + e * D)[lane] = pk;
+            reinterpret_cast<uint32_t*>(payload + pl.vals_off + q * D)[lane] = pk;
         } else {
             uint2 pk;
             pk.x = ((uint32_t)(uint16_t)(int16_t)(int)q0) | ((uint32_t)(uint16_t)(int16_t)(int)q1 << 16);
             pk.y = ((uint32_t)(uint16_t)(int16_t)(int)q2) | ((uint32_t)(uint16_t)(int16_t)(int)q3 << 16);
-            reinterpret_cast<uint2*>(payload + pl.vals_off + e * D * 2)[lane] = pk;
+            reinterpret_cast<uint2*>(payload + pl.vals_off + q * D * 2)[lane] = pk;
         }
     }
 }
 
 // ------------------------------------------------------------------------------------
-// K6: decode N payloads, union rows, sum, dequantize, SGD update + maintenance
-// keys = (row << 32) | (rank << 24) | entry
+// K6: decode N payloads, union rows, sum, dequantize, SGD update + maintenance.
+// Slot (t, s) binary-searches each rank's sorted row list for its row range;
+// keys = (row << 32) | (rank << 24) | entry.
 // ------------------------------------------------------------------------------------
 struct ApplyArgs {
     float* W;
@@ -982,7 +1233,7 @@ struct ApplyArgs {
     float* rowmax;
     float* blkmax;
     float* sblkmax;
-    float* tmax;
+    uint8_t* sdirty;
     const float* pscale;
     const int64_t* meta;
     uint32_t* err;
@@ -997,7 +1248,6 @@ struct ApplyArgs {
     float nlr;
     int mode;
     int repack;
-    int key_cap;
 };
 
 // one payload entry (rank = lo >> 24, entry = lo & 0xFFFFFF) widened to f32
@@ -1028,14 +1278,18 @@ struct PayloadSource {
 };
 
 template <int LPR>
-__global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
+__global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
-    __shared__ int s_cnt[68];
+    uint16_t* heads = reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8);
+    __shared__ int s_wsum[TWG / WAVE + 8];
+    __shared__ int s_e0[68];
     __shared__ int s_start[68];
-    __shared__ float s_red[TABLE_WG / WAVE];
+    __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
+    __shared__ int s_nlong_arr[4];
+    int* s_nlong = &s_nlong_arr[0];
 
-    const int t = blockIdx.x;
+    const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
     const int T = a.T;
     const int D = LPR * 4;
     Meta m = make_meta(a.meta, T);
@@ -1043,83 +1297,110 @@ __global__ void __launch_bounds__(TABLE_WG) k_table_apply(ApplyArgs a) {
     const int64_t cap = a.cap_base[t + 1] - a.cap_base[t];
     const int64_t rb = m.row_base[t];
     const int64_t nrows = m.num_rows[t];
-    if (threadIdx.x < a.N) {
+    int64_t r0, r1;
+    slot_rows(nrows, s, r0, r1);
+    if (threadIdx.x < a.N) {  // this slot's entry range in rank r's ascending row list
         const unsigned char* p = a.payloads + (int64_t)threadIdx.x * a.payload_bytes;
         int c = reinterpret_cast<const int32_t*>(p)[t];
-        if (c < 0 || c > cap) { flag_error(a.err, DQRM_ERRF_OVERFLOW); c = c < 0 ? 0 : (int)cap; }
-        s_cnt[threadIdx.x] = c;
+        if (c < 0 || c > cap) {
+            if (s == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+            c = c < 0 ? 0 : (int)cap;
+        }
+        const int32_t* rows = reinterpret_cast<const int32_t*>(p + pl.rows_off) + a.cap_base[t];
+        int lo = 0, hi = c;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (rows[mid] < r0) lo = mid + 1; else hi = mid; }
+        const int e0 = lo;
+        hi = c;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (rows[mid] < r1) lo = mid + 1; else hi = mid; }
+        s_e0[threadIdx.x] = e0;
+        s_start[threadIdx.x] = lo - e0;  // count, prefix-summed below
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         int run = 0;
-        for (int r = 0; r < a.N; ++r) { s_start[r] = run; run += s_cnt[r]; }
+        for (int r = 0; r < a.N; ++r) { int c = s_start[r]; s_start[r] = run; run += c; }
         s_start[a.N] = run;
     }
     __syncthreads();
     const int M = s_start[a.N];
-    if (next_pow2(M < 2 ? 2 : M) > a.key_cap) {  // uniform: whole workgroup leaves
+    if (M > SLOT_KEYS) {  // uniform: whole workgroup leaves
         if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
         return;
     }
-    const int np2 = next_pow2(M < 2 ? 2 : M);
-    for (int i = threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
-    __syncthreads();
     for (int i = threadIdx.x; i < M; i += blockDim.x) {
         int r = 0;
         while (i >= s_start[r + 1]) ++r;
-        const int e = i - s_start[r];
+        const int e = s_e0[r] + (i - s_start[r]);
         const unsigned char* p = a.payloads + (int64_t)r * a.payload_bytes;
         int64_t row = reinterpret_cast<const int32_t*>(p + pl.rows_off)[a.cap_base[t] + e];
-        if (row < 0 || row >= nrows) { flag_error(a.err, DQRM_ERRF_INDEX); continue; }
+        if (row < 0 || row >= nrows) {  // cannot happen for payloads this library packed
+            flag_error(a.err, DQRM_ERRF_INDEX);
+            row = r0;
+        }
         keys[i] = ((uint64_t)row << 32) | ((uint64_t)r << 24) | (uint64_t)e;
     }
     __syncthreads();
-    bitonic_sort_lds(keys, np2);
-    int n;
-    {
-        int lo = 0, hi = M;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (keys[mid] == ~0ull) hi = mid; else lo = mid + 1; }
-        n = lo;
-    }
+    const int n = M;
+    const int U = sort_and_heads(keys, heads, n, s_wsum);
 
-    const float s = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
     const float inv_n = (float)(1.0 / (double)a.N);
-    const float sim_f = (float)((double)s / (double)a.N);
+    const float sim_f = (float)((double)sc / (double)a.N);
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
     PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, a.cap_base[t]};
 
-    for_each_segment<LPR>(keys, n, [&](int i, uint32_t row, int sub, bool writer, bool wave_mode) {
+    float* tile = reinterpret_cast<float*>(lds + SLOT_KEYS * 10) + (threadIdx.x / WAVE) * TILE_FLOATS;
+    const int mode = a.mode;
+    const float nlr = a.nlr;
+    // dequantize + SGD, one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
+    auto update = [=](float w, float acc) {
+        float v;
+        if (mode == DQRM_UPD_DP) v = (acc * inv_n) * sc;                  // s_q_g_p_c.py:885,618-622
+        else if (mode == DQRM_UPD_SIMULATED) v = acc * sim_f;            // sgd_quantized_gradients.py:366-371
+        else v = acc * inv_n;                                            // FP32 sparse all_reduce (:319-327)
+        return w + nlr * v;  // separately rounded product, then add
+    };
+    auto group_fn = [&](int u, int i, int len, int sub) {
+        (void)u;
+        const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
         float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
         const float old_rm = a.rowmax[grow];
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
         // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
-        acc = wave_mode ? seg_reduce_wave<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f)
-                        : seg_reduce_group<LPR, OP_SUM>(keys, n, i, row, acc, src, 0.0f, sub);
-        float4 v;
-        if (a.mode == DQRM_UPD_DP) {          // update.mul_(1/N) ; grad * s.item()
-            v.x = (acc.x * inv_n) * s; v.y = (acc.y * inv_n) * s;
-            v.z = (acc.z * inv_n) * s; v.w = (acc.w * inv_n) * s;
-        } else if (a.mode == DQRM_UPD_SIMULATED) {  // buffer * (s.item()/N)
-            v.x = acc.x * sim_f; v.y = acc.y * sim_f; v.z = acc.z * sim_f; v.w = acc.w * sim_f;
-        } else {                              // FP32 sparse allreduce, mul_(1/N)
-            v.x = acc.x * inv_n; v.y = acc.y * inv_n; v.z = acc.z * inv_n; v.w = acc.w * inv_n;
-        }
-        // weight.data.add_(-lr * grad_update): separately rounded product, then add
-        w.x = w.x + a.nlr * v.x; w.y = w.y + a.nlr * v.y; w.z = w.z + a.nlr * v.z; w.w = w.w + a.nlr * v.w;
+        acc = seg_reduce_group<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, sub);
+        w.x = update(w.x, acc.x); w.y = update(w.y, acc.y); w.z = update(w.z, acc.z); w.w = update(w.w, acc.w);
         const float rm = group_max<LPR>(abs_max4(w));
-        if (writer) {
-            reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
-            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
-            if (sub == 0) {
-                a.rowmax[grow] = rm;
-                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-            }
+        reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+        if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
+        if (sub == 0) {
+            a.rowmax[grow] = rm;
+            keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
         }
-    });
+    };
+    auto wave_fn = [&](int u, int i, int len) {
+        (void)u;
+        const uint32_t row = key_row(keys[i]);
+        const int64_t grow = rb + row;
+        const int lane = threadIdx.x % WAVE;
+        LaneRow<LPR> w = load_lane_row<LPR>(a.W + grow * D);
+        const float old_rm = a.rowmax[grow];
+        LaneRow<LPR> acc{};
+        acc = seg_reduce_tile<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, tile);
+#pragma unroll
+        for (int d = 0; d < LaneRow<LPR>::NDL; ++d) w.v[d] = update(w.v[d], acc.v[d]);
+        const float rm = lane_row_absmax<LPR>(w);
+        store_lane_row<LPR>(a.W + grow * D, w);
+        if (a.repack) pack_lane_row<LPR>(w, tile, a.packed, grow, r_pack);
+        if (lane == 0) {
+            a.rowmax[grow] = rm;
+            keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+        }
+    };
+    for_each_segment<LPR>(heads, U, n, s_long, s_nlong, group_fn, wave_fn);
     __syncthreads();
-    maintain_hierarchy(m, t, keys, n, a.rowmax, a.blkmax, a.sblkmax, a.tmax, s_red);
+    maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1133,7 +1414,7 @@ int check_set(const dqrm_table_set* s) {
     if (D < 4 || D > 256 || (D & 3) || ((D / 4) & (D / 4 - 1)))
         return set_error(DQRM_E_INVALID, "dqrm: dim must be 4*2^k <= 256 (got %d)", D);
     if (!s->W || !s->rowmax || !s->blkmax || !s->sblkmax || !s->tmax || !s->scale || !s->pscale ||
-        !s->meta || !s->err || !s->tflags)
+        !s->meta || !s->err || !s->tflags || !s->sdirty)
         return set_error(DQRM_E_INVALID, "dqrm: null state pointer");
     if (((uintptr_t)s->W) & 15)
         return set_error(DQRM_E_INVALID, "dqrm: W must be 16-byte aligned");
@@ -1168,10 +1449,11 @@ int allow_lds(K kernel, size_t bytes) {
     return DQRM_OK;
 }
 
-size_t table_lds_bytes(int64_t max_keys) {
-    int64_t n = 2;
-    while (n < max_keys) n <<= 1;
-    return (size_t)n * sizeof(uint64_t);
+int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
+    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(256), 0, st, set->blkmax, set->sblkmax,
+                       set->sdirty, set->tmax, set->meta, set->num_tables);
+    LAUNCH_CHECK();
+    return DQRM_OK;
 }
 
 }  // namespace
@@ -1211,6 +1493,7 @@ int dqrm_refresh_absmax(const dqrm_table_set* set, void* stream) {
     hipLaunchKernelGGL(k_level_max, dim3(grid_for(set->total_sblocks * WAVE, 256, 8192)), dim3(256), 0, st,
                        set->blkmax, set->sblkmax, set->meta, set->num_tables, 2, set->total_sblocks);
     LAUNCH_CHECK();
+    HIP_TRY(hipMemsetAsync(set->sdirty, 0, (size_t)set->total_sblocks, st));
     hipLaunchKernelGGL(k_table_max, dim3(set->num_tables), dim3(256), 0, st, set->sblkmax, set->tmax,
                        set->meta, set->num_tables);
     LAUNCH_CHECK();
@@ -1260,23 +1543,41 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, u
     a.out = out; a.B = batch->num_bags; a.ost_t = out_stride_t; a.ost_b = out_stride_b;
     a.T = set->num_tables; a.bits = bits; a.flags = flags;
     hipStream_t st = (hipStream_t)stream;
-    const int64_t total = (int64_t)a.T * a.B;
     const int D = set->dim;
+    const bool packed_path = (flags & DQRM_FWD_USE_PACKED) && !(flags & DQRM_FWD_FULL_PRECISION) && D >= 8;
+    if (packed_path) {
+        int64_t bx = (a.B + 255) / 256;
+        const int64_t cap = (16384 + a.T - 1) / a.T;
+        if (bx > cap) bx = cap;
+        const bool nt = (flags & DQRM_FWD_NT_STORE) != 0;
+        DISPATCH_LPR(D, {
+            if constexpr (LPR >= 2) {
+                if (nt)
+                    hipLaunchKernelGGL((k_emb_fwd_packed<LPR, true>), dim3((unsigned)bx, (unsigned)a.T), dim3(256), 0, st, a);
+                else
+                    hipLaunchKernelGGL((k_emb_fwd_packed<LPR, false>), dim3((unsigned)bx, (unsigned)a.T), dim3(256), 0, st, a);
+            }
+        });
+        LAUNCH_CHECK();
+        return DQRM_OK;
+    }
     DISPATCH_LPR(D, {
         constexpr int UNR = 4;
-        int blocks = grid_for(total * LPR, 256 * UNR, 4096);
-        hipLaunchKernelGGL((k_emb_fwd<LPR, UNR>), dim3(blocks), dim3(256), 0, st, a);
+        constexpr int BAGS_PER_WG = (256 / LPR) * UNR;
+        int64_t bx = (a.B + BAGS_PER_WG - 1) / BAGS_PER_WG;
+        const int64_t cap = (8192 + a.T - 1) / a.T;  // ~8k workgroups in total, grid-stride beyond
+        if (bx > cap) bx = cap;
+        hipLaunchKernelGGL((k_emb_fwd<LPR, UNR>), dim3((unsigned)bx, (unsigned)a.T), dim3(256), 0, st, a);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
 }
 
-static int check_batch_capacity(const dqrm_batch* batch, const char* who) {
+static int check_batch(const dqrm_batch* batch, const char* who) {
     if (!batch || !batch->idx || !batch->off || !batch->idx_base)
         return set_error(DQRM_E_INVALID, "%s: null batch pointer", who);
-    if (batch->max_lookups > MAX_LDS_KEYS || batch->num_bags > 0xFFFFFFFFll)
-        return set_error(DQRM_E_CAPACITY, "%s: per-table lookups %lld exceed the on-chip sort capacity (16384)",
-                         who, (long long)batch->max_lookups);
+    if (batch->num_bags > 0xFFFFFFFFll)
+        return set_error(DQRM_E_CAPACITY, "%s: more than 2^32 bags", who);
     return DQRM_OK;
 }
 
@@ -1285,7 +1586,7 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
                      void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
-    if ((rc = check_batch_capacity(batch, "dqrm_emb_bwd_sgd"))) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_sgd"))) return rc;
     if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
         return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_sgd");
     if (repack_bits && (repack_bits != 4 || !set->packed))
@@ -1294,48 +1595,65 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     BwdArgs a;
     memset(&a, 0, sizeof(a));
     a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
-    a.sblkmax = set->sblkmax; a.tmax = set->tmax; a.scale = set->scale; a.pscale = set->pscale;
+    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.scale = set->scale; a.pscale = set->pscale;
     a.meta = set->meta; a.err = set->err;
     a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
     a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
     a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4;
     hipStream_t st = (hipStream_t)stream;
-    const size_t lds = table_lds_bytes(batch->max_lookups);
-    a.key_cap = (int)(lds / sizeof(uint64_t));
     const int D = set->dim;
     DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_bwd<LPR, 0>, lds))) return rc;
-        hipLaunchKernelGGL((k_table_bwd<LPR, 0>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
+        if ((rc = allow_lds(k_table_bwd<LPR, 0>, SLOT_LDS))) return rc;
+        hipLaunchKernelGGL((k_table_bwd<LPR, 0>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
     });
     LAUNCH_CHECK();
-    return DQRM_OK;
+    return launch_finalize(set, st);
+}
+
+int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, int64_t max_lookups,
+                                int64_t* ws_cap_base_host) {
+    if (!num_rows_host || !ws_cap_base_host || num_tables <= 0 || max_lookups < 0)
+        return set_error(DQRM_E_INVALID, "dqrm_coalesce_slot_caps: bad arguments");
+    int64_t run = 0;
+    for (int t = 0; t < num_tables; ++t) {
+        for (int s = 0; s < SPLIT; ++s) {
+            const int64_t nblk = (num_rows_host[t] + BLK - 1) / BLK;
+            const int64_t b0 = nblk * s / SPLIT, b1 = nblk * (s + 1) / SPLIT;
+            const int64_t r1 = b1 * BLK < num_rows_host[t] ? b1 * BLK : num_rows_host[t];
+            int64_t rows = r1 - b0 * BLK;
+            if (rows < 0) rows = 0;
+            const int64_t lim = max_lookups < SLOT_KEYS ? max_lookups : SLOT_KEYS;
+            ws_cap_base_host[t * SPLIT + s] = run;
+            run += rows < lim ? rows : lim;
+        }
+    }
+    ws_cap_base_host[num_tables * SPLIT] = run;
+    return run;
 }
 
 int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
-                          int64_t dy_stride_t, int64_t dy_stride_b, int ste,
-                          const int64_t* cap_base, int32_t* rows, float* vals, int32_t* counts,
-                          float* s_loc, int grad_bits, void* stream) {
+                          int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
+                          int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount, float* ws_absmax,
+                          void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
-    if ((rc = check_batch_capacity(batch, "dqrm_emb_bwd_coalesce"))) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_coalesce"))) return rc;
     if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
         return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_coalesce");
-    if (!cap_base || !rows || !vals || !counts || !s_loc || (((uintptr_t)vals) & 15))
-        return set_error(DQRM_E_INVALID, "%s: null/unaligned output", "dqrm_emb_bwd_coalesce");
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !ws_absmax || (((uintptr_t)ws_vals) & 15))
+        return set_error(DQRM_E_INVALID, "%s: null/unaligned workspace", "dqrm_emb_bwd_coalesce");
     BwdArgs a;
     memset(&a, 0, sizeof(a));
     a.W = set->W; a.scale = set->scale; a.meta = set->meta; a.err = set->err;
     a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
     a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables; a.ste = ste;
-    a.cap_base = cap_base; a.rows_out = rows; a.vals_out = vals; a.counts_out = counts; a.s_loc = s_loc;
-    a.grad_bits = grad_bits;
+    a.ws_cap_base = ws_cap_base; a.ws_rows = ws_rows; a.ws_vals = ws_vals; a.ws_ucount = ws_ucount;
+    a.ws_absmax = ws_absmax;
     hipStream_t st = (hipStream_t)stream;
-    const size_t lds = table_lds_bytes(batch->max_lookups);
-    a.key_cap = (int)(lds / sizeof(uint64_t));
     const int D = set->dim;
     DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_bwd<LPR, 1>, lds))) return rc;
-        hipLaunchKernelGGL((k_table_bwd<LPR, 1>), dim3(a.T), dim3(TABLE_WG), lds, st, a);
+        if ((rc = allow_lds(k_table_bwd<LPR, 1>, SLOT_LDS))) return rc;
+        hipLaunchKernelGGL((k_table_bwd<LPR, 1>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
@@ -1345,21 +1663,22 @@ size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_b
     return (size_t)payload_layout(num_tables, cap_total, dim, grad_bits).bytes;
 }
 
-int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* cap_base, int64_t cap_total,
-                         const int32_t* rows, const float* vals, const int32_t* counts,
-                         const float* s_all, int num_ranks, int grad_bits, float* s_avg,
-                         void* payload, void* stream) {
+int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                         const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                         const float* absmax_all, int num_ranks, int grad_bits, const int64_t* cap_base,
+                         int64_t cap_total, float* s_avg, void* payload, void* stream) {
     if (num_tables <= 0 || num_tables > MAX_TABLES || num_ranks <= 0 || num_ranks > 64)
         return set_error(DQRM_E_INVALID, "%s: bad num_tables/num_ranks", "dqrm_grad_quant_pack");
     if (!(grad_bits == 32 || (grad_bits >= 2 && grad_bits <= 16)))
         return set_error(DQRM_E_INVALID, "%s: grad bits %d unsupported", "dqrm_grad_quant_pack", grad_bits);
-    if (!cap_base || !rows || !vals || !counts || !payload || (grad_bits != 32 && (!s_all || !s_avg)))
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !cap_base || !payload ||
+        (grad_bits != 32 && (!absmax_all || !s_avg)))
         return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_grad_quant_pack");
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_LPR(dim, {
-        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(grid_for(cap_total * LPR, 256, 4096)), dim3(256), 0, st,
-                           num_tables, cap_base, cap_total, rows, vals, counts, s_all, num_ranks, grad_bits,
-                           s_avg, (unsigned char*)payload);
+        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(grid_for(ws_cap_total * LPR, 256, 2048)), dim3(256), 0, st,
+                           num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, absmax_all,
+                           num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
@@ -1380,22 +1699,19 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_apply_sparse_update", repack_bits);
     ApplyArgs a;
     a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
-    a.sblkmax = set->sblkmax; a.tmax = set->tmax; a.pscale = set->pscale; a.meta = set->meta;
+    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.pscale = set->pscale; a.meta = set->meta;
     a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
     a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)payload_bytes;
     a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
     a.mode = mode; a.repack = repack_bits == 4;
-    // every table's merged entry count must fit the on-chip sort (checked again on device)
     hipStream_t st = (hipStream_t)stream;
-    a.key_cap = MAX_LDS_KEYS;
-    const size_t lds = table_lds_bytes(MAX_LDS_KEYS);
     const int D = set->dim;
     DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_apply<LPR>, lds))) return rc;
-        hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T), dim3(TABLE_WG), lds, st, a);
+        if ((rc = allow_lds(k_table_apply<LPR>, SLOT_LDS))) return rc;
+        hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
     });
     LAUNCH_CHECK();
-    return DQRM_OK;
+    return launch_finalize(set, st);
 }
 
 int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {

@@ -1,0 +1,299 @@
+"""Drop-in for the reference's ``quantization_supp/quant_modules_not_quantize_grad.py``
+embedding module, backed by libdqrm's HIP kernels (no CPU fallback).
+
+``QuantEmbeddingBagTwo`` keeps the reference constructor and forward signature
+(quant_modules_not_quantize_grad.py:240-248, :317), its attribute / buffer names and
+state-dict keys (:258-280, :288), and its semantics (:317-398):
+
+  * training forward: s = clamp(max|W|, 1e-8) / (2^(b-1)-1) over the WHOLE table
+    (recomputed on every call, as the live snapshot does: the period counters only advance
+    in stringified code, F4 in SURVEY.md), out = EmbeddingBag-sum, y = clamp(round(out/s))*s;
+  * test_mode forward: the last training scale is reused (:331);
+  * full_precision_flag: plain FP32 EmbeddingBag sum;
+  * backward: STE (g*s)/s (quant_utils.py:349-363), then one of
+      grad_mode="sparse"    -> a coalesced sparse COO ``embedding_bag.weight.grad``
+                               (usable by torch.optim.SGD or the DP hooks below),
+      grad_mode="fused_sgd" -> the update W -= lr * grad is applied inside the backward
+                               kernel with torch.optim.SGD's rounding (per lookup, in order),
+      grad_mode="dp"        -> the gradient is kept on device for
+                               sgd_quantized_gradients_parallel_comm.grad_update_parallel_comm.
+
+``QuantEmbeddingBagCollection`` is the fused T-table form used to replace the per-table
+loop of DLRM_Net.apply_emb (dlrm_s_pytorch_single_gpu.py:609-674): one launch per step for
+all tables instead of 26.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib as L
+from .comm import SparseGradExchange
+from .tables import EmbeddingTableSet, LookupBatch
+
+
+def _batch_from_input(input: torch.Tensor, offsets: torch.Tensor | None, device) -> LookupBatch:
+    """nn.EmbeddingBag input conventions: 1-D input + offsets, or 2-D [B, L] fixed bags."""
+    if input.dim() == 2:
+        if offsets is not None:
+            raise ValueError("if input is 2D, then offsets has to be None")
+        B, Lb = input.shape
+        offsets = torch.arange(0, B * Lb, Lb, dtype=torch.int64, device=input.device)
+        input = input.reshape(-1)
+    elif offsets is None:
+        raise ValueError("offsets has to be a 1D Tensor but got None")
+    return LookupBatch([input.reshape(-1)], [offsets.reshape(-1)], device=device)
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    """Autograd bridge: forward = dqrm_emb_fwd; backward per the module's grad_mode."""
+
+    @staticmethod
+    def forward(ctx, weight, owner, batches, bits, flags_refresh, full_precision, layout):
+        tset: EmbeddingTableSet = owner._tset
+        y = tset.forward(batches, bits=bits, refresh_scale=flags_refresh, use_packed=owner._use_packed(full_precision),
+                         full_precision=full_precision, layout=layout)
+        ctx.owner = owner
+        ctx.batches = batches
+        ctx.ste = not full_precision
+        ctx.layout = layout
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        owner = ctx.owner
+        dy = dy.contiguous()
+        grad_w = owner._backward(ctx.batches, dy, ctx.ste, ctx.layout)
+        return grad_w, None, None, None, None, None, None
+
+
+class _WeightHolder(nn.Module):
+    """Carries ``weight`` so that the reference's attribute path
+    ``module.embedding_bag.weight`` (and the state-dict key) is unchanged."""
+
+    def __init__(self, weight: nn.Parameter, mode: str = "sum", sparse: bool = True):
+        super().__init__()
+        self.weight = weight
+        self.mode = mode
+        self.sparse = sparse
+
+
+class _QuantEmbeddingBase(nn.Module):
+    grad_modes = ("sparse", "fused_sgd", "dp")
+
+    def _init_common(self, grad_mode, lr, scale_period, use_packed_int4):
+        if grad_mode not in self.grad_modes:
+            raise ValueError(f"grad_mode must be one of {self.grad_modes}")
+        self.grad_mode = grad_mode
+        self.lr = lr
+        # period P of the (stringified in the snapshot) periodic scale refresh,
+        # quant_modules_not_quantize_grad.py:303-315,354-363; 0 = every training call (live code)
+        self.scale_period = int(scale_period)
+        self.use_packed_int4 = bool(use_packed_int4)
+        self._pending = None      # (batch, dy, ste, layout) for grad_mode == "dp"
+        self._exchange = None
+        self._counters = None     # host mirror of (now_iteration, iteration_bound, iteration_nt)
+
+    # ------------------------------------------------------------ scale refresh logic
+    def _refresh_due(self, fp: bool, test_mode: bool) -> bool:
+        """q_m_n_q_g.py:331-363: recompute when training (or first call); with a period the
+        counters now_iteration / iteration_bound / iteration_nt follow the reference code."""
+        first = tuple(self.eb_scaling_factor.shape) == (self.batch_size, 1)
+        if not ((not fp and not test_mode) or first):
+            return False
+        if self.scale_period <= 0:
+            return True  # live snapshot: the counters never advance, now == bound == 0
+        if self._counters is None:  # one host read after construction / load_state_dict
+            self._counters = [int(self.now_iteration.item()), int(self.iteration_bound.item()),
+                              int(self.iteration_nt.item())]
+        now, bound, nt = self._counters
+        due = now == bound
+        if due:  # update period info + set_iteration_bound (q_m_n_q_g.py:303-315,354-363)
+            nt += 1
+            now = 0
+            if nt == 1 and bound == 0:
+                bound += self.scale_period
+        else:
+            nt += 1
+            now += 1
+        self._counters = [now, bound, nt]
+        self.now_iteration.fill_(now)
+        self.iteration_bound.fill_(bound)
+        self.iteration_nt.fill_(nt)
+        return due
+
+    def _use_packed(self, full_precision: bool) -> bool:
+        return self.use_packed_int4 and not full_precision and self._tset.packed is not None
+
+    # ------------------------------------------------------------ backward
+    def _backward(self, batch: LookupBatch, dy: torch.Tensor, ste: bool, layout: str):
+        ts = self._tset
+        if self.grad_mode == "fused_sgd":
+            if self.lr is None:
+                raise RuntimeError("grad_mode='fused_sgd' needs module.lr")
+            ts.backward_sgd(batch, dy, self.lr, ste=ste, repack=self._use_packed(False), layout=layout)
+            return None
+        if self.grad_mode == "dp":
+            self._pending = (batch, dy, ste, layout)
+            return None
+        return self._sparse_grad(batch, dy, ste, layout)
+
+    def _sparse_grad(self, batch, dy, ste, layout):
+        ex = SparseGradExchange(self._tset, max(batch.max_lookups, 1), grad_bits=32, device=self._tset.device)
+        self._tset.backward_coalesce(batch, dy, ex.ws, ste=ste, layout=layout)
+        ws = ex.ws
+        rows, vals = [], []
+        uc = ws.ucount.cpu().tolist()
+        base = ws.slot_base
+        for k, u in enumerate(uc):
+            if u:  # slot k = t * DQRM_TABLE_SPLIT + s; table-local rows -> slab rows
+                t = k // L.DQRM_TABLE_SPLIT
+                rows.append(ws.rows[base[k]: base[k] + u].to(torch.int64) + self._tset.row_base[t])
+                vals.append(ws.vals[base[k]: base[k] + u])
+        R, D = self._tset.R, self._tset.D
+        dev = self._tset.device
+        if not rows:
+            return torch.sparse_coo_tensor(torch.zeros(1, 0, dtype=torch.int64, device=dev),
+                                           torch.zeros(0, D, device=dev), (R, D))
+        g_rows = torch.cat(rows).to(torch.int64)
+        return torch.sparse_coo_tensor(g_rows.view(1, -1), torch.cat(vals), (R, D))._coalesced_(True)
+
+
+class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
+    """quant_modules_not_quantize_grad.py:220-398, one table, on libdqrm."""
+
+    def __init__(self, num_embeddings, embedding_dim, embedding_bit=4, full_precision_flag=False,
+                 quant_mode="symmetric", fix_flag=False, weight_percentile=0, embedding_id=None, *,
+                 device="cuda", weight: torch.Tensor | None = None, init: str = "numpy",
+                 grad_mode: str = "sparse", lr: float | None = None, scale_period: int = 0,
+                 use_packed_int4: bool = False):
+        super().__init__()
+        self.num_embeddings = num_embeddings
+        self.embedding_dim = embedding_dim
+        self.embedding_bit = embedding_bit
+        self.full_precision_flag = full_precision_flag
+        self.quant_mode = quant_mode
+        self.fix_flag = fix_flag
+        self.weight_percentile = weight_percentile
+        self.batch_size = 128
+        self.embedding_id = embedding_id
+        self._init_common(grad_mode, lr, scale_period, use_packed_int4)
+        if weight is None and init == "numpy":
+            # q_m_n_q_g.py:273-275: numpy global RNG, U(-sqrt(1/n), sqrt(1/n)), f32
+            weight = torch.from_numpy(np.random.uniform(
+                low=-np.sqrt(1 / num_embeddings), high=np.sqrt(1 / num_embeddings),
+                size=(num_embeddings, embedding_dim)).astype(np.float32))
+        self._tset = EmbeddingTableSet([num_embeddings], embedding_dim, device=device, packed=use_packed_int4,
+                                       init=None if weight is not None else "uniform",
+                                       weights=[weight] if weight is not None else None)
+        dev = self._tset.device
+        self.register_buffer("eb_scaling_factor", torch.zeros(self.batch_size, 1, device=dev), persistent=True)
+        self.register_buffer("output_integer", torch.zeros((1, 16), device=dev), persistent=False)
+        self.register_buffer("embedding_bound", torch.sqrt(torch.tensor(1 / num_embeddings, device=dev)) * 4.0,
+                             persistent=False)
+        self.register_buffer("now_iteration", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("iteration_bound", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("iteration_nt", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("emb_scaling_factor", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("gradient_bit_width", torch.zeros(1, device=dev), persistent=True)
+        self.embedding_bag = _WeightHolder(nn.Parameter(self._tset.W, requires_grad=True))
+
+    def __repr__(self):
+        s = super().__repr__()
+        return "(" + s + " embedding_bit = {}, full_precision_flag = {}, quant_mode = {})".format(
+            self.embedding_bit, self.full_precision_flag, self.quant_mode)
+
+    def fix(self):
+        self.fix_flag = True
+
+    def unfix(self):
+        self.fix_flag = False
+
+    def forward(self, input, offsets=None, per_sample_weights=None, full_precision_flag=False, test_mode=False):
+        fp = bool(full_precision_flag or self.full_precision_flag)
+        if self.quant_mode not in ("symmetric", "speed_symmetric", "asymmetric"):
+            raise ValueError("unknown quant mode: {}".format(self.quant_mode))
+        refresh = self._refresh_due(fp, test_mode)
+        if refresh and self.quant_mode != "symmetric":
+            raise Exception("for embedding weights, we only support symmetric quantization")
+        if per_sample_weights is not None:
+            print("Warning: Embedding Table Assumes per_sample_weights to be None but it is not")
+        batch = _batch_from_input(input, offsets, self._tset.device)
+        if refresh and self._use_packed(fp):
+            self._tset.refresh_scale_and_pack(self.embedding_bit)
+            refresh_in_fwd = False
+        else:
+            refresh_in_fwd = refresh
+        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "tbd")
+        if refresh:
+            self.eb_scaling_factor = self._tset.scale.view(())  # 0-d scale, as the reference stores it
+        return y[0]
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._tset.refresh_absmax()  # W changed outside the kernels: rebuild the |W| hierarchy
+        self._counters = None
+        return out
+
+
+class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
+    """All tables of a DLRM in one resident slab; forward(lS_o, lS_i) replaces the per-table
+    loop of DLRM_Net.apply_emb (dlrm_s_pytorch_single_gpu.py:609-674) with ONE launch."""
+
+    def __init__(self, ln: Sequence[int], m: int, embedding_bit: int = 4, full_precision_flag: bool = False,
+                 *, device="cuda", init: str = "numpy", weights: Sequence[torch.Tensor] | None = None,
+                 grad_mode: str = "sparse", lr: float | None = None, scale_period: int = 0,
+                 use_packed_int4: bool = False, seed: int = 123):
+        super().__init__()
+        self.ln = [int(n) for n in ln]
+        self.embedding_dim = int(m)
+        self.embedding_bit = embedding_bit
+        self.full_precision_flag = full_precision_flag
+        self.quant_mode = "symmetric"
+        self.batch_size = 128
+        self._init_common(grad_mode, lr, scale_period, use_packed_int4)
+        if weights is None and init == "numpy":
+            weights = [torch.from_numpy(np.random.uniform(low=-np.sqrt(1 / n), high=np.sqrt(1 / n),
+                                                          size=(n, m)).astype(np.float32)) for n in self.ln]
+        self._tset = EmbeddingTableSet(self.ln, m, device=device, packed=use_packed_int4,
+                                       init=None if weights is not None else "uniform", seed=seed, weights=weights)
+        dev = self._tset.device
+        T = len(self.ln)
+        self.register_buffer("eb_scaling_factor", torch.zeros(self.batch_size, 1, device=dev), persistent=True)
+        self.register_buffer("now_iteration", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("iteration_bound", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("iteration_nt", torch.zeros(1, device=dev), persistent=True)
+        self.register_buffer("emb_scaling_factor", torch.zeros(T, device=dev), persistent=True)
+        self.embedding_bag = _WeightHolder(nn.Parameter(self._tset.W, requires_grad=True))
+
+    def table_weight(self, t: int) -> torch.Tensor:
+        return self._tset.table_weight(t)
+
+    def forward(self, lS_o, lS_i, full_precision_flag=False, test_mode=False, layout="list"):
+        """lS_o / lS_i: per-table lists or stacked [T, B] tensors (dlrm_data_pytorch.py:328-345).
+        layout "list" -> list of T [B, D] tensors (apply_emb's ly); "btd" -> [B, T, D]."""
+        fp = bool(full_precision_flag or self.full_precision_flag)
+        refresh = self._refresh_due(fp, test_mode)
+        batch = LookupBatch(lS_i, lS_o, device=self._tset.device)
+        if refresh and self._use_packed(fp):
+            self._tset.refresh_scale_and_pack(self.embedding_bit)
+            refresh_in_fwd = False
+        else:
+            refresh_in_fwd = refresh
+        kl = "btd" if layout == "btd" else "tbd"
+        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, kl)
+        if refresh:
+            self.eb_scaling_factor = self._tset.scale
+        return list(y.unbind(0)) if layout == "list" else y
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._tset.refresh_absmax()
+        self._counters = None
+        return out
+
+
+__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection"]

@@ -144,11 +144,12 @@ class EmbeddingTableSet:
         ).contiguous()
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tflags = torch.zeros(T, dtype=torch.int32, device=dev)
+        self.sdirty = torch.zeros(NS, dtype=torch.uint8, device=dev)
         self._c = L.TableSet(
             T, D, self.R, NB, NS,
             _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
             _ptr(self.tmax), _ptr(self.scale), _ptr(self.pscale), _ptr(self.meta), _ptr(self.err),
-            _ptr(self.tflags),
+            _ptr(self.tflags), _ptr(self.sdirty),
         )
         if weights is not None:
             if len(weights) != T:
@@ -199,6 +200,7 @@ class EmbeddingTableSet:
         full_precision: bool = False,
         out: torch.Tensor | None = None,
         layout: str = "tbd",
+        nt_store: bool | None = None,
     ) -> torch.Tensor:
         """Fused T-table fake-quant EmbeddingBag (q_m_n_q_g.py:317-398 for every table).
 
@@ -221,8 +223,12 @@ class EmbeddingTableSet:
             flags |= L.DQRM_FWD_USE_PACKED
         if full_precision:
             flags |= L.DQRM_FWD_FULL_PRECISION
-        if layout != "tbd":
-            flags |= L.DQRM_FWD_BAG_MAJOR
+        if nt_store is None:
+            # stream the output past the caches once it cannot stay in the 256 MiB
+            # Infinity Cache anyway (measured: +10-27% at 0.4-1.7 GB, -9% at 109 MB)
+            nt_store = B * T * D * 4 > (192 << 20)
+        if nt_store:
+            flags |= L.DQRM_FWD_NT_STORE
         L.check(
             self.lib.dqrm_emb_fwd(C.byref(self._c), C.byref(batch.c), bits, flags, _ptr(out), st, sb,
                                   _stream_handle()),
@@ -254,52 +260,64 @@ class EmbeddingTableSet:
         )
 
     def backward_coalesce(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad",
-                          ste: bool = True, grad_bits: int = 8, layout: str = "tbd") -> None:
-        """STE + sparse backward + coalesce + local grad scale (s_q_g_p_c.py:850-861)."""
+                          ste: bool = True, layout: str = "tbd") -> None:
+        """STE + sparse backward + coalesce + per-slot max |grad| (s_q_g_p_c.py:850-861)."""
         st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
         L.check(
             self.lib.dqrm_emb_bwd_coalesce(
-                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.cap_base),
-                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.counts), _ptr(ws.s_loc), grad_bits,
-                _stream_handle()),
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.slot_cap_base),
+                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), _stream_handle()),
             "dqrm_emb_bwd_coalesce",
         )
 
 
+def slot_caps(num_rows: Sequence[int], max_lookups: int) -> list[int]:
+    """Exclusive prefix of the coalesce-slot capacities (dqrm_coalesce_slot_caps): slot
+    t*S+s holds at most min(max_lookups, rows in row-range s of table t) entries."""
+    lib = L.load()
+    T = len(num_rows)
+    nr = (C.c_int64 * T)(*[int(n) for n in num_rows])
+    out = (C.c_int64 * (T * L.DQRM_TABLE_SPLIT + 1))()
+    total = lib.dqrm_coalesce_slot_caps(nr, T, int(max_lookups), out)
+    if total < 0:
+        L.check(int(total), "dqrm_coalesce_slot_caps")
+    return list(out)
+
+
 @dataclass
 class CoalescedGrad:
-    """Fixed-capacity coalesced sparse gradient of all tables (one rank)."""
+    """Coalesced sparse gradient of all tables (one rank), in row-range slots: slot
+    k = t * DQRM_TABLE_SPLIT + s (include/dqrm.h)."""
 
-    caps: list[int]
-    cap_base: torch.Tensor   # i64 [T+1]
-    rows: torch.Tensor       # i32 [CAP]
-    vals: torch.Tensor       # f32 [CAP, D]
-    counts: torch.Tensor     # i32 [T]
-    s_loc: torch.Tensor      # f32 [T]
+    slot_base: list[int]        # host copy of slot_cap_base
+    slot_cap_base: torch.Tensor  # i64 [T*S+1]
+    rows: torch.Tensor           # i32 [WCAP]
+    vals: torch.Tensor           # f32 [WCAP, D]
+    ucount: torch.Tensor         # i32 [T*S]
+    absmax: torch.Tensor         # f32 [T*S]
 
     @classmethod
-    def allocate(cls, caps: Sequence[int], dim: int, device) -> "CoalescedGrad":
-        caps = [int(c) for c in caps]
-        base = [0]
-        for c in caps:
-            base.append(base[-1] + c)
-        CAP = base[-1]
+    def allocate(cls, num_rows: Sequence[int], max_lookups: int, dim: int, device) -> "CoalescedGrad":
+        base = slot_caps(num_rows, max_lookups)
+        W = base[-1]
+        TS = len(num_rows) * L.DQRM_TABLE_SPLIT
         return cls(
-            caps=caps,
-            cap_base=torch.tensor(base, dtype=torch.int64, device=device),
-            rows=torch.zeros(max(CAP, 1), dtype=torch.int32, device=device),
-            vals=torch.zeros(max(CAP, 1), dim, dtype=torch.float32, device=device),
-            counts=torch.zeros(len(caps), dtype=torch.int32, device=device),
-            s_loc=torch.zeros(len(caps), dtype=torch.float32, device=device),
+            slot_base=base,
+            slot_cap_base=torch.tensor(base, dtype=torch.int64, device=device),
+            rows=torch.zeros(max(W, 1), dtype=torch.int32, device=device),
+            vals=torch.zeros(max(W, 1), dim, dtype=torch.float32, device=device),
+            ucount=torch.zeros(TS, dtype=torch.int32, device=device),
+            absmax=torch.zeros(TS, dtype=torch.float32, device=device),
         )
 
     @property
     def cap_total(self) -> int:
-        return sum(self.caps)
+        return self.slot_base[-1]
 
 
 def default_caps(num_rows: Sequence[int], max_lookups: int) -> list[int]:
-    """cap_t = min(max lookups per table, n_t): the most unique rows a table can touch."""
+    """Payload capacity per table: cap_t = min(max lookups per table, n_t), the most
+    unique rows one rank can send for table t."""
     return [min(int(max_lookups), int(n)) for n in num_rows]
 
 
@@ -312,4 +330,4 @@ def reference_scale(absmax: float, bits: int) -> float:
     return float(np.float32(a) / np.float32(2 ** (bits - 1) - 1))
 
 
-__all__ = ["LookupBatch", "EmbeddingTableSet", "CoalescedGrad", "default_caps", "reference_scale"]
+__all__ = ["LookupBatch", "EmbeddingTableSet", "CoalescedGrad", "default_caps", "slot_caps", "reference_scale"]

@@ -61,6 +61,8 @@ extern "C" {
 
 #define DQRM_BLOCK_ROWS   256     /* rows per blkmax entry */
 #define DQRM_SBLOCK_ROWS  65536   /* rows per sblkmax entry */
+#define DQRM_TABLE_SPLIT  8       /* workgroups (row-range slots) per table in the backward */
+#define DQRM_SLOT_KEYS    8192    /* max lookups / merged entries one slot sorts on chip */
 
 /* Resident state of T tables. All pointers are device pointers. */
 typedef struct dqrm_table_set {
@@ -80,6 +82,7 @@ typedef struct dqrm_table_set {
     const int64_t* meta;      /* [4][T]: row_base, num_rows, blk_base, sblk_base */
     uint32_t* err;            /* 1 word, device-side error flags */
     uint32_t* tflags;         /* [T] scratch (repack decision), library-internal */
+    uint8_t*  sdirty;         /* [NS] zero-initialised scratch (superblock rescan flags) */
 } dqrm_table_set;
 
 /* A batch of lookups for all T tables, in the reference's per-table
@@ -87,7 +90,10 @@ typedef struct dqrm_table_set {
  *   idx      i64 [sum_t L_t]  table t's indices at [idx_base[t], idx_base[t+1])
  *   off      i64 [T][B]       bag b of table t = idx_base[t] + [off[t][b], off[t][b+1])
  *                             (last bag ends at L_t), exactly nn.EmbeddingBag offsets
- *   idx_base i64 [T+1]        device copy */
+ *   idx_base i64 [T+1]        device copy
+ * Backward capacity: the lookups of one table that fall in one row-range slot (1/8 of
+ * the table's 256-row blocks) must not exceed DQRM_SLOT_KEYS (DQRM_E_CAPACITY / the
+ * DQRM_ERRF_OVERFLOW flag otherwise). */
 typedef struct dqrm_batch {
     const int64_t* idx;
     const int64_t* off;
@@ -100,7 +106,7 @@ typedef struct dqrm_batch {
 #define DQRM_FWD_REFRESH_SCALE 1u  /* s_t = clamp(tmax_t, 1e-8)/(2^(bits-1)-1), write scale[] */
 #define DQRM_FWD_USE_PACKED    2u  /* single-lookup bags read INT4 rows (valid iff pscale==scale) */
 #define DQRM_FWD_FULL_PRECISION 4u /* full_precision_flag: plain FP32 sum, no fake-quant */
-#define DQRM_FWD_BAG_MAJOR     8u  /* iterate bags b-major (output [B][T][D]) for coalescing */
+#define DQRM_FWD_NT_STORE      16u /* stream the output with non-temporal stores (packed path) */
 
 /* ---------------------------------------------------------------------------------
  * Table maintenance
@@ -150,36 +156,48 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
 /* ---------------------------------------------------------------------------------
  * Data-parallel gradient path (sgd_quantized_gradients_parallel_comm.py)
  *
- * Coalesced-gradient buffer (per rank), fixed capacity per table:
- *   cap_base i64 [T+1] (device)  table t owns entries [cap_base[t], cap_base[t+1])
- *   rows     i32 [CAP]           ascending unique local row ids
- *   vals     f32 [CAP][D]        coalesced sums
- *   counts   i32 [T]             U_t
+ * Coalesced-gradient workspace (per rank). Slot k = t * DQRM_TABLE_SPLIT + s holds the
+ * coalesced rows of table t that fall in row range s (ascending, unique):
+ *   ws_cap_base i64 [T*S+1] (device)  slot k owns entries [ws_cap_base[k], ws_cap_base[k+1])
+ *   ws_rows     i32 [WCAP]            local row ids
+ *   ws_vals     f32 [WCAP][D]         coalesced sums
+ *   ws_ucount   i32 [T*S]             entries used per slot
+ *   ws_absmax   f32 [T*S]             max |vals| per slot (the local scale's input)
+ * dqrm_coalesce_slot_caps() gives the slot capacities (host).
  * ------------------------------------------------------------------------------ */
 
-/* STE backward + EmbeddingBag sparse backward + grad.coalesce() (s_q_g_p_c.py:859) +
- * local scale s_loc[t] = clamp(max|vals_t|, 1e-8) / (2^(grad_bits-1)-1) (:861,
- * quant_utils.py:141-194). grad_bits = 0 skips the scale (FP32 gradient path). */
+/* Host helper: slot capacities cap[t*S+s] = min(max_lookups, rows in slot s of table t);
+ * writes the exclusive prefix into ws_cap_base_host[T*S+1]; returns WCAP (>= 0). */
+int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, int64_t max_lookups,
+                                int64_t* ws_cap_base_host);
+
+/* STE backward + EmbeddingBag sparse backward + grad.coalesce() (s_q_g_p_c.py:859),
+ * plus the per-slot max |value| feeding the local scale
+ * s_loc[t] = clamp(max|vals_t|, 1e-8) / (2^(bits-1)-1) (:861, quant_utils.py:141-194). */
 int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
                           const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
-                          int ste, const int64_t* cap_base, int32_t* rows, float* vals,
-                          int32_t* counts, float* s_loc, int grad_bits, void* stream);
+                          int ste, const int64_t* ws_cap_base, int32_t* ws_rows, float* ws_vals,
+                          int32_t* ws_ucount, float* ws_absmax, void* stream);
 
 /* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
  *   [counts i32 T | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
- *   int8 (bits<=8) / int16 (bits<=16) / f32 (bits==32, unquantized path)]        */
+ *   int8 (bits<=8) / int16 (bits<=16) / f32 (bits==32, unquantized path)]
+ * table t's entries sit at [cap_base[t], cap_base[t] + counts[t]), rows ascending. */
 size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits);
 
-/* Scale average + quantize-pack (s_q_g_p_c.py:863-869):
- *   s[t] = (((s_all[N-1][t] + s_all[N-2][t]) + ...) + s_all[0][t]) * (1/N)
+/* Scale average + quantize-pack (s_q_g_p_c.py:861-869). absmax_all = the N ranks'
+ * ws_absmax gathered [N][T*S]. Per table:
+ *   s_r  = clamp(max_s absmax_all[r][t*S+s], 1e-8) / (2^(bits-1)-1)     (rank r's scale)
+ *   s    = (((s_{N-1} + s_{N-2}) + ...) + s_0) * (1/N)
  *          (Gloo's one-element allreduce order; identical on every rank; -> s_avg)
- *                                                                [bits 2..16 only]
  *   q    = clamp(round(1/s * v + 0), -2^(bits-1), 2^(bits-1)-1)  (quant_utils.py:101,343)
- * grad_bits = 32 copies FP32 values (emb_grad_quantized=False path, :319-327). */
-int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* cap_base, int64_t cap_total,
-                         const int32_t* rows, const float* vals, const int32_t* counts,
-                         const float* s_all, int num_ranks, int grad_bits,
-                         float* s_avg, void* payload, void* stream);
+ * and the slots are compacted into the dense payload. grad_bits = 32 copies FP32 values
+ * (emb_grad_quantized=False path, :319-327); absmax_all / s_avg may then be NULL. */
+int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                         const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                         const float* absmax_all, int num_ranks, int grad_bits,
+                         const int64_t* cap_base, int64_t cap_total, float* s_avg, void* payload,
+                         void* stream);
 
 /* update modes for dqrm_apply_sparse_update */
 #define DQRM_UPD_DP        0  /* v = ((Q * (1/N)) * s) ; W += -lr * v   (s_q_g_p_c.py:885,618-622) */

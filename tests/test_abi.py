@@ -41,8 +41,8 @@ def test_payload_bytes_agree(lib):
 
 
 def test_struct_layouts():
-    # dqrm_table_set: 2 x i32 + 3 x i64 + 11 pointers; dqrm_batch: 3 pointers + 2 x i64
-    assert C.sizeof(L.TableSet) == 8 + 24 + 11 * 8
+    # dqrm_table_set: 2 x i32 + 3 x i64 + 12 pointers; dqrm_batch: 3 pointers + 2 x i64
+    assert C.sizeof(L.TableSet) == 8 + 24 + 12 * 8
     assert C.sizeof(L.Batch) == 5 * 8
 
 
@@ -53,8 +53,21 @@ def test_invalid_arguments_rejected_without_device(lib):
     ts.num_tables, ts.dim = 2, 12  # dim must be 4 * 2^k
     assert lib.dqrm_emb_fwd(C.byref(ts), None, 4, 0, None, 0, 0, None) == L.DQRM_E_INVALID
     assert b"dim" in lib.dqrm_last_error()
-    assert lib.dqrm_grad_quant_pack(0, 16, None, 0, None, None, None, None, 1, 8, None, None, None) == L.DQRM_E_INVALID
-    assert lib.dqrm_grad_quant_pack(2, 16, None, 0, None, None, None, None, 1, 7 + 30, None, None, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_grad_quant_pack(0, 16, None, 0, None, None, None, None, 1, 8, None, 0, None, None, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_grad_quant_pack(2, 16, None, 0, None, None, None, None, 1, 37, None, 0, None, None, None) == L.DQRM_E_INVALID
+
+
+def test_slot_caps_partition():
+    from deep_quantized_recommendation_model_dqrm_amd.tables import slot_caps
+    rows = [3, 1000, 10**7, 256 * 9]
+    base = slot_caps(rows, 2048)
+    S = L.DQRM_TABLE_SPLIT
+    assert len(base) == len(rows) * S + 1 and base[0] == 0
+    caps = [base[k + 1] - base[k] for k in range(len(rows) * S)]
+    # every row of a table lands in exactly one slot; a slot holds <= min(max_lookups, its rows)
+    assert sum(caps[0:S]) == 3 and sum(caps[S:2 * S]) == 1000
+    assert all(c <= 2048 for c in caps)
+    assert sum(caps[3 * S:4 * S]) == 256 * 9
 
 
 def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):

@@ -133,7 +133,7 @@ def test_packed_int4_path_bitexact(dq, golden_dir):
         np.testing.assert_array_equal(P2[base:base + n], O.pack_int4(W_host[base:base + n], s2[t]))
 
 
-def _emulate_ranks(dq, ts, caps, rank_batches, rank_dys, grad_bits, lr, mode=None, repack=False):
+def _emulate_ranks(dq, ts, rank_batches, rank_dys, grad_bits, lr, mode=None, repack=False):
     """Run the exchange's three device steps for N ranks on one GPU (the all-gathers become
     stacking), exactly as SparseGradExchange does on each rank."""
     from deep_quantized_recommendation_model_dqrm_amd import _lib as L
@@ -141,21 +141,30 @@ def _emulate_ranks(dq, ts, caps, rank_batches, rank_dys, grad_bits, lr, mode=Non
 
     N = len(rank_batches)
     k = HipExchangeKernels(ts)
+    max_lookups = max(b.max_lookups for b in rank_batches)
     wss = []
     for r in range(N):
-        ws = dq.CoalescedGrad.allocate(caps, ts.D, "cuda")
-        k.coalesce(rank_batches[r], rank_dys[r], ws, True, grad_bits, "tbd")
+        ws = dq.CoalescedGrad.allocate(ts.num_rows, max_lookups, ts.D, "cuda")
+        k.coalesce(rank_batches[r], rank_dys[r], ws, True, "tbd")
         wss.append(ws)
-    s_all = torch.stack([ws.s_loc for ws in wss])
-    P = payload_bytes(ts.T, wss[0].cap_total, ts.D, grad_bits)
+    absmax_all = torch.stack([ws.absmax for ws in wss])
+    caps = dq.default_caps(ts.num_rows, max_lookups)
+    cap_base = torch.tensor(np.concatenate([[0], np.cumsum(caps)]), dtype=torch.int64, device="cuda")
+    cap_total = int(sum(caps))
+    P = payload_bytes(ts.T, cap_total, ts.D, grad_bits)
     payloads = torch.zeros(N, P, dtype=torch.uint8, device="cuda")
     s_avg = torch.zeros(ts.T, dtype=torch.float32, device="cuda")
     for r in range(N):
-        k.quant_pack(wss[r], s_all, N, grad_bits, s_avg, payloads[r])
+        k.quant_pack(wss[r], absmax_all, N, grad_bits, cap_base, cap_total, s_avg, payloads[r])
     if mode is None:
         mode = L.DQRM_UPD_FP32 if grad_bits == 32 else L.DQRM_UPD_DP
-    k.apply(wss[0], payloads, P, N, grad_bits, s_avg, lr, mode, repack)
-    return wss, payloads, s_avg
+    k.apply(cap_base, cap_total, payloads, P, N, grad_bits, s_avg, lr, mode, repack)
+    return wss, payloads, s_avg, cap_base.cpu().numpy()
+
+
+def _local_scale(ws, T, bits):
+    a = ws.absmax.view(T, -1).max(dim=1).values.cpu().numpy()
+    return np.array([O.sym_scale(x, bits) for x in a], dtype=f32)
 
 
 def _decode_payload(p, T, cap_base, D, bits, t):
@@ -189,14 +198,12 @@ def test_data_parallel_exchange_bitexact(dq, golden_dir, name):
         rank_dys = [torch.from_numpy(np.stack(dys[r])).cuda() for r in range(N)]
         for rb in rank_batches:  # each rank's forward refreshes the same scale
             ts.forward(rb, refresh_scale=True)
-        caps = dq.default_caps(num_rows, max(rb.max_lookups for rb in rank_batches))
-        wss, payloads, s_avg = _emulate_ranks(dq, ts, caps, rank_batches, rank_dys, gb, float(fx["lr"]))
+        wss, payloads, s_avg, cb = _emulate_ranks(dq, ts, rank_batches, rank_dys, gb, float(fx["lr"]))
         if quantized:
-            cb = wss[0].cap_base.cpu().numpy()
             for t in range(len(num_rows)):
                 assert s_avg[t].item() == fx[f"k{k}_t{t}_s_avg"]
                 for r in range(N):
-                    assert wss[r].s_loc[t].item() == fx[f"k{k}_t{t}_r{r}_s_loc"]
+                    assert _local_scale(wss[r], len(num_rows), bits)[t] == fx[f"k{k}_t{t}_r{r}_s_loc"]
                     rows, q = _decode_payload(payloads[r], len(num_rows), cb, D, bits, t)
                     np.testing.assert_array_equal(rows, fx[f"k{k}_t{t}_r{r}_rows"])
                     np.testing.assert_array_equal(q, fx[f"k{k}_t{t}_r{r}_q"])
@@ -224,18 +231,20 @@ def test_simulated_dp_bitexact(dq, golden_dir):
     from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels, payload_bytes
     kern = HipExchangeKernels(ts)
     caps = dq.default_caps(num_rows, B)
+    cap_base = torch.tensor(np.concatenate([[0], np.cumsum(caps)]), dtype=torch.int64, device="cuda")
+    cap_total = int(sum(caps))
     wss = []
     for k in range(N):
-        ws = dq.CoalescedGrad.allocate(caps, D, "cuda")
-        kern.coalesce(batches[k], dys[k], ws, True, 8, "tbd")
+        ws = dq.CoalescedGrad.allocate(num_rows, B, D, "cuda")
+        kern.coalesce(batches[k], dys[k], ws, True, "tbd")
         wss.append(ws)
-    s_first = wss[0].s_loc.clone()
-    Pb = payload_bytes(len(num_rows), wss[0].cap_total, D, 8)
+    first_absmax = wss[0].absmax.clone().view(1, -1)
+    Pb = payload_bytes(len(num_rows), cap_total, D, 8)
     payloads = torch.zeros(N, Pb, dtype=torch.uint8, device="cuda")
-    s_avg = torch.zeros(len(num_rows), dtype=torch.float32, device="cuda")
+    s_first = torch.zeros(len(num_rows), dtype=torch.float32, device="cuda")
     for k in range(N):
-        kern.quant_pack(wss[k], s_first.view(1, -1), 1, 8, s_avg, payloads[k])
-    kern.apply(wss[0], payloads, Pb, N, 8, s_first, 0.1, L.DQRM_UPD_SIMULATED, False)
+        kern.quant_pack(wss[k], first_absmax, 1, 8, cap_base, cap_total, s_first, payloads[k])
+    kern.apply(cap_base, cap_total, payloads, Pb, N, 8, s_first, 0.1, L.DQRM_UPD_SIMULATED, False)
     for t in range(len(num_rows)):
         assert s_first[t].item() == fx[f"s_t{t}"]
         np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), fx[f"w_t{t}"])
@@ -256,11 +265,14 @@ def test_invalid_indices_flag_not_fault(dq):
     assert ts.read_errors() & L.DQRM_ERRF_INDEX
 
 
-def test_capacity_error_is_reported(dq):
+def test_capacity_overflow_is_flagged(dq):
+    """One row-range slot receiving more than DQRM_SLOT_KEYS lookups is flagged, not faulted."""
     ts = make_set(dq, G.table_weights([100], 16, 3))
-    b = dq.LookupBatch.pooling_one(torch.zeros(1, 20000, dtype=torch.int64, device="cuda"))
-    with pytest.raises(dq._lib.DQRMError):
-        ts.backward_sgd(b, torch.zeros(1, 20000, 16, device="cuda"), lr=0.1)
+    W0 = ts.W.clone()
+    b = dq.LookupBatch.pooling_one(torch.zeros(1, 9000, dtype=torch.int64, device="cuda"))
+    ts.backward_sgd(b, torch.ones(1, 9000, 16, device="cuda"), lr=0.1)
+    assert ts.read_errors() & dq._lib.DQRM_ERRF_OVERFLOW
+    assert torch.equal(ts.W, W0)  # the overflowing slot did not touch its rows
 
 
 def test_kaggle_full_size_forward_and_step(dq):
