@@ -527,9 +527,30 @@ __global__ void __launch_bounds__(256) k_emb_fwd_packed(FwdArgs a) {
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
 constexpr int TWG = 512;                       // threads per (table, slot) workgroup
 constexpr int SLOT_KEYS = DQRM_SLOT_KEYS;      // keys one slot sorts on chip (64 KiB)
-constexpr int TILE_FLOATS = 2048;              // per-wave LDS tile for long segments (8 KiB)
-// dynamic LDS of a slot workgroup: keys u64 | heads u16 | one tile per wave  (144 KiB)
-constexpr int SLOT_LDS = SLOT_KEYS * 8 + SLOT_KEYS * 2 + (TWG / WAVE) * TILE_FLOATS * 4;
+
+constexpr int LONG_SEG = 8;   // longer segments are combined block-cooperatively
+constexpr int LONG_SEGS_MAX = SLOT_KEYS / (LONG_SEG + 1) + 1;
+constexpr int STAGE_FLOATS = 16384;                        // 64 KiB
+constexpr int STAGE_F4 = STAGE_FLOATS / 4 / TWG;           // 8 float4 per thread per chunk
+constexpr int CARRY_FLOATS = 2 * 256;                      // two rows of max D
+constexpr int LPRE_INTS = (LONG_SEGS_MAX + 1 + 3) / 4 * 4;
+// dynamic LDS of a slot workgroup: keys u64 | heads u16 | stage | carry | long prefix
+constexpr int SLOT_LDS = SLOT_KEYS * 8 + SLOT_KEYS * 2 + STAGE_FLOATS * 4 + CARRY_FLOATS * 4 + LPRE_INTS * 4;
+static_assert(SLOT_LDS + 4096 <= 160 * 1024, "slot LDS budget");
+
+struct SlotLds {
+    uint64_t* keys;
+    uint16_t* heads;
+    float* stage;
+    float* carry;
+    int* lpre;
+    DQRM_INLINE explicit SlotLds(unsigned char* lds)
+        : keys(reinterpret_cast<uint64_t*>(lds)),
+          heads(reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8)),
+          stage(reinterpret_cast<float*>(lds + SLOT_KEYS * 10)),
+          carry(reinterpret_cast<float*>(lds + SLOT_KEYS * 10 + STAGE_FLOATS * 4)),
+          lpre(reinterpret_cast<int*>(lds + SLOT_KEYS * 10 + STAGE_FLOATS * 4 + CARRY_FLOATS * 4)) {}
+};
 
 DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
 DQRM_INLINE uint32_t key_lo(uint64_t k) { return (uint32_t)k; }
@@ -565,22 +586,9 @@ DQRM_INLINE void slot_rows(int64_t nrows, int s, int64_t& r0, int64_t& r1) {
     r1 = b1 * BLK < nrows ? b1 * BLK : nrows;
 }
 
-// sort the n keys already in LDS, then compact segment heads: heads[u] = first key of the
-// u-th distinct row. Returns U. (heads are u16: n <= SLOT_KEYS <= 65536)
-DQRM_INLINE int sort_and_heads(uint64_t* keys, uint16_t* heads, int n, int* s_wsum) {
-    const int np2 = next_pow2(n < 2 ? 2 : n);
-    for (int i = n + threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_lds(keys, np2);
-    // compact heads with a block-wide scan over chunks of CH keys per thread
-    constexpr int CH = SLOT_KEYS / TWG;
-    const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
-    const int i0 = tid * CH;
-    int cnt = 0;
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
-    }
+// exclusive block-wide prefix of one int per thread; *total = the sum (s_wsum: TWG/WAVE+1)
+DQRM_INLINE int block_excl_scan(int cnt, int* s_wsum, int* total) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
     int v = cnt;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -589,19 +597,159 @@ DQRM_INLINE int sort_and_heads(uint64_t* keys, uint16_t* heads, int n, int* s_ws
     }
     if (lane == WAVE - 1) s_wsum[w] = v;
     __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
         int run = 0;
         for (int k = 0; k < TWG / WAVE; ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
         s_wsum[TWG / WAVE] = run;
     }
     __syncthreads();
-    int u = s_wsum[w] + v - cnt;
+    *total = s_wsum[TWG / WAVE];
+    return s_wsum[w] + v - cnt;
+}
+
+// Sorting a slot's keys. The keys arrive in ascending tag order (lookup position, or
+// (rank, entry)), so what is needed is a STABLE sort by row; three strategies:
+//  * n <= 512: one wave, bitonic in registers (KPL keys per lane, no block barriers);
+//  * narrow row span (<= 2^RADIX_MAX_BITS rows, tiny/mid tables): stable LSD radix sort,
+//    4-bit digits, each thread owning a contiguous run of keys;
+//  * otherwise: bitonic over LDS on the full 64-bit key (row, tag).
+template <int KPL>
+DQRM_INLINE void wave_sort_regs(uint64_t* keys, int n) {
+    const int lane = threadIdx.x % WAVE;
+    uint64_t x[KPL];
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+        const int i = lane * KPL + r;
+        x[r] = i < n ? keys[i] : ~0ull;
+    }
+    constexpr int NP = WAVE * KPL;
+#pragma unroll
+    for (int k = 2; k <= NP; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < KPL) {  // partner in the same lane
+#pragma unroll
+                for (int r = 0; r < KPL; ++r) {
+                    const int p = r ^ j;
+                    if (p > r) {
+                        const bool up = ((lane * KPL + r) & k) == 0;
+                        const uint64_t a = x[r], b = x[p];
+                        if ((a > b) == up) { x[r] = b; x[p] = a; }
+                    }
+                }
+            } else {        // partner lane = lane ^ (j / KPL)
+#pragma unroll
+                for (int r = 0; r < KPL; ++r) {
+                    const int i = lane * KPL + r;
+                    const bool take_min = ((i & j) == 0) == ((i & k) == 0);
+                    const uint32_t lo = __shfl_xor((uint32_t)x[r], j / KPL, WAVE);
+                    const uint32_t hi = __shfl_xor((uint32_t)(x[r] >> 32), j / KPL, WAVE);
+                    const uint64_t y = ((uint64_t)hi << 32) | lo;
+                    x[r] = take_min ? (x[r] < y ? x[r] : y) : (x[r] < y ? y : x[r]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < KPL; ++r) {
+        const int i = lane * KPL + r;
+        if (i < n) keys[i] = x[r];
+    }
+}
+
+constexpr int RADIX_MAX_BITS = 12;
+
+DQRM_INLINE void radix_sort_rows(uint64_t* keys, uint64_t* tmp, uint16_t* cnt, int n, uint32_t r0, int bits,
+                                 int* s_wsum) {
+    constexpr int NB = 16;
+    const int tid = threadIdx.x;
+    const int CH = (n + TWG - 1) / TWG;
+    const int i0 = min(tid * CH, n), i1 = min(i0 + CH, n);
+    uint64_t* src = keys;
+    uint64_t* dst = tmp;
+    for (int sh = 0; sh < bits; sh += 4) {
+        uint32_t c[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) c[b] = 0;
+        for (int i = i0; i < i1; ++i) {
+            const uint32_t d = ((key_row(src[i]) - r0) >> sh) & (NB - 1);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) c[b] += (d == (uint32_t)b);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) cnt[b * TWG + tid] = (uint16_t)c[b];
+        __syncthreads();
+        int loc[NB], sum = 0;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) { loc[k] = cnt[tid * NB + k]; sum += loc[k]; }
+        int total;
+        int ex = block_excl_scan(sum, s_wsum, &total);  // digit-major, thread-minor order
+#pragma unroll
+        for (int k = 0; k < NB; ++k) { cnt[tid * NB + k] = (uint16_t)ex; ex += loc[k]; }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB; ++b) c[b] = cnt[b * TWG + tid];
+        for (int i = i0; i < i1; ++i) {
+            const uint64_t kk = src[i];
+            const uint32_t d = ((key_row(kk) - r0) >> sh) & (NB - 1);
+            uint32_t p = 0;
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+                if (d == (uint32_t)b) { p = c[b]; c[b] = p + 1; }
+            dst[p] = kk;
+        }
+        __syncthreads();
+        uint64_t* t = src; src = dst; dst = t;
+    }
+    if (src != keys) {
+        for (int i = tid; i < n; i += TWG) keys[i] = src[i];
+        __syncthreads();
+    }
+}
+
+// sort the slot's n keys (rows in [r0, r0 + span)), then compact segment heads:
+// heads[u] = first key of the u-th distinct row. Returns U. (heads are u16: n <= 65536)
+DQRM_INLINE int sort_and_heads(const SlotLds& L, int n, uint32_t r0, uint32_t span, int* s_wsum) {
+    uint64_t* keys = L.keys;
+    uint16_t* heads = L.heads;
+    const int bits = span <= 1 ? 0 : 32 - __builtin_clz(span - 1);
+    if (n <= 512) {
+        if (threadIdx.x < WAVE && n > 1) {
+            if (n <= 64) wave_sort_regs<1>(keys, n);
+            else if (n <= 128) wave_sort_regs<2>(keys, n);
+            else if (n <= 256) wave_sort_regs<4>(keys, n);
+            else wave_sort_regs<8>(keys, n);
+        }
+        __syncthreads();
+    } else if (bits <= RADIX_MAX_BITS) {
+        // scratch: the heads + stage regions are free until the heads are compacted
+        // (tmp keys: 8*SLOT_KEYS bytes from the heads; digit counters: the 32 KiB after them)
+        static_assert(SLOT_KEYS * 16 + 16 * TWG * 2 <= SLOT_KEYS * 10 + STAGE_FLOATS * 4, "radix scratch");
+        radix_sort_rows(keys, reinterpret_cast<uint64_t*>(L.heads),
+                        reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(keys) + SLOT_KEYS * 16), n, r0,
+                        bits, s_wsum);
+    } else {
+        const int np2 = next_pow2(n);
+        for (int i = n + threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
+        __syncthreads();
+        bitonic_sort_lds(keys, np2);
+    }
+    // compact heads with a block-wide scan over chunks of CH keys per thread
+    constexpr int CH = SLOT_KEYS / TWG;
+    const int i0 = threadIdx.x * CH;
+    int cnt = 0;
+    for (int c = 0; c < CH; ++c) {
+        const int i = i0 + c;
+        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
+    }
+    int U;
+    int u = block_excl_scan(cnt, s_wsum, &U);
     for (int c = 0; c < CH; ++c) {
         const int i = i0 + c;
         if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) heads[u++] = (uint16_t)i;
     }
     __syncthreads();
-    return s_wsum[TWG / WAVE];
+    return U;
 }
 
 DQRM_INLINE int seg_end(const uint16_t* heads, int U, int n, int u) {
@@ -619,7 +767,6 @@ DQRM_INLINE int seg_end(const uint16_t* heads, int U, int n, int u) {
 // entries per chunk (the next chunk prefetched) and combines them in order via shuffles.
 // Masked entries re-load the head's own entry, so they never address out of bounds.
 // ------------------------------------------------------------------------------------
-constexpr int LONG_SEG = 32;
 constexpr int OP_FMA = 0;
 constexpr int OP_SUM = 1;
 
@@ -656,25 +803,16 @@ DQRM_INLINE float4 seg_reduce_group(const uint64_t* keys, int i, int len, float4
     return acc;
 }
 
-// Long segments: lane-owned dimensions. Lane l owns dims l, l+64, ... of the row; the wave
-// stages CH = TILE_FLOATS/D entries at a time in its LDS tile (8 float4 loads per lane,
-// coalesced, the next chunk in flight while the current one is reduced) and every lane
-// walks the tile's entries in order for its own dims: no shuffles, no per-entry branches.
+// Long segments (> LONG_SEG entries: tiny hot tables, Zipf-hot rows) are combined by
+// "dim-lane" groups of GD = min(D, 64) lanes, each lane owning NDL = D/GD dimensions, so the
+// strictly ordered chain is one add (or fma) per entry per lane. Their entries are fed
+// block-cooperatively (staged_long_segments below).
 template <int LPR>
-struct LaneRow {
+struct DimLane {
     static constexpr int D = LPR * 4;
-    static constexpr int NDL = (D + WAVE - 1) / WAVE;
-    float v[NDL];
+    static constexpr int GD = D < WAVE ? D : WAVE;
+    static constexpr int NDL = D / GD;
 };
-
-// Order one wave's LDS writes before its own later LDS reads (and vice versa). A wave's
-// DS instructions execute in order, so only the compiler must be stopped from moving
-// them; no s_waitcnt on the vector-memory counter is wanted here (it would drain the
-// prefetched global loads).
-DQRM_INLINE void wave_lds_sync() {
-    __builtin_amdgcn_wave_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
 
 template <int OP>
 DQRM_INLINE float combine1(float acc, float v, bool first, float nlr) {
@@ -682,101 +820,34 @@ DQRM_INLINE float combine1(float acc, float v, bool first, float nlr) {
     return first ? v : acc + v;
 }
 
-template <int LPR, int OP, class Src>
-DQRM_INLINE LaneRow<LPR> seg_reduce_tile(const uint64_t* keys, int i, int len, LaneRow<LPR> acc,
-                                         const Src& src, float nlr, float* tile) {
-    constexpr int D = LPR * 4;
-    constexpr int CH = TILE_FLOATS / D;             // entries per chunk
-    constexpr int F4 = TILE_FLOATS / 4 / WAVE;      // float4 loads per lane per chunk (8)
-    constexpr int NDL = LaneRow<LPR>::NDL;
-    const int lane = threadIdx.x % WAVE;
-    const uint32_t head_lo = key_lo(keys[i]);
-    float4 buf[F4];
-    auto load_chunk = [&](int j0) {
-#pragma unroll
-        for (int f = 0; f < F4; ++f) {
-            const int flat = f * WAVE + lane;        // float4 index in the tile = e * LPR + q
-            const int e = flat / LPR, q = flat % LPR;
-            const int jj = j0 + e;
-            buf[f] = src.load(jj < len ? key_lo(keys[i + jj]) : head_lo, q);
-        }
-    };
-    load_chunk(0);
-    bool first = true;
-    for (int j = 0; j < len; j += CH) {
-        wave_lds_sync();  // previous chunk fully read before it is overwritten
-#pragma unroll
-        for (int f = 0; f < F4; ++f) reinterpret_cast<float4*>(tile)[f * WAVE + lane] = buf[f];
-        wave_lds_sync();
-        if (j + CH < len) load_chunk(j + CH);      // wave-uniform; overlaps the walk below
-        const int cnt = len - j < CH ? len - j : CH;
-        for (int e = 0; e < cnt; e += 8) {
-#pragma unroll
-            for (int d = 0; d < NDL; ++d) {
-                const int dim = lane + WAVE * d;
-                if (dim >= D) continue;
-                float v[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = tile[((e + k) % CH) * D + dim];  // 8 reads in flight
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (e + k < cnt) acc.v[d] = combine1<OP>(acc.v[d], v[k], first && k == 0 && e == 0, nlr);
-            }
-            first = false;
-        }
-    }
-    wave_lds_sync();
-    return acc;
-}
-
 template <int LPR>
-DQRM_INLINE LaneRow<LPR> load_lane_row(const float* row) {
-    LaneRow<LPR> r;
-    const int lane = threadIdx.x % WAVE;
-#pragma unroll
-    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) {
-        const int dim = lane + WAVE * d;
-        r.v[d] = dim < LPR * 4 ? row[dim] : 0.0f;
-    }
-    return r;
-}
-
-template <int LPR>
-DQRM_INLINE void store_lane_row(float* row, const LaneRow<LPR>& r) {
-    const int lane = threadIdx.x % WAVE;
-#pragma unroll
-    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) {
-        const int dim = lane + WAVE * d;
-        if (dim < LPR * 4) row[dim] = r.v[d];
-    }
-}
-
-template <int LPR>
-DQRM_INLINE float lane_row_absmax(const LaneRow<LPR>& r) {
+DQRM_INLINE float dl_absmax(const float (&v)[DimLane<LPR>::NDL]) {
     float m = 0.0f;
 #pragma unroll
-    for (int d = 0; d < LaneRow<LPR>::NDL; ++d) m = fmaxf(m, fabsf(r.v[d]));
-    return wave_max(m);
+    for (int d = 0; d < DimLane<LPR>::NDL; ++d) m = fmaxf(m, fabsf(v[d]));
+    return group_max<DimLane<LPR>::GD>(m);
 }
 
-// repack a lane-owned row: stage it in the wave's tile, lanes 0..LPR-1 pack float4 slices
+// repack a dim-lane row: even lanes combine their nibble with the odd neighbour's
 template <int LPR>
-DQRM_INLINE void pack_lane_row(const LaneRow<LPR>& r, float* tile, uint8_t* packed, int64_t grow, float rcp) {
-    const int lane = threadIdx.x % WAVE;
-    wave_lds_sync();
-    store_lane_row<LPR>(tile, r);
-    wave_lds_sync();
-    if (lane < LPR) pack_row_int4<LPR>(reinterpret_cast<const float4*>(tile)[lane], packed, grow, lane, rcp);
-    wave_lds_sync();
+DQRM_INLINE void dl_pack_int4(const float (&v)[DimLane<LPR>::NDL], uint8_t* packed, int64_t grow, int lig,
+                              float rcp) {
+    using DL = DimLane<LPR>;
+#pragma unroll
+    for (int d = 0; d < DL::NDL; ++d) {
+        const int q = (int)fake_quant(v[d], rcp, -8.0f, 7.0f) + 8;
+        const int qn = __shfl_xor(q, 1, WAVE);
+        const int dim = lig + DL::GD * d;
+        if ((dim & 1) == 0) packed[grow * (DL::D / 2) + dim / 2] = (uint8_t)(q | (qn << 4));
+    }
 }
 
-// Visit every segment once: short ones by lane groups (strided over heads) through
-// fg(u, i, len, sub); long ones by whole waves through fw(u, i, len) (all 64 lanes).
-constexpr int LONG_SEGS_MAX = SLOT_KEYS / (LONG_SEG + 1) + 1;
+// Visit every short segment (<= LONG_SEG entries) once by float4 lane groups (LPR lanes,
+// strided over heads) through fg(u, i, len, sub), and compact the long ones' indices u
+// (ascending) into s_long. Returns their number.
 
-template <int LPR, class FG, class FW>
-DQRM_INLINE void for_each_segment(const uint16_t* heads, int U, int n, uint16_t* s_long, int* s_nlong,
-                                  FG&& fg, FW&& fw) {
+template <int LPR, class FG>
+DQRM_INLINE int short_segments(const uint16_t* heads, int U, int n, uint16_t* s_long, int* s_wsum, FG&& fg) {
     const int sub = threadIdx.x % LPR;
     const int grp = threadIdx.x / LPR;
     const int ngrp = blockDim.x / LPR;
@@ -786,26 +857,144 @@ DQRM_INLINE void for_each_segment(const uint16_t* heads, int U, int n, uint16_t*
         if (len > LONG_SEG) continue;
         fg(u, i, len, sub);
     }
-    // long segments: compact their head ordinals, then deal them round-robin to the waves
-    // (a segment > LONG_SEG entries long means at most n / (LONG_SEG+1) <= LONG_SEGS_MAX of them)
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    if (threadIdx.x == 0) *s_nlong = 0;
-    __syncthreads();
-    for (int base = w * WAVE; base < U; base += nw * WAVE) {
-        const int u = base + lane;
-        const bool lg = u < U && (seg_end(heads, U, n, u) - (int)heads[u]) > LONG_SEG;
-        const uint64_t msk = __ballot(lg);
-        int off = 0;
-        if (lane == 0 && msk) off = atomicAdd(s_nlong, __popcll(msk));
-        off = __shfl(off, 0, WAVE);
-        if (lg) s_long[off + __popcll(msk & ((1ull << lane) - 1))] = (uint16_t)u;
+    // ordered compaction: thread tid owns heads [tid*PER, tid*PER + PER)
+    constexpr int PER = SLOT_KEYS / TWG;
+    const int u0 = threadIdx.x * PER;
+    int cnt = 0;
+    for (int c = 0; c < PER; ++c) {
+        const int u = u0 + c;
+        cnt += (u < U && seg_end(heads, U, n, u) - (int)heads[u] > LONG_SEG);
+    }
+    int nlong;
+    int o = block_excl_scan(cnt, s_wsum, &nlong);
+    for (int c = 0; c < PER && cnt; ++c) {
+        const int u = u0 + c;
+        if (u < U && seg_end(heads, U, n, u) - (int)heads[u] > LONG_SEG) { s_long[o++] = (uint16_t)u; --cnt; }
     }
     __syncthreads();
-    const int nlong = *s_nlong;
-    for (int k = w; k < nlong; k += nw) {
-        const int uu = s_long[k];
-        const int i = heads[uu];
-        fw(uu, i, seg_end(heads, U, n, uu) - i);
+    return nlong;
+}
+
+// Long segments, block-cooperatively. Their entries, concatenated in key order, stream
+// through an LDS stage CE = STAGE_FLOATS / D entries at a time: all TWG threads fetch the
+// rows (STAGE_F4 float4 per thread; the next chunk's fetch is in flight while the current
+// chunk is combined), then every piece (segment part) of the chunk is combined in entry
+// order by one dim-lane group straight from LDS. A segment crossing a chunk boundary
+// hands its partial row on through a carry row (two, alternating by chunk parity).
+//   fbegin(i, lig, acc)      initial value of a segment (head key index i)
+//   fend(u, i, lig, acc)     the finished row
+template <int LPR, int OP, class Src, class FB, class FE>
+DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint16_t* s_long, int nlong,
+                                      int* s_wsum, const Src& src, float nlr, FB&& fbegin, FE&& fend) {
+    if (nlong == 0) return;  // uniform
+    constexpr int D = LPR * 4;
+    using DL = DimLane<LPR>;
+    constexpr int GD = DL::GD, NDL = DL::NDL;
+    constexpr int CE = STAGE_FLOATS / D;          // entries per chunk
+    constexpr int EPF = TWG / LPR;                // entries between a thread's fetches
+    const uint64_t* keys = L.keys;
+    const uint16_t* heads = L.heads;
+    int* lpre = L.lpre;
+    // exclusive prefix of the long segments' lengths
+    {
+        constexpr int PER = (LONG_SEGS_MAX + TWG - 1) / TWG;
+        int len[PER], cnt = 0;
+#pragma unroll
+        for (int c = 0; c < PER; ++c) {
+            const int k = threadIdx.x * PER + c;
+            len[c] = 0;
+            if (k < nlong) { const int u = s_long[k]; len[c] = seg_end(heads, U, n, u) - (int)heads[u]; }
+            cnt += len[c];
+        }
+        int total;
+        int run = block_excl_scan(cnt, s_wsum, &total);
+#pragma unroll
+        for (int c = 0; c < PER; ++c) {
+            const int k = threadIdx.x * PER + c;
+            if (k < nlong) lpre[k] = run;
+            run += len[c];
+        }
+        if (threadIdx.x == 0) lpre[nlong] = total;
+        __syncthreads();
+    }
+    const int E = lpre[nlong];
+    // largest k in [lo, hi] with lpre[k] <= e
+    auto seg_of = [&](int e, int lo, int hi) {
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lpre[mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    };
+    const int sub = threadIdx.x % LPR;
+    typename Src::Raw raw[STAGE_F4];
+    auto fetch = [&](int c0) {
+        const int e0 = c0 + threadIdx.x / LPR;
+        int k = e0 < E ? seg_of(e0, 0, nlong - 1) : 0;
+#pragma unroll
+        for (int f = 0; f < STAGE_F4; ++f) {
+            const int e = e0 + f * EPF;
+            if (e < E) {
+                if (f) k = seg_of(e, k, min(nlong - 1, k + EPF / (LONG_SEG + 1) + 1));
+                const int ki = heads[s_long[k]] + (e - lpre[k]);
+                raw[f] = src.fetch(key_lo(keys[ki]), sub);
+            }
+        }
+    };
+    const int dg = threadIdx.x / GD, ndg = TWG / GD, lig = threadIdx.x % GD;
+    fetch(0);
+    int par = 0;
+    for (int c0 = 0; c0 < E; c0 += CE, par ^= 1) {
+#pragma unroll
+        for (int f = 0; f < STAGE_F4; ++f) {
+            const int q = threadIdx.x + f * TWG;  // float4 slot = entry * LPR + sub
+            if (c0 + q / LPR < E) reinterpret_cast<float4*>(L.stage)[q] = src.finish(raw[f]);
+        }
+        __syncthreads();
+        if (c0 + CE < E) fetch(c0 + CE);
+        const int ce = min(CE, E - c0);
+        const int kf = seg_of(c0, 0, nlong - 1), kl = seg_of(c0 + ce - 1, kf, nlong - 1);
+        for (int k = kf + dg; k <= kl; k += ndg) {
+            const int sb = lpre[k], se = lpre[k + 1];
+            const int a0 = max(sb, c0), a1 = min(se, c0 + ce);
+            const int u = s_long[k], i = heads[u];
+            float acc[NDL];
+            bool first = sb >= c0;
+            if (first) {
+                fbegin(i, lig, acc);
+            } else {
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) acc[d] = L.carry[(par ^ 1) * 256 + lig + GD * d];
+            }
+            const float* sp = L.stage + (a0 - c0) * D + lig;
+            const int len = a1 - a0;
+            int j = 0;
+            for (; j + 8 <= len; j += 8) {
+                float v[8][NDL];
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) v[c][d] = sp[(j + c) * D + GD * d];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) acc[d] = combine1<OP>(acc[d], v[c][d], first, nlr);
+                    first = false;
+                }
+            }
+            for (; j < len; ++j) {
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) acc[d] = combine1<OP>(acc[d], sp[j * D + GD * d], first, nlr);
+                first = false;
+            }
+            if (se <= c0 + ce) {
+                fend(u, i, lig, acc);
+            } else {
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) L.carry[par * 256 + lig + GD * d] = acc[d];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -910,39 +1099,64 @@ __global__ void k_table_finalize(const float* __restrict__ blkmax, float* __rest
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
-// deterministic placement (count, block-scan, write); returns the key count, or -1
-// (uniform) when the slot overflows SLOT_KEYS.
+// deterministic placement (count, block-scan, write; keys end up in bag order); returns
+// the key count, or -1 (uniform) when the slot overflows SLOT_KEYS. Each thread owns a
+// contiguous run of bags, processed GB at a time with every offset / first-index load of
+// the batch in flight together.
+template <class Visit>
+DQRM_INLINE void visit_slot_lookups(const int64_t* off, const int64_t* idx, int64_t B, int64_t L,
+                                    int64_t nrows, int64_t b0, int64_t b1, bool report, uint32_t* err,
+                                    Visit&& visit) {
+    constexpr int GB = 8;
+    for (int64_t bs = b0; bs < b1; bs += GB) {
+        int64_t o[GB + 1];
+#pragma unroll
+        for (int k = 0; k <= GB; ++k) {  // GB+1 offsets in flight
+            const int64_t b = bs + k;
+            o[k] = b < B ? off[b] : L;
+        }
+        int64_t beg[GB], end[GB], first[GB];
+#pragma unroll
+        for (int k = 0; k < GB; ++k) {  // validate, then the first index of every bag in flight
+            const int64_t b = bs + k;
+            int64_t s0 = o[k], s1 = o[k + 1];
+            if (b < b1 && (s0 < 0 || s1 > L || s1 < s0)) {
+                if (report) flag_error(err, DQRM_ERRF_OFFSET);
+                s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+                s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+            }
+            beg[k] = s0;
+            end[k] = b < b1 ? s1 : s0;
+            first[k] = end[k] > s0 ? idx[s0] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < GB; ++k) {
+            const int64_t b = bs + k;
+            for (int64_t p = beg[k]; p < end[k]; ++p) {
+                const int64_t r = p == beg[k] ? first[k] : idx[p];
+                if (r < 0 || r >= nrows) {
+                    if (report) flag_error(err, DQRM_ERRF_INDEX);
+                    continue;
+                }
+                visit(r, b);
+            }
+        }
+    }
+}
+
 DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* idx, const int64_t* off,
                                    const int64_t* idx_base, int64_t B, int t, int64_t nrows,
                                    int64_t r0, int64_t r1, bool report, uint32_t* err) {
     const int64_t ib = idx_base[t];
     const int64_t L = idx_base[t + 1] - ib;
+    const int64_t* __restrict__ toff = off + (int64_t)t * B;
+    const int64_t* __restrict__ tidx = idx + ib;
     const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
-    // each thread owns a contiguous run of bags
     const int64_t per = (B + blockDim.x - 1) / blockDim.x;
     const int64_t b0 = (int64_t)tid * per, b1 = b0 + per < B ? b0 + per : B;
-    auto bag_range = [&](int64_t b, int64_t& s0, int64_t& s1) {
-        s0 = off[(int64_t)t * B + b];
-        s1 = (b + 1 < B) ? off[(int64_t)t * B + b + 1] : L;
-        if (s0 < 0 || s1 > L || s1 < s0) {
-            if (report) flag_error(err, DQRM_ERRF_OFFSET);
-            s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
-            s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
-        }
-    };
     int cnt = 0;
-    for (int64_t b = b0; b < b1; ++b) {
-        int64_t s0, s1;
-        bag_range(b, s0, s1);
-        for (int64_t p = s0; p < s1; ++p) {
-            const int64_t r = idx[ib + p];
-            if (r < 0 || r >= nrows) {
-                if (report) flag_error(err, DQRM_ERRF_INDEX);
-                continue;
-            }
-            cnt += (r >= r0 && r < r1);
-        }
-    }
+    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err,
+                       [&](int64_t r, int64_t) { cnt += (r >= r0 && r < r1); });
     int v = cnt;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -963,14 +1177,10 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
         return -1;
     }
     int pos = s_wsum[w] + v - cnt;
-    for (int64_t b = b0; b < b1 && cnt > 0; ++b) {
-        int64_t s0, s1;
-        bag_range(b, s0, s1);
-        for (int64_t p = s0; p < s1; ++p) {
-            const int64_t r = idx[ib + p];
+    if (cnt > 0)
+        visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, false, err, [&](int64_t r, int64_t b) {
             if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
-        }
-    }
+        });
     __syncthreads();
     return n;
 }
@@ -1010,25 +1220,29 @@ struct DySource {
     int64_t st_b;
     float s;
     int ste;
-    DQRM_INLINE float4 load(uint32_t bag, int sub) const {
-        float4 g = reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[sub];
+    using Raw = float4;
+    DQRM_INLINE float4 fetch(uint32_t bag, int sub) const {
+        return reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[sub];
+    }
+    DQRM_INLINE float4 finish(float4 g) const {
         if (ste) {
             g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
         }
         return g;
     }
+    DQRM_INLINE float4 load(uint32_t bag, int sub) const { return finish(fetch(bag, sub)); }
 };
 
 // MODE 0: fused SGD (single GPU);  MODE 1: coalesce + per-slot max |grad| (DP)
 template <int LPR, int MODE>
 __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
-    uint16_t* heads = reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8);
+    const SlotLds sl(lds);
+    uint64_t* keys = sl.keys;
+    uint16_t* heads = sl.heads;
     __shared__ int s_wsum[TWG / WAVE + 8];   // 64 B: static LDS stays a multiple of 16
     __shared__ unsigned int s_misc[4];
     __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
-    int* s_nlong = reinterpret_cast<int*>(&s_misc[2]);
 
     const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
     const int T = a.T;
@@ -1050,7 +1264,7 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
 #if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 1
     if (n >= 0) return;  // diagnostic build: gather only
 #endif
-    const int U = sort_and_heads(keys, heads, n, s_wsum);
+    const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum);
 #if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 2
     if (U >= 0) return;  // diagnostic build: gather + sort + heads
 #endif
@@ -1059,7 +1273,6 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
     const int64_t cap = MODE == 1 ? a.ws_cap_base[slot + 1] - a.ws_cap_base[slot] : 0;
     float local_absmax = 0.0f;
-    float* tile = reinterpret_cast<float*>(lds + SLOT_KEYS * 10) + (threadIdx.x / WAVE) * TILE_FLOATS;
 
     auto group_fn = [&](int u, int i, int len, int sub) {
         const uint32_t row = key_row(keys[i]);
@@ -1086,33 +1299,38 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
             local_absmax = fmaxf(local_absmax, abs_max4(acc));
         }
     };
-    auto wave_fn = [&](int u, int i, int len) {
+    using DL = DimLane<LPR>;
+    auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
+        const int64_t grow = rb + key_row(keys[i]);
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE == 0 ? a.W[grow * D + lig + DL::GD * d] : 0.0f;
+    };
+    auto fend = [&](int u, int i, int lig, float (&v)[DL::NDL]) {
         const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
-        const int lane = threadIdx.x % WAVE;
         if (MODE == 0) {
-            LaneRow<LPR> w = load_lane_row<LPR>(a.W + grow * D);
             const float old_rm = a.rowmax[grow];
-            w = seg_reduce_tile<LPR, OP_FMA>(keys, i, len, w, src, a.nlr, tile);
-            const float rm = lane_row_absmax<LPR>(w);
-            store_lane_row<LPR>(a.W + grow * D, w);
-            if (a.repack) pack_lane_row<LPR>(w, tile, a.packed, grow, r_pack);
-            if (lane == 0) {
+            const float rm = dl_absmax<LPR>(v);
+#pragma unroll
+            for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + lig + DL::GD * d] = v[d];
+            if (a.repack) dl_pack_int4<LPR>(v, a.packed, grow, lig, r_pack);
+            if (lig == 0) {
                 a.rowmax[grow] = rm;
                 keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
             }
         } else {
-            LaneRow<LPR> acc{};
-            acc = seg_reduce_tile<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, tile);
             if (u < cap) {
                 const int64_t e = a.ws_cap_base[slot] + u;
-                store_lane_row<LPR>(a.ws_vals + e * D, acc);
-                if (lane == 0) a.ws_rows[e] = (int32_t)row;
+#pragma unroll
+                for (int d = 0; d < DL::NDL; ++d) a.ws_vals[e * D + lig + DL::GD * d] = v[d];
+                if (lig == 0) a.ws_rows[e] = (int32_t)row;
             }
-            local_absmax = fmaxf(local_absmax, lane_row_absmax<LPR>(acc));
+            local_absmax = fmaxf(local_absmax, dl_absmax<LPR>(v));
         }
     };
-    for_each_segment<LPR>(heads, U, n, s_long, s_nlong, group_fn, wave_fn);
+    const int nlong = short_segments<LPR>(heads, U, n, s_long, s_wsum, group_fn);
+    staged_long_segments<LPR, MODE == 0 ? OP_FMA : OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, a.nlr, fbegin,
+                                                           fend);
     if (MODE == 1) {
         local_absmax = wave_max(local_absmax);
         if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
@@ -1257,37 +1475,48 @@ struct PayloadSource {
     int64_t payload_bytes;
     PayloadLayout pl;
     int64_t cap_base_t;
-    DQRM_INLINE float4 load(uint32_t lo, int sub) const {
+    using Raw = uint4;
+    DQRM_INLINE uint4 fetch(uint32_t lo, int sub) const {
         constexpr int D = LPR * 4;
-        const unsigned char* p = payloads + (int64_t)(lo >> 24) * payload_bytes;
+        const unsigned char* p = payloads + (int64_t)(lo >> 24) * payload_bytes + pl.vals_off;
         const int64_t e = cap_base_t + (int64_t)(lo & 0xFFFFFF);
+        uint4 x = make_uint4(0u, 0u, 0u, 0u);
+        if (pl.elem == 1) {
+            x.x = reinterpret_cast<const uint32_t*>(p + e * D)[sub];
+        } else if (pl.elem == 2) {
+            const uint2 y = reinterpret_cast<const uint2*>(p + e * D * 2)[sub];
+            x.x = y.x; x.y = y.y;
+        } else {
+            x = reinterpret_cast<const uint4*>(p + e * D * 4)[sub];
+        }
+        return x;
+    }
+    DQRM_INLINE float4 finish(uint4 x) const {
         float4 v;
         if (pl.elem == 1) {
-            uint32_t x = reinterpret_cast<const uint32_t*>(p + pl.vals_off + e * D)[sub];
-            v.x = (float)(int8_t)(x & 0xFF); v.y = (float)(int8_t)((x >> 8) & 0xFF);
-            v.z = (float)(int8_t)((x >> 16) & 0xFF); v.w = (float)(int8_t)(x >> 24);
+            v.x = (float)(int8_t)(x.x & 0xFF); v.y = (float)(int8_t)((x.x >> 8) & 0xFF);
+            v.z = (float)(int8_t)((x.x >> 16) & 0xFF); v.w = (float)(int8_t)(x.x >> 24);
         } else if (pl.elem == 2) {
-            uint2 x = reinterpret_cast<const uint2*>(p + pl.vals_off + e * D * 2)[sub];
             v.x = (float)(int16_t)(x.x & 0xFFFF); v.y = (float)(int16_t)(x.x >> 16);
             v.z = (float)(int16_t)(x.y & 0xFFFF); v.w = (float)(int16_t)(x.y >> 16);
         } else {
-            v = reinterpret_cast<const float4*>(p + pl.vals_off + e * D * 4)[sub];
+            v = __builtin_bit_cast(float4, x);
         }
         return v;
     }
+    DQRM_INLINE float4 load(uint32_t lo, int sub) const { return finish(fetch(lo, sub)); }
 };
 
 template <int LPR>
 __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
-    uint16_t* heads = reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8);
+    const SlotLds sl(lds);
+    uint64_t* keys = sl.keys;
+    uint16_t* heads = sl.heads;
     __shared__ int s_wsum[TWG / WAVE + 8];
     __shared__ int s_e0[68];
     __shared__ int s_start[68];
     __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
-    __shared__ int s_nlong_arr[4];
-    int* s_nlong = &s_nlong_arr[0];
 
     const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
     const int T = a.T;
@@ -1341,7 +1570,7 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     }
     __syncthreads();
     const int n = M;
-    const int U = sort_and_heads(keys, heads, n, s_wsum);
+    const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum);
 
     const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
     const float inv_n = (float)(1.0 / (double)a.N);
@@ -1349,7 +1578,6 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
     PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, a.cap_base[t]};
 
-    float* tile = reinterpret_cast<float*>(lds + SLOT_KEYS * 10) + (threadIdx.x / WAVE) * TILE_FLOATS;
     const int mode = a.mode;
     const float nlr = a.nlr;
     // dequantize + SGD, one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
@@ -1379,26 +1607,28 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
             keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
         }
     };
-    auto wave_fn = [&](int u, int i, int len) {
-        (void)u;
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        const int lane = threadIdx.x % WAVE;
-        LaneRow<LPR> w = load_lane_row<LPR>(a.W + grow * D);
-        const float old_rm = a.rowmax[grow];
-        LaneRow<LPR> acc{};
-        acc = seg_reduce_tile<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, tile);
+    using DL = DimLane<LPR>;
+    auto fbegin = [&](int, int, float (&acc)[DL::NDL]) {
 #pragma unroll
-        for (int d = 0; d < LaneRow<LPR>::NDL; ++d) w.v[d] = update(w.v[d], acc.v[d]);
-        const float rm = lane_row_absmax<LPR>(w);
-        store_lane_row<LPR>(a.W + grow * D, w);
-        if (a.repack) pack_lane_row<LPR>(w, tile, a.packed, grow, r_pack);
-        if (lane == 0) {
+        for (int d = 0; d < DL::NDL; ++d) acc[d] = 0.0f;
+    };
+    auto fend = [&](int, int i, int lig, float (&acc)[DL::NDL]) {
+        const int64_t grow = rb + key_row(keys[i]);
+        float w[DL::NDL];
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) w[d] = update(a.W[grow * D + lig + DL::GD * d], acc[d]);
+        const float old_rm = a.rowmax[grow];
+        const float rm = dl_absmax<LPR>(w);
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + lig + DL::GD * d] = w[d];
+        if (a.repack) dl_pack_int4<LPR>(w, a.packed, grow, lig, r_pack);
+        if (lig == 0) {
             a.rowmax[grow] = rm;
             keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
         }
     };
-    for_each_segment<LPR>(heads, U, n, s_long, s_nlong, group_fn, wave_fn);
+    const int nlong = short_segments<LPR>(heads, U, n, s_long, s_wsum, group_fn);
+    staged_long_segments<LPR, OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, 0.0f, fbegin, fend);
     __syncthreads();
     maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
 }

@@ -310,3 +310,81 @@ def test_determinism_bitwise(dq):
             ts.backward_sgd(b, dy, lr=0.1)
         outs.append(ts.W.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+SORT_ROWS = [3, 62, 971, 5000, 300000]
+
+
+def _table_slots(ws, t):
+    """Concatenate table t's row-range slots of a coalesced workspace (host copies)."""
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+
+    ucount = ws.ucount.cpu().numpy()
+    rows_all, vals_all = ws.rows.cpu().numpy(), ws.vals.cpu().numpy()
+    rows, vals = [], []
+    for k in range(t * L.DQRM_TABLE_SPLIT, (t + 1) * L.DQRM_TABLE_SPLIT):
+        b = ws.slot_base[k]
+        rows.append(rows_all[b: b + ucount[k]])
+        vals.append(vals_all[b: b + ucount[k]])
+    return np.concatenate(rows), np.concatenate(vals)
+
+
+@pytest.mark.parametrize("D", [16, 64, 128])
+@pytest.mark.parametrize("dist", ["uniform", "zipf", "bags"])
+def test_slot_sort_and_segment_paths_bitexact(dq, D, dist):
+    """Every per-slot sort strategy (register wave sort for <= 512 keys, radix on narrow
+    row spans, LDS bitonic on crowded wide slots) and long segments that cross the LDS
+    stage's chunks, in both the fused-SGD and the coalesce kernels, against the oracle."""
+    rows = SORT_ROWS
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 21)
+    if dist == "bags":
+        idxs, offs = G.random_bags(rows, 1024, 22, num_indices_per_lookup=6)
+    else:
+        P = G.pooling_one(rows, 4096, 22, dist=dist)
+        idxs = [P[t] for t in range(T)]
+        offs = [np.arange(P.shape[1], dtype=np.int64) for _ in range(T)]
+    nb = len(offs[0])
+    dy = G.upstream_grad(T, nb, D, 23)
+    ts = make_set(dq, Ws)
+    b = to_batch(dq, idxs, offs)
+    ts.forward(b)
+    s = ts.scale.cpu().numpy()
+    ws = dq.CoalescedGrad.allocate(rows, b.max_lookups, D, "cuda")
+    ts.backward_coalesce(b, torch.from_numpy(dy).cuda(), ws)
+    for t in range(T):
+        r_o, v_o, err = O.emb_bwd_coalesce(rows[t], idxs[t], offs[t], dy[t], s[t])
+        assert err == 0
+        r_g, v_g = _table_slots(ws, t)
+        np.testing.assert_array_equal(r_g, r_o)
+        np.testing.assert_array_equal(v_g, v_o)
+    ts.backward_sgd(b, torch.from_numpy(dy).cuda(), lr=0.1)
+    assert ts.read_errors() == 0
+    for t in range(T):
+        Wo = Ws[t].copy()
+        O.emb_bwd_sgd(Wo, idxs[t], offs[t], dy[t], s[t], 0.1)
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Wo)
+    tmax_inc = ts.tmax.clone()
+    ts.refresh_absmax()
+    torch.testing.assert_close(tmax_inc, ts.tmax, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("grad_bits", [8, 32])
+def test_exchange_many_ranks_long_segments(dq, grad_bits):
+    """N=12 emulated ranks: a row present in every rank's payload is a 12-entry segment in
+    the apply kernel (the block-cooperative long-segment path); against oracle.dp_step."""
+    rows, D, B, N = [3, 50, 2000], 32, 256, 12
+    Ws = G.table_weights(rows, D, 31)
+    ts = make_set(dq, Ws)
+    Ps = [G.pooling_one(rows, B, 100 + r, dist="zipf") for r in range(N)]
+    dys = [G.upstream_grad(len(rows), B, D, 200 + r) for r in range(N)]
+    rank_batches = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+    ts.forward(rank_batches[0])
+    s_fwd = ts.scale.cpu().numpy()
+    _emulate_ranks(dq, ts, rank_batches, [torch.from_numpy(d).cuda() for d in dys], grad_bits, 0.1)
+    ar = np.arange(B, dtype=np.int64)
+    O.dp_step(Ws, [[(Ps[r][t], ar) for t in range(len(rows))] for r in range(N)],
+              [[dys[r][t] for t in range(len(rows))] for r in range(N)], s_fwd, 0.1, grad_bits=grad_bits)
+    assert ts.read_errors() == 0
+    for t in range(len(rows)):
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Ws[t])
