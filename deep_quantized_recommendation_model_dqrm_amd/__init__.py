@@ -10,6 +10,8 @@ from . import _lib
 from ._build import LIB_PATH, build
 from .tables import CoalescedGrad, EmbeddingTableSet, LookupBatch, default_caps, reference_scale
 from .comm import SparseGradExchange, get_my_slice, payload_bytes
+from . import quant_modules_not_quantize_grad, sgd_quantized_gradients, sgd_quantized_gradients_parallel_comm
+from .quant_modules_not_quantize_grad import QuantEmbeddingBagCollection, QuantEmbeddingBagTwo
 
 __all__ = [
     "LIB_PATH",
@@ -23,4 +25,9 @@ __all__ = [
     "SparseGradExchange",
     "get_my_slice",
     "payload_bytes",
+    "QuantEmbeddingBagTwo",
+    "QuantEmbeddingBagCollection",
+    "quant_modules_not_quantize_grad",
+    "sgd_quantized_gradients",
+    "sgd_quantized_gradients_parallel_comm",
 ]

@@ -95,6 +95,7 @@ class SparseGradExchange:
             raise ValueError("grad_bits must be 2..16 or 32")
         self.tables = tables
         self.grad_bits = grad_bits
+        self.max_lookups = int(max_lookups)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0

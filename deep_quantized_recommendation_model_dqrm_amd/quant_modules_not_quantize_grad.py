@@ -94,7 +94,8 @@ class _QuantEmbeddingBase(nn.Module):
         self.scale_period = int(scale_period)
         self.use_packed_int4 = bool(use_packed_int4)
         self._pending = None      # (batch, dy, ste, layout) for grad_mode == "dp"
-        self._exchange = None
+        self._exchange = None     # SparseGradExchange used by the DP hooks
+        self._ready = None        # grad bits of an exchanged, not yet applied update
         self._counters = None     # host mirror of (now_iteration, iteration_bound, iteration_nt)
 
     # ------------------------------------------------------------ scale refresh logic

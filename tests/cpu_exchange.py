@@ -1,0 +1,119 @@
+"""TEST INFRASTRUCTURE: a CPU implementation of the ExchangeKernels protocol built on the
+oracle, so that SparseGradExchange's host logic (buffer sizing, the two all-gathers, rank
+handling, the wire layout) runs under a multi-process Gloo group on machines without a
+GPU. Never used by the product (which only has HipExchangeKernels)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import oracle as O
+from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+
+f32 = np.float32
+SPLIT = L.DQRM_TABLE_SPLIT
+BLK = L.DQRM_BLOCK_ROWS
+
+
+def slot_rows(n: int, s: int) -> tuple[int, int]:
+    """Row range of slot s of an n-row table (block-aligned split, include/dqrm.h)."""
+    nblk = (n + BLK - 1) // BLK
+    b0, b1 = nblk * s // SPLIT, nblk * (s + 1) // SPLIT
+    return b0 * BLK, min(b1 * BLK, n)
+
+
+def a16(x: int) -> int:
+    return (x + 15) & ~15
+
+
+class HostTables:
+    """The attributes SparseGradExchange reads from a table set, plus host weights."""
+
+    def __init__(self, Ws, device="cpu"):
+        self.Ws = [w.copy() for w in Ws]
+        self.T = len(Ws)
+        self.D = Ws[0].shape[1]
+        self.num_rows = [w.shape[0] for w in Ws]
+        self.device = torch.device(device)
+
+
+class HostBatch:
+    def __init__(self, idxs, offs, s_fwd):
+        self.idxs, self.offs, self.s_fwd = idxs, offs, s_fwd
+        self.max_lookups = max(len(i) for i in idxs)
+
+
+class OracleExchangeKernels:
+    def __init__(self, tables: HostTables):
+        self.t = tables
+
+    def coalesce(self, batch, dy, ws, ste, layout):
+        assert layout == "tbd"
+        dy = dy.numpy()
+        ws.ucount.zero_()
+        ws.absmax.zero_()
+        for t, n in enumerate(self.t.num_rows):
+            rows, vals, err = O.emb_bwd_coalesce(n, batch.idxs[t], batch.offs[t], dy[t], batch.s_fwd[t], ste)
+            assert err == 0
+            for s in range(SPLIT):
+                k = t * SPLIT + s
+                r0, r1 = slot_rows(n, s)
+                sel = (rows >= r0) & (rows < r1)
+                u = int(sel.sum())
+                b = ws.slot_base[k]
+                assert u <= ws.slot_base[k + 1] - b
+                ws.rows[b: b + u] = torch.from_numpy(rows[sel].astype(np.int32))
+                ws.vals[b: b + u] = torch.from_numpy(vals[sel])
+                ws.ucount[k] = u
+                ws.absmax[k] = float(np.abs(vals[sel]).max()) if u else 0.0
+
+    def quant_pack(self, ws, absmax_all, num_ranks, grad_bits, cap_base, cap_total, s_avg, payload):
+        T, D = self.t.T, self.t.D
+        cb = cap_base.numpy()
+        elem = 1 if grad_bits <= 8 else (2 if grad_bits <= 16 else 4)
+        rows_off = a16(4 * T)
+        vals_off = rows_off + a16(4 * cap_total)
+        p = payload.numpy()
+        p[:] = 0
+        if grad_bits != 32:  # FP32 payloads carry no scale (absmax_all is not gathered)
+            amax = absmax_all.numpy().reshape(num_ranks, T, SPLIT).max(axis=2)
+        for t in range(T):
+            rows, vals = [], []
+            for s in range(SPLIT):
+                k = t * SPLIT + s
+                b, u = ws.slot_base[k], int(ws.ucount[k])
+                rows.append(ws.rows[b: b + u].numpy())
+                vals.append(ws.vals[b: b + u].numpy())
+            rows, vals = np.concatenate(rows), np.concatenate(vals)
+            U = len(rows)
+            assert U <= cb[t + 1] - cb[t]
+            p[4 * t: 4 * t + 4] = np.array([U], np.int32).view(np.uint8)
+            p[rows_off + 4 * cb[t]: rows_off + 4 * (cb[t] + U)] = rows.astype(np.int32).view(np.uint8)
+            if grad_bits == 32:
+                q = vals.astype(f32)
+                s_avg[t] = 1.0
+            else:
+                s = O.average_scale([O.sym_scale(amax[r, t], grad_bits) for r in range(num_ranks)], num_ranks)
+                s_avg[t] = float(s)
+                q = O.quantize(vals, s, grad_bits).astype(np.int8 if elem == 1 else np.int16)
+            lo = vals_off + cb[t] * D * elem
+            p[lo: lo + U * D * elem] = np.ascontiguousarray(q).reshape(-1).view(np.uint8)
+
+    def apply(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack):
+        T, D = self.t.T, self.t.D
+        cb = cap_base.numpy()
+        elem = 1 if grad_bits <= 8 else (2 if grad_bits <= 16 else 4)
+        dt = {1: np.int8, 2: np.int16, 4: f32}[elem]
+        rows_off = a16(4 * T)
+        vals_off = rows_off + a16(4 * cap_total)
+        g = gathered.numpy()
+        for t in range(T):
+            rr, qq = [], []
+            for r in range(num_ranks):
+                p = g[r]
+                U = int(p[4 * t: 4 * t + 4].view(np.int32)[0])
+                rr.append(p[rows_off + 4 * cb[t]: rows_off + 4 * (cb[t] + U)].view(np.int32).astype(np.int64))
+                lo = vals_off + cb[t] * D * elem
+                qq.append(p[lo: lo + U * D * elem].view(dt).reshape(U, D).astype(f32))
+            O.dp_apply(self.t.Ws[t], rr, qq, f32(s_avg[t]), num_ranks, lr,
+                       mode="fp32" if mode == L.DQRM_UPD_FP32 else "dp")
