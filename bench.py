@@ -62,7 +62,32 @@ def parse():
     p.add_argument("--gather-iters", type=int, default=50)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--seed", type=int, default=123)
+    p.add_argument("--traffic-profile", default=None,
+                   help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; "
+                        "default profiles/r1_<config>_summary.json when present")
     return p.parse_args()
+
+
+PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "kaggle": "kaggle"}
+KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
+    "emb_fwd": "k_emb_fwd<{lpr},",
+    "bwd_coalesce": "k_table_bwd<{lpr}, 1>",
+    "grad_quant_pack": "k_quant_pack<{lpr}>",
+    "apply_sparse_update": "k_table_apply<{lpr}>",
+}
+
+
+def pmc_traffic(path, phase, D):
+    """HBM bytes per launch of the phase's kernel from a committed rocprofv3 PMC summary
+    (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    if not path or not os.path.exists(path):
+        return None
+    prefix = KERNEL_SYMBOL[phase].format(lpr=D // 4)
+    for name, v in json.load(open(path))["kernels"].items():
+        if name.startswith(prefix) and v.get("hbm_bytes_per_launch") is not None:
+            return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
+                    "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def make_batches(rows, B_global, rank, world, count, seed, dist_kind, device):
@@ -210,6 +235,8 @@ def main():
     if rank == 0 and a.cpu_baseline:
         cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
 
+    prof = a.traffic_profile or os.path.join(ROOT, "profiles", f"r1_{PROFILE_TAG[a.config]}_summary.json")
+    traffic = pmc_traffic(prof, dom, D)
     if rank == 0:
         value = world * B * a.steps / elapsed
         line = {
@@ -233,7 +260,9 @@ def main():
                 "grad_bits": a.grad_bits, "scale_period": 1, "parallelism": f"dp{world} (tables replicated)",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic["bytes"] if traffic else None, "traffic_unit": "bytes/launch",
+                         "traffic_src": traffic,
                          "alg_bytes_per_launch": alg[dom], "avg_launch_ms": round(kms[dom], 5)},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "int4_gather": gather,

@@ -35,6 +35,19 @@ from .comm import SparseGradExchange
 from .tables import EmbeddingTableSet, LookupBatch
 
 
+_DEFAULT_GRAD_MODE = "sparse"
+
+
+def set_default_grad_mode(mode: str) -> None:
+    """Default ``grad_mode`` of modules constructed afterwards, so a driver can switch its
+    unmodified ``QuantEmbeddingBagTwo(n, m, bit, embedding_id=i)`` calls
+    (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:380) to the DP path with one line."""
+    global _DEFAULT_GRAD_MODE
+    if mode not in _QuantEmbeddingBase.grad_modes:
+        raise ValueError(f"grad_mode must be one of {_QuantEmbeddingBase.grad_modes}")
+    _DEFAULT_GRAD_MODE = mode
+
+
 def _batch_from_input(input: torch.Tensor, offsets: torch.Tensor | None, device) -> LookupBatch:
     """nn.EmbeddingBag input conventions: 1-D input + offsets, or 2-D [B, L] fixed bags."""
     if input.dim() == 2:
@@ -85,6 +98,8 @@ class _QuantEmbeddingBase(nn.Module):
     grad_modes = ("sparse", "fused_sgd", "dp")
 
     def _init_common(self, grad_mode, lr, scale_period, use_packed_int4):
+        if grad_mode is None:
+            grad_mode = _DEFAULT_GRAD_MODE
         if grad_mode not in self.grad_modes:
             raise ValueError(f"grad_mode must be one of {self.grad_modes}")
         self.grad_mode = grad_mode
@@ -169,7 +184,7 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
     def __init__(self, num_embeddings, embedding_dim, embedding_bit=4, full_precision_flag=False,
                  quant_mode="symmetric", fix_flag=False, weight_percentile=0, embedding_id=None, *,
                  device="cuda", weight: torch.Tensor | None = None, init: str = "numpy",
-                 grad_mode: str = "sparse", lr: float | None = None, scale_period: int = 0,
+                 grad_mode: str | None = None, lr: float | None = None, scale_period: int = 0,
                  use_packed_int4: bool = False):
         super().__init__()
         self.num_embeddings = num_embeddings
@@ -246,7 +261,7 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
 
     def __init__(self, ln: Sequence[int], m: int, embedding_bit: int = 4, full_precision_flag: bool = False,
                  *, device="cuda", init: str = "numpy", weights: Sequence[torch.Tensor] | None = None,
-                 grad_mode: str = "sparse", lr: float | None = None, scale_period: int = 0,
+                 grad_mode: str | None = None, lr: float | None = None, scale_period: int = 0,
                  use_packed_int4: bool = False, seed: int = 123):
         super().__init__()
         self.ln = [int(n) for n in ln]
@@ -297,4 +312,4 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         return out
 
 
-__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection"]
+__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode"]
