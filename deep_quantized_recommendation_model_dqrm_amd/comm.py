@@ -11,8 +11,8 @@ per step for all tables together, both all-gathers over RCCL (torch.distributed 
 on ROCm, xGMI point-to-point):
   1. all_gather of the per-slot max|grad| [T*8] -> every rank derives each rank's
      local scale and averages them in Gloo's order (bit-identical on every rank);
-  2. all_gather of one fixed-capacity payload per rank  {counts i32[T], rows i32[CAP],
-     q int8[CAP, D]} -> every rank decodes all N payloads, unions rows and sums the
+  2. all_gather of one fixed-capacity payload per rank  {counts i32[T*8] (per table and
+     row-range slot), rows i32[CAP], q int8[CAP, D]} -> every rank decodes all N payloads, unions rows and sums the
      integers exactly (= Gloo sparse all_reduce, torch-internal: coalesce, allgather,
      sum, coalesce), then applies the dequantized SGD update.
 Kernels: dqrm_emb_bwd_coalesce (K4), dqrm_grad_quant_pack (K5), dqrm_apply_sparse_update (K6).
@@ -76,7 +76,7 @@ def payload_bytes(num_tables: int, cap_total: int, dim: int, grad_bits: int) -> 
     """Bytes of one rank's wire payload (mirrors dqrm_payload_bytes)."""
     a16 = lambda x: (x + 15) & ~15  # noqa: E731
     elem = 1 if grad_bits <= 8 else (2 if grad_bits <= 16 else 4)
-    return a16(4 * num_tables) + a16(4 * cap_total) + a16(cap_total * dim * elem)
+    return a16(4 * num_tables * L.DQRM_TABLE_SPLIT) + a16(4 * cap_total) + a16(cap_total * dim * elem)
 
 
 class SparseGradExchange:

@@ -27,6 +27,16 @@
 
 namespace {
 
+// Diagnostic build only (-DDQRM_DIAG_CLOCK, tools/diag_clock.py): thread 0 of every slot
+// workgroup stamps the 100 MHz wall clock at phase boundaries.
+#ifdef DQRM_DIAG_CLOCK
+__device__ unsigned long long g_diag_clk[8192 * 8];
+#define DIAG_T(k) \
+    do { if (threadIdx.x == 0) g_diag_clk[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define DIAG_T(k) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------------------------
 // error reporting (host)
 // ------------------------------------------------------------------------------------
@@ -231,12 +241,17 @@ __global__ void k_refresh_scale(const float* __restrict__ tmax, float* __restric
     tflags[t] = need;
 }
 
+// INT4-pack the 4 dims of float4 number idx4 of a row (prow = the row's packed bytes)
+DQRM_INLINE void pack4_row(const float4 w, uint8_t* __restrict__ prow, int idx4, float r) {
+    float q0 = fake_quant(w.x, r, -8.0f, 7.0f), q1 = fake_quant(w.y, r, -8.0f, 7.0f);
+    float q2 = fake_quant(w.z, r, -8.0f, 7.0f), q3 = fake_quant(w.w, r, -8.0f, 7.0f);
+    reinterpret_cast<uint16_t*>(prow)[idx4] = pack4_int4(q0, q1, q2, q3);
+}
+
 template <int LPR>
 DQRM_INLINE void pack_row_int4(const float4 w, uint8_t* __restrict__ packed, int64_t grow,
                                int lane, float r) {
-    float q0 = fake_quant(w.x, r, -8.0f, 7.0f), q1 = fake_quant(w.y, r, -8.0f, 7.0f);
-    float q2 = fake_quant(w.z, r, -8.0f, 7.0f), q3 = fake_quant(w.w, r, -8.0f, 7.0f);
-    reinterpret_cast<uint16_t*>(packed + grow * (LPR * 2))[lane] = pack4_int4(q0, q1, q2, q3);
+    pack4_row(w, packed + grow * (LPR * 2), lane, r);
 }
 
 template <int LPR>
@@ -521,7 +536,7 @@ __global__ void __launch_bounds__(256) k_emb_fwd_packed(FwdArgs a) {
 // Per-table workgroup machinery (backward / coalesce / apply).
 // Each table is split into DQRM_TABLE_SPLIT row-range slots (block-aligned); one
 // 512-thread workgroup per (table, slot) gathers the lookups (or payload entries) of its
-// rows as keys (row << 32 | tag) in LDS, sorts them (bitonic), compacts the segment heads
+// rows as keys (row << 32 | tag) in LDS, sorts them (stable radix), compacts the segment heads
 // (= unique rows) and processes every segment in exact sequential order.
 // ------------------------------------------------------------------------------------
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
@@ -556,28 +571,6 @@ DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
 DQRM_INLINE uint32_t key_lo(uint64_t k) { return (uint32_t)k; }
 DQRM_INLINE uint64_t with_lo(uint64_t k, uint32_t lo) { return (k & 0xFFFFFFFF00000000ull) | lo; }
 
-DQRM_INLINE int next_pow2(int n) {
-    int p = 1;
-    while (p < n) p <<= 1;
-    return p;
-}
-
-DQRM_INLINE void bitonic_sort_lds(uint64_t* keys, int n_pow2) {
-    for (int k = 2; k <= n_pow2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const int lj = __builtin_ctz(j);
-            for (int p = threadIdx.x; p < (n_pow2 >> 1); p += blockDim.x) {
-                const int i = ((p >> lj) << (lj + 1)) | (p & (j - 1));  // j is a power of two
-                const int l = i + j;
-                uint64_t x = keys[i], y = keys[l];
-                const bool up = (i & k) == 0;
-                if ((x > y) == up) { keys[i] = y; keys[l] = x; }
-            }
-            __syncthreads();
-        }
-    }
-}
-
 // rows [r0, r1) of slot s of a table with nrows rows (block-aligned split)
 DQRM_INLINE void slot_rows(int64_t nrows, int s, int64_t& r0, int64_t& r1) {
     const int64_t nblk = ceil_div(nrows, BLK);
@@ -608,145 +601,102 @@ DQRM_INLINE int block_excl_scan(int cnt, int* s_wsum, int* total) {
 }
 
 // Sorting a slot's keys. The keys arrive in ascending tag order (lookup position, or
-// (rank, entry)), so what is needed is a STABLE sort by row; three strategies:
-//  * n <= 512: one wave, bitonic in registers (KPL keys per lane, no block barriers);
-//  * narrow row span (<= 2^RADIX_MAX_BITS rows, tiny/mid tables): stable LSD radix sort,
-//    4-bit digits, each thread owning a contiguous run of keys;
-//  * otherwise: bitonic over LDS on the full 64-bit key (row, tag).
-template <int KPL>
-DQRM_INLINE void wave_sort_regs(uint64_t* keys, int n) {
-    const int lane = threadIdx.x % WAVE;
-    uint64_t x[KPL];
-#pragma unroll
-    for (int r = 0; r < KPL; ++r) {
-        const int i = lane * KPL + r;
-        x[r] = i < n ? keys[i] : ~0ull;
-    }
-    constexpr int NP = WAVE * KPL;
-#pragma unroll
-    for (int k = 2; k <= NP; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j < KPL) {  // partner in the same lane
-#pragma unroll
-                for (int r = 0; r < KPL; ++r) {
-                    const int p = r ^ j;
-                    if (p > r) {
-                        const bool up = ((lane * KPL + r) & k) == 0;
-                        const uint64_t a = x[r], b = x[p];
-                        if ((a > b) == up) { x[r] = b; x[p] = a; }
-                    }
-                }
-            } else {        // partner lane = lane ^ (j / KPL)
-#pragma unroll
-                for (int r = 0; r < KPL; ++r) {
-                    const int i = lane * KPL + r;
-                    const bool take_min = ((i & j) == 0) == ((i & k) == 0);
-                    const uint32_t lo = __shfl_xor((uint32_t)x[r], j / KPL, WAVE);
-                    const uint32_t hi = __shfl_xor((uint32_t)(x[r] >> 32), j / KPL, WAVE);
-                    const uint64_t y = ((uint64_t)hi << 32) | lo;
-                    x[r] = take_min ? (x[r] < y ? x[r] : y) : (x[r] < y ? y : x[r]);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < KPL; ++r) {
-        const int i = lane * KPL + r;
-        if (i < n) keys[i] = x[r];
-    }
+// (rank, entry)), so what is needed is a STABLE sort by row: an LSD radix sort on
+// (row - r0), 4-bit digits, wave-parallel. Wave w owns keys [w*64*KPL, (w+1)*64*KPL),
+// held in registers (KPL per lane). Per pass: every wave counts its digits with four
+// bit-sliced ballots per 64 keys, one wave scans the 16x8 (digit, wave) counts, and every
+// lane places its key at base[digit] + (earlier lanes with that digit), the per-digit
+// bases living in lanes 0..15 and read with one bpermute. 3 barriers per pass, no
+// serial per-thread loops. Heads are then compacted with ballots as well.
+DQRM_INLINE uint64_t lanemask_lt() { return (1ull << (threadIdx.x % WAVE)) - 1ull; }
+
+// lanes whose digit equals v, from the four bit-slice ballots
+DQRM_INLINE uint64_t digit_mask(uint32_t v, uint64_t b0, uint64_t b1, uint64_t b2, uint64_t b3) {
+    return ((v & 1) ? b0 : ~b0) & ((v & 2) ? b1 : ~b1) & ((v & 4) ? b2 : ~b2) & ((v & 8) ? b3 : ~b3);
 }
 
-constexpr int RADIX_MAX_BITS = 12;
-
-DQRM_INLINE void radix_sort_rows(uint64_t* keys, uint64_t* tmp, uint16_t* cnt, int n, uint32_t r0, int bits,
-                                 int* s_wsum) {
-    constexpr int NB = 16;
-    const int tid = threadIdx.x;
-    const int CH = (n + TWG - 1) / TWG;
-    const int i0 = min(tid * CH, n), i1 = min(i0 + CH, n);
-    uint64_t* src = keys;
-    uint64_t* dst = tmp;
-    for (int sh = 0; sh < bits; sh += 4) {
-        uint32_t c[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) c[b] = 0;
-        for (int i = i0; i < i1; ++i) {
-            const uint32_t d = ((key_row(src[i]) - r0) >> sh) & (NB - 1);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) c[b] += (d == (uint32_t)b);
-        }
-#pragma unroll
-        for (int b = 0; b < NB; ++b) cnt[b * TWG + tid] = (uint16_t)c[b];
-        __syncthreads();
-        int loc[NB], sum = 0;
-#pragma unroll
-        for (int k = 0; k < NB; ++k) { loc[k] = cnt[tid * NB + k]; sum += loc[k]; }
-        int total;
-        int ex = block_excl_scan(sum, s_wsum, &total);  // digit-major, thread-minor order
-#pragma unroll
-        for (int k = 0; k < NB; ++k) { cnt[tid * NB + k] = (uint16_t)ex; ex += loc[k]; }
-        __syncthreads();
-#pragma unroll
-        for (int b = 0; b < NB; ++b) c[b] = cnt[b * TWG + tid];
-        for (int i = i0; i < i1; ++i) {
-            const uint64_t kk = src[i];
-            const uint32_t d = ((key_row(kk) - r0) >> sh) & (NB - 1);
-            uint32_t p = 0;
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-                if (d == (uint32_t)b) { p = c[b]; c[b] = p + 1; }
-            dst[p] = kk;
-        }
-        __syncthreads();
-        uint64_t* t = src; src = dst; dst = t;
-    }
-    if (src != keys) {
-        for (int i = tid; i < n; i += TWG) keys[i] = src[i];
-        __syncthreads();
-    }
-}
-
-// sort the slot's n keys (rows in [r0, r0 + span)), then compact segment heads:
-// heads[u] = first key of the u-th distinct row. Returns U. (heads are u16: n <= 65536)
-DQRM_INLINE int sort_and_heads(const SlotLds& L, int n, uint32_t r0, uint32_t span, int* s_wsum) {
-    uint64_t* keys = L.keys;
-    uint16_t* heads = L.heads;
+// sort the slot's n keys (rows in [r0, r0 + span)) stably by row, then compact segment
+// heads: heads[u] = index of the first key of the u-th distinct row. Returns U.
+// Wave w owns keys [w*64*kpl, (w+1)*64*kpl), kpl = ceil(n / TWG), 64 at a time.
+DQRM_INLINE int sort_and_heads(const SlotLds& L, int n, uint32_t r0, uint32_t span, int* s_wsum,
+                               bool presorted = false) {
     const int bits = span <= 1 ? 0 : 32 - __builtin_clz(span - 1);
-    if (n <= 512) {
-        if (threadIdx.x < WAVE && n > 1) {
-            if (n <= 64) wave_sort_regs<1>(keys, n);
-            else if (n <= 128) wave_sort_regs<2>(keys, n);
-            else if (n <= 256) wave_sort_regs<4>(keys, n);
-            else wave_sort_regs<8>(keys, n);
+    uint64_t* keys = L.keys;
+    uint64_t* tmp = reinterpret_cast<uint64_t*>(L.heads);  // scratch over heads + stage until heads exist
+    int* s_hist = reinterpret_cast<int*>(reinterpret_cast<unsigned char*>(keys) + SLOT_KEYS * 16);
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const int kpl = (n + TWG - 1) / TWG;
+    const int i0 = w * WAVE * kpl + lane;  // this lane's keys: i0 + k * WAVE, k < kpl
+    const uint64_t lt = lanemask_lt();
+    if (!presorted && bits > 0) {
+        uint64_t* src = keys;
+        uint64_t* dst = tmp;
+        for (int sh = 0; sh < bits; sh += 4) {
+            uint32_t cnt = 0;  // lane d < 16: this wave's keys with digit d
+#pragma unroll 4
+            for (int k = 0; k < kpl; ++k) {
+                const int i = i0 + k * WAVE;
+                const bool v = i < n;
+                const uint32_t d = v ? ((key_row(src[i]) - r0) >> sh) & 15u : 0u;
+                const uint64_t b0 = __ballot(d & 1), b1 = __ballot(d & 2), b2 = __ballot(d & 4), b3 = __ballot(d & 8);
+                cnt += __popcll(digit_mask(lane, b0, b1, b2, b3) & __ballot(v));
+            }
+            if (lane < 16) s_hist[lane * 8 + w] = (int)cnt;
+            __syncthreads();
+            if (w == 0) {  // exclusive scan of the 128 (digit-major, wave-minor) counts
+                const int v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1];
+                int v = v0 + v1;
+#pragma unroll
+                for (int o = 1; o < WAVE; o <<= 1) {
+                    const int y = __shfl_up(v, o, WAVE);
+                    if (lane >= o) v += y;
+                }
+                const int ex = v - v0 - v1;
+                s_hist[2 * lane] = ex;
+                s_hist[2 * lane + 1] = ex + v0;
+            }
+            __syncthreads();
+            uint32_t base = lane < 16 ? (uint32_t)s_hist[lane * 8 + w] : 0u;
+#pragma unroll 4
+            for (int k = 0; k < kpl; ++k) {
+                const int i = i0 + k * WAVE;
+                const bool v = i < n;
+                const uint64_t x = v ? src[i] : 0ull;
+                const uint64_t vmask = __ballot(v);
+                const uint32_t d = ((key_row(x) - r0) >> sh) & 15u;
+                const uint64_t b0 = __ballot(d & 1), b1 = __ballot(d & 2), b2 = __ballot(d & 4), b3 = __ballot(d & 8);
+                const uint64_t mine = digit_mask(d, b0, b1, b2, b3) & vmask;
+                const uint32_t pos = (uint32_t)__shfl((int)base, (int)d, WAVE) + (uint32_t)__popcll(mine & lt);
+                if (v) dst[pos] = x;
+                base += (uint32_t)__popcll(digit_mask(lane, b0, b1, b2, b3) & vmask);
+            }
+            __syncthreads();
+            uint64_t* t = src; src = dst; dst = t;
         }
-        __syncthreads();
-    } else if (bits <= RADIX_MAX_BITS) {
-        // scratch: the heads + stage regions are free until the heads are compacted
-        // (tmp keys: 8*SLOT_KEYS bytes from the heads; digit counters: the 32 KiB after them)
-        static_assert(SLOT_KEYS * 16 + 16 * TWG * 2 <= SLOT_KEYS * 10 + STAGE_FLOATS * 4, "radix scratch");
-        radix_sort_rows(keys, reinterpret_cast<uint64_t*>(L.heads),
-                        reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(keys) + SLOT_KEYS * 16), n, r0,
-                        bits, s_wsum);
-    } else {
-        const int np2 = next_pow2(n);
-        for (int i = n + threadIdx.x; i < np2; i += blockDim.x) keys[i] = ~0ull;
-        __syncthreads();
-        bitonic_sort_lds(keys, np2);
+        if (src != keys) {  // the sorted keys sit in tmp: bring them home (the heads reuse tmp)
+            for (int i = threadIdx.x; i < n; i += TWG) keys[i] = src[i];
+            __syncthreads();
+        }
     }
-    // compact heads with a block-wide scan over chunks of CH keys per thread
-    constexpr int CH = SLOT_KEYS / TWG;
-    const int i0 = threadIdx.x * CH;
-    int cnt = 0;
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) ++cnt;
-    }
-    int U;
-    int u = block_excl_scan(cnt, s_wsum, &U);
-    for (int c = 0; c < CH; ++c) {
-        const int i = i0 + c;
-        if (i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]))) heads[u++] = (uint16_t)i;
+    DIAG_T(6);
+    // heads: first key of every distinct row, by ballots over the same ownership
+    auto is_head = [&](int k) {
+        const int i = i0 + k * WAVE;
+        return i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1]));
+    };
+    int hc = 0;
+#pragma unroll 4
+    for (int k = 0; k < kpl; ++k) hc += __popcll(__ballot(is_head(k)));
+    if (lane == 0) s_wsum[w] = hc;
+    __syncthreads();
+    int run = 0, U = 0;
+    for (int k = 0; k < TWG / WAVE; ++k) { const int c = s_wsum[k]; run += k < w ? c : 0; U += c; }
+#pragma unroll 4
+    for (int k = 0; k < kpl; ++k) {
+        const bool h = is_head(k);
+        const uint64_t hm = __ballot(h);
+        if (h) L.heads[run + __popcll(hm & lt)] = (uint16_t)(i0 + k * WAVE);
+        run += __popcll(hm);
     }
     __syncthreads();
     return U;
@@ -828,51 +778,103 @@ DQRM_INLINE float dl_absmax(const float (&v)[DimLane<LPR>::NDL]) {
     return group_max<DimLane<LPR>::GD>(m);
 }
 
-// repack a dim-lane row: even lanes combine their nibble with the odd neighbour's
+// repack a dim-lane row: even lanes combine their nibble with the odd neighbour's.
+// prow = the row's packed bytes, dim0 = first dim this group owns.
 template <int LPR>
-DQRM_INLINE void dl_pack_int4(const float (&v)[DimLane<LPR>::NDL], uint8_t* packed, int64_t grow, int lig,
-                              float rcp) {
+DQRM_INLINE void dl_pack_int4(const float (&v)[DimLane<LPR>::NDL], uint8_t* prow, int dim0, int lig, float rcp) {
     using DL = DimLane<LPR>;
 #pragma unroll
     for (int d = 0; d < DL::NDL; ++d) {
         const int q = (int)fake_quant(v[d], rcp, -8.0f, 7.0f) + 8;
         const int qn = __shfl_xor(q, 1, WAVE);
-        const int dim = lig + DL::GD * d;
-        if ((dim & 1) == 0) packed[grow * (DL::D / 2) + dim / 2] = (uint8_t)(q | (qn << 4));
+        const int dim = dim0 + lig + DL::GD * d;
+        if ((dim & 1) == 0) prow[dim / 2] = (uint8_t)(q | (qn << 4));
     }
 }
 
-// Visit every short segment (<= LONG_SEG entries) once by float4 lane groups (LPR lanes,
-// strided over heads) through fg(u, i, len, sub), and compact the long ones' indices u
-// (ascending) into s_long. Returns their number.
+// Short segments (<= LONG_SEG entries): one float4 lane group (LPRS lanes) per segment, SB
+// segments of a group in flight together: heads, the first 4 entries' rows of all SB
+// segments and their initial values are loaded before anything is combined (one HBM
+// round trip per SB segments instead of per segment). finit(u, i, sub, st) loads the
+// initial state, ffin(u, i, sub, st) stores the result; combination is strictly in key order.
+struct SegState {
+    float4 acc;   // running value (W row for SGD, sum otherwise)
+    float4 w;     // apply: the W row being updated
+    float aux;    // old rowmax
+};
 
-template <int LPR, class FG>
-DQRM_INLINE int short_segments(const uint16_t* heads, int U, int n, uint16_t* s_long, int* s_wsum, FG&& fg) {
-    const int sub = threadIdx.x % LPR;
-    const int grp = threadIdx.x / LPR;
-    const int ngrp = blockDim.x / LPR;
-    for (int u = grp; u < U; u += ngrp) {
-        const int i = heads[u];
-        const int len = seg_end(heads, U, n, u) - i;
-        if (len > LONG_SEG) continue;
-        fg(u, i, len, sub);
+template <int LPRS, int OP, int SB, class Src, class FI, class FF>
+DQRM_INLINE void short_segments(const uint64_t* keys, const uint16_t* heads, int U, int n, const Src& src,
+                                float nlr, FI&& finit, FF&& ffin) {
+    const int sub = threadIdx.x % LPRS, grp = threadIdx.x / LPRS;
+    constexpr int NGRP = TWG / LPRS;
+    for (int u0 = grp; u0 < U; u0 += NGRP * SB) {
+        int ii[SB], ll[SB];
+#pragma unroll
+        for (int b = 0; b < SB; ++b) {
+            const int u = u0 + b * NGRP;
+            int i = 0, len = 0;
+            if (u < U) {
+                i = heads[u];
+                len = seg_end(heads, U, n, u) - i;
+                if (len > LONG_SEG) len = 0;  // long: block-cooperative path
+            }
+            ii[b] = i;
+            ll[b] = len;
+        }
+        SegState st[SB];
+        typename Src::Raw r[SB][4];
+#pragma unroll
+        for (int b = 0; b < SB; ++b) {
+            if (ll[b]) finit(u0 + b * NGRP, ii[b], sub, st[b]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < ll[b]) r[b][c] = src.fetch(key_lo(keys[ii[b] + c]), sub);
+        }
+#pragma unroll
+        for (int b = 0; b < SB; ++b) {
+            bool first = true;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < ll[b]) st[b].acc = combine<OP>(st[b].acc, src.finish(r[b][c]), first, nlr);
+            for (int j = 4; j < ll[b]; j += 4) {  // 5..LONG_SEG entries
+                typename Src::Raw q[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (j + c < ll[b]) q[c] = src.fetch(key_lo(keys[ii[b] + j + c]), sub);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (j + c < ll[b]) st[b].acc = combine<OP>(st[b].acc, src.finish(q[c]), first, nlr);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < SB; ++b)
+            if (ll[b]) ffin(u0 + b * NGRP, ii[b], sub, st[b]);
     }
-    // ordered compaction: thread tid owns heads [tid*PER, tid*PER + PER)
-    constexpr int PER = SLOT_KEYS / TWG;
-    const int u0 = threadIdx.x * PER;
-    int cnt = 0;
-    for (int c = 0; c < PER; ++c) {
-        const int u = u0 + c;
-        cnt += (u < U && seg_end(heads, U, n, u) - (int)heads[u] > LONG_SEG);
-    }
-    int nlong;
-    int o = block_excl_scan(cnt, s_wsum, &nlong);
-    for (int c = 0; c < PER && cnt; ++c) {
-        const int u = u0 + c;
-        if (u < U && seg_end(heads, U, n, u) - (int)heads[u] > LONG_SEG) { s_long[o++] = (uint16_t)u; --cnt; }
+}
+
+// ordered compaction of the long segments' indices u into s_long (ballots); returns their number
+DQRM_INLINE int compact_long(const uint16_t* heads, int U, int n, uint16_t* s_long, int* s_wsum) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const int kpl = (U + TWG - 1) / TWG;
+    const int u0 = w * WAVE * kpl + lane;
+    const uint64_t lt = lanemask_lt();
+    auto is_long = [&](int u) { return u < U && seg_end(heads, U, n, u) - (int)heads[u] > LONG_SEG; };
+    int c = 0;
+    for (int k = 0; k < kpl; ++k) c += __popcll(__ballot(is_long(u0 + k * WAVE)));
+    if (lane == 0) s_wsum[w] = c;
+    __syncthreads();
+    int run = 0, total = 0;
+    for (int k = 0; k < TWG / WAVE; ++k) { const int x = s_wsum[k]; run += k < w ? x : 0; total += x; }
+    for (int k = 0; k < kpl; ++k) {
+        const int u = u0 + k * WAVE;
+        const bool lg = is_long(u);
+        const uint64_t m = __ballot(lg);
+        if (lg) s_long[run + __popcll(m & lt)] = (uint16_t)u;
+        run += __popcll(m);
     }
     __syncthreads();
-    return nlong;
+    return total;
 }
 
 // Long segments, block-cooperatively. Their entries, concatenated in key order, stream
@@ -1059,13 +1061,37 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const uint64_t* keys, con
     }
 }
 
-// one workgroup per table: re-reduce flagged superblocks, then tmax over all superblocks
-__global__ void k_table_finalize(const float* __restrict__ blkmax, float* __restrict__ sblkmax,
+// one workgroup per table: re-reduce flagged superblocks, then tmax over all superblocks.
+// Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their rowmax, block,
+// superblock and table maxima rebuilt from W here (at most 256 rows x D floats).
+__global__ void k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
+                                 float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                  uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
-                                 const int64_t* __restrict__ meta, int T) {
+                                 const int64_t* __restrict__ meta, int T, int D) {
     Meta m = make_meta(meta, T);
     __shared__ float red[16];
     const int t = blockIdx.x;
+    if (m.num_rows[t] <= BLK) {
+        const int64_t grow = m.row_base[t] + threadIdx.x;
+        float v = 0.0f;
+        if (threadIdx.x < m.num_rows[t]) {
+            const float4* wr = reinterpret_cast<const float4*>(W + grow * D);
+            for (int k = 0; k < D / 4; ++k) v = fmaxf(v, abs_max4(wr[k]));
+            rowmax[grow] = v;
+        }
+        v = wave_max(v);
+        if (threadIdx.x % WAVE == 0) red[threadIdx.x / WAVE] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float r = 0.0f;
+            for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) r = fmaxf(r, red[k]);
+            blkmax[m.blk_base[t]] = r;
+            sblkmax[m.sblk_base[t]] = r;
+            sdirty[m.sblk_base[t]] = 0;
+            tmax[t] = r;
+        }
+        return;
+    }
     const int64_t nblk = ceil_div(m.num_rows[t], BLK);
     const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
     const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
@@ -1214,15 +1240,17 @@ struct BwdArgs {
     float* ws_absmax;
 };
 
-// dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363)
+// dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363);
+// off4 = first float4 of the row this slot owns (dimension-split tables)
 struct DySource {
     const float* base;  // dy + t * dst_t
     int64_t st_b;
     float s;
     int ste;
+    int off4;
     using Raw = float4;
     DQRM_INLINE float4 fetch(uint32_t bag, int sub) const {
-        return reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[sub];
+        return reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[off4 + sub];
     }
     DQRM_INLINE float4 finish(float4 g) const {
         if (ste) {
@@ -1233,13 +1261,127 @@ struct DySource {
     DQRM_INLINE float4 load(uint32_t bag, int sub) const { return finish(fetch(bag, sub)); }
 };
 
+// Narrow tables (at most one 256-row block, i.e. every row would fall into one slot) are
+// split across the SPLIT slots by DIMENSION instead: slot s owns float4s
+// [s*LPRS, (s+1)*LPRS) of every row. All slots gather and sort the same keys, each streams
+// only its slice of the rows, so the long ordered segments of tiny hot tables run on 8
+// CUs at once. Per-row maxima of such tables are rebuilt by k_table_finalize; in the
+// coalesced workspace / payload the table's entries sit in slot SPLIT-1 (which owns the
+// table's single block in the row split).
+template <int LPR>
+struct DimSplit {
+    static constexpr int LPRS = LPR / SPLIT > 0 ? LPR / SPLIT : 1;
+    static constexpr int ACTIVE = LPR / LPRS;  // slots with a slice
+};
+
+DQRM_INLINE bool narrow_table(int64_t nrows) { return nrows <= BLK; }
+
 // MODE 0: fused SGD (single GPU);  MODE 1: coalesce + per-slot max |grad| (DP)
+template <int LPR, int LPRS, int MODE>
+DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_long, int* s_wsum,
+                              unsigned int* s_misc, const Meta& m, int t, int slot, int U, int n, int off4,
+                              bool dsplit, int64_t ws_e0, int64_t cap) {
+    constexpr int D = LPR * 4;
+    uint64_t* keys = sl.keys;
+    const uint16_t* heads = sl.heads;
+    const int64_t rb = m.row_base[t];
+    DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, off4};
+    const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+    float local_absmax = 0.0f;
+
+    auto finit = [&](int, int i, int sub, SegState& st) {
+        const int64_t grow = rb + key_row(keys[i]);
+        if (MODE == 0) {
+            st.acc = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
+            st.aux = dsplit ? 0.0f : a.rowmax[grow];
+        } else {
+            st.acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto ffin = [&](int u, int i, int sub, SegState& st) {
+        const uint32_t row = key_row(keys[i]);
+        const int64_t grow = rb + row;
+        if (MODE == 0) {
+            reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = st.acc;
+            if (a.repack) pack4_row(st.acc, a.packed + grow * (D / 2), off4 + sub, r_pack);
+            if (!dsplit) {
+                const float rm = group_max<LPRS>(abs_max4(st.acc));
+                if (sub == 0) {
+                    a.rowmax[grow] = rm;
+                    keys[i] = with_lo(keys[i], __float_as_uint(st.aux));
+                }
+            }
+        } else {
+            if (u < cap) {
+                const int64_t e = ws_e0 + u;
+                reinterpret_cast<float4*>(a.ws_vals + e * D)[off4 + sub] = st.acc;
+                if (sub == 0 && off4 == 0) a.ws_rows[e] = (int32_t)row;
+            }
+            local_absmax = fmaxf(local_absmax, abs_max4(st.acc));
+        }
+    };
+    constexpr int OP = MODE == 0 ? OP_FMA : OP_SUM;
+    short_segments<LPRS, OP, 4>(keys, heads, U, n, src, a.nlr, finit, ffin);
+
+    using DL = DimLane<LPRS>;
+    auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
+        const int64_t grow = rb + key_row(keys[i]);
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE == 0 ? a.W[grow * D + off4 * 4 + lig + DL::GD * d] : 0.0f;
+    };
+    auto fend = [&](int u, int i, int lig, float (&v)[DL::NDL]) {
+        const uint32_t row = key_row(keys[i]);
+        const int64_t grow = rb + row;
+        if (MODE == 0) {
+#pragma unroll
+            for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = v[d];
+            if (a.repack) dl_pack_int4<LPRS>(v, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
+            if (!dsplit) {
+                const float old_rm = a.rowmax[grow];
+                const float rm = dl_absmax<LPRS>(v);
+                if (lig == 0) {
+                    a.rowmax[grow] = rm;
+                    keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+                }
+            }
+        } else {
+            if (u < cap) {
+                const int64_t e = ws_e0 + u;
+#pragma unroll
+                for (int d = 0; d < DL::NDL; ++d) a.ws_vals[e * D + off4 * 4 + lig + DL::GD * d] = v[d];
+                if (lig == 0 && off4 == 0) a.ws_rows[e] = (int32_t)row;
+            }
+            local_absmax = fmaxf(local_absmax, dl_absmax<LPRS>(v));
+        }
+    };
+    const int nlong = compact_long(heads, U, n, s_long, s_wsum);
+    DIAG_T(3);
+    staged_long_segments<LPRS, OP>(sl, U, n, s_long, nlong, s_wsum, src, a.nlr, fbegin, fend);
+    DIAG_T(4);
+    if (MODE == 1) {
+        local_absmax = wave_max(local_absmax);
+        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
+    }
+    __syncthreads();
+    if (MODE == 0) {
+        if (!dsplit) maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
+    } else if (threadIdx.x == 0) {
+        if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        const int32_t used = U < cap ? U : (int32_t)cap;
+        if (!dsplit) {
+            a.ws_ucount[slot] = used;
+        } else {
+            if (off4 == 0) a.ws_ucount[t * SPLIT + SPLIT - 1] = used;
+            if (slot % SPLIT != SPLIT - 1) a.ws_ucount[slot] = 0;
+        }
+        a.ws_absmax[slot] = __uint_as_float(s_misc[1]);
+    }
+}
+
 template <int LPR, int MODE>
 __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const SlotLds sl(lds);
-    uint64_t* keys = sl.keys;
-    uint16_t* heads = sl.heads;
     __shared__ int s_wsum[TWG / WAVE + 8];   // 64 B: static LDS stays a multiple of 16
     __shared__ unsigned int s_misc[4];
     __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
@@ -1248,101 +1390,55 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     const int T = a.T;
     Meta m = make_meta(a.meta, T);
     const int64_t nrows = m.num_rows[t];
-    const int64_t rb = m.row_base[t];
-    const int D = LPR * 4;
-    int64_t r0, r1;
-    slot_rows(nrows, s, r0, r1);
     const int slot = t * SPLIT + s;
+    const bool dsplit = narrow_table(nrows);
+    using DS = DimSplit<LPR>;
+    int64_t r0, r1;
+    int off4 = 0;
+    if (dsplit) {
+        r0 = 0;
+        r1 = nrows;
+        off4 = s * DS::LPRS;
+        if (s >= DS::ACTIVE) {  // no slice for this slot (D < 4 * SPLIT)
+            if (MODE == 1 && threadIdx.x == 0) {
+                if (s != SPLIT - 1) a.ws_ucount[slot] = 0;
+                a.ws_absmax[slot] = 0.0f;
+            }
+            return;
+        }
+    } else {
+        slot_rows(nrows, s, r0, r1);
+    }
+    const int own = dsplit ? t * SPLIT + SPLIT - 1 : slot;  // workspace slot of these rows
     if (threadIdx.x == 1) s_misc[1] = 0u;
+    DIAG_T(0);
 
-    const int n = gather_lookup_keys(keys, s_wsum, a.idx, a.off, a.idx_base, a.B, t, nrows, r0, r1, s == 0,
+    const int n = gather_lookup_keys(sl.keys, s_wsum, a.idx, a.off, a.idx_base, a.B, t, nrows, r0, r1, s == 0,
                                      a.err);
     if (n < 0) {
-        if (MODE == 1 && threadIdx.x == 0) { a.ws_ucount[slot] = 0; a.ws_absmax[slot] = 0.0f; }
+        if (MODE == 1 && threadIdx.x == 0) {
+            if (off4 == 0) a.ws_ucount[own] = 0;
+            if (!dsplit || s != SPLIT - 1) a.ws_ucount[slot] = 0;
+            a.ws_absmax[slot] = 0.0f;
+        }
         return;
     }
 #if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 1
     if (n >= 0) return;  // diagnostic build: gather only
 #endif
+    DIAG_T(1);
     const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum);
+    DIAG_T(2);
 #if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 2
     if (U >= 0) return;  // diagnostic build: gather + sort + heads
 #endif
-
-    DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste};
-    const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
-    const int64_t cap = MODE == 1 ? a.ws_cap_base[slot + 1] - a.ws_cap_base[slot] : 0;
-    float local_absmax = 0.0f;
-
-    auto group_fn = [&](int u, int i, int len, int sub) {
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        if (MODE == 0) {
-            float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
-            const float old_rm = a.rowmax[grow];
-            w = seg_reduce_group<LPR, OP_FMA>(keys, i, len, w, src, a.nlr, sub);
-            const float rm = group_max<LPR>(abs_max4(w));
-            reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
-            if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
-            if (sub == 0) {
-                a.rowmax[grow] = rm;
-                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-            }
-        } else {
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            acc = seg_reduce_group<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, sub);
-            if (u < cap) {
-                const int64_t e = a.ws_cap_base[slot] + u;
-                reinterpret_cast<float4*>(a.ws_vals + e * D)[sub] = acc;
-                if (sub == 0) a.ws_rows[e] = (int32_t)row;
-            }
-            local_absmax = fmaxf(local_absmax, abs_max4(acc));
-        }
-    };
-    using DL = DimLane<LPR>;
-    auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
-        const int64_t grow = rb + key_row(keys[i]);
-#pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE == 0 ? a.W[grow * D + lig + DL::GD * d] : 0.0f;
-    };
-    auto fend = [&](int u, int i, int lig, float (&v)[DL::NDL]) {
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        if (MODE == 0) {
-            const float old_rm = a.rowmax[grow];
-            const float rm = dl_absmax<LPR>(v);
-#pragma unroll
-            for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + lig + DL::GD * d] = v[d];
-            if (a.repack) dl_pack_int4<LPR>(v, a.packed, grow, lig, r_pack);
-            if (lig == 0) {
-                a.rowmax[grow] = rm;
-                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-            }
-        } else {
-            if (u < cap) {
-                const int64_t e = a.ws_cap_base[slot] + u;
-#pragma unroll
-                for (int d = 0; d < DL::NDL; ++d) a.ws_vals[e * D + lig + DL::GD * d] = v[d];
-                if (lig == 0) a.ws_rows[e] = (int32_t)row;
-            }
-            local_absmax = fmaxf(local_absmax, dl_absmax<LPR>(v));
-        }
-    };
-    const int nlong = short_segments<LPR>(heads, U, n, s_long, s_wsum, group_fn);
-    staged_long_segments<LPR, MODE == 0 ? OP_FMA : OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, a.nlr, fbegin,
-                                                           fend);
-    if (MODE == 1) {
-        local_absmax = wave_max(local_absmax);
-        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
-    }
-    __syncthreads();
-    if (MODE == 0) {
-        maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
-    } else if (threadIdx.x == 0) {
-        if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        a.ws_ucount[slot] = U < cap ? U : (int32_t)cap;
-        a.ws_absmax[slot] = __uint_as_float(s_misc[1]);
-    }
+    const int64_t ws_e0 = MODE == 1 ? a.ws_cap_base[own] : 0;
+    const int64_t cap = MODE == 1 ? a.ws_cap_base[own + 1] - ws_e0 : 0;
+    if (dsplit)
+        bwd_segments<LPR, DS::LPRS, MODE>(a, sl, s_long, s_wsum, s_misc, m, t, slot, U, n, off4, true, ws_e0, cap);
+    else
+        bwd_segments<LPR, LPR, MODE>(a, sl, s_long, s_wsum, s_misc, m, t, slot, U, n, 0, false, ws_e0, cap);
+    DIAG_T(5);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1360,7 +1456,7 @@ __host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64
 __host__ __device__ inline PayloadLayout payload_layout(int T, int64_t cap, int D, int bits) {
     PayloadLayout p;
     p.elem = bits <= 8 ? 1 : (bits <= 16 ? 2 : 4);
-    p.rows_off = align16(4 * (int64_t)T);
+    p.rows_off = align16(4 * (int64_t)T * SPLIT);  // header: entries per (table, slot)
     p.vals_off = p.rows_off + align16(4 * cap);
     p.bytes = p.vals_off + align16(cap * (int64_t)D * p.elem);
     return p;
@@ -1385,22 +1481,39 @@ DQRM_INLINE float average_scale(const float* absmax_all, int T, int N, int t, in
     return acc * inv_n;
 }
 
+// The slots' used entries are enumerated densely (e in [0, sum ucount)): every block builds
+// the clamped per-slot counts, their dense prefix and the per-table scales in LDS, then
+// LPR lanes handle one entry (slot found by a binary search in LDS). Payload header =
+// the entries of each (table, slot), so the receiver needs no search.
 template <int LPR>
-__global__ void k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base, int64_t ws_cap_total,
-                             const int32_t* __restrict__ ws_rows, const float* __restrict__ ws_vals,
-                             const int32_t* __restrict__ ws_ucount, const float* __restrict__ absmax_all,
-                             int N, int bits, const int64_t* __restrict__ cap_base, int64_t cap_total,
-                             float* __restrict__ s_avg, unsigned char* __restrict__ payload) {
-    __shared__ int s_pre[MAX_TABLES * SPLIT];   // exclusive prefix of ucount within each table
+__global__ void __launch_bounds__(256) k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base,
+                                                    int64_t ws_cap_total, const int32_t* __restrict__ ws_rows,
+                                                    const float* __restrict__ ws_vals,
+                                                    const int32_t* __restrict__ ws_ucount,
+                                                    const float* __restrict__ absmax_all, int N, int bits,
+                                                    const int64_t* __restrict__ cap_base, int64_t cap_total,
+                                                    float* __restrict__ s_avg, unsigned char* __restrict__ payload) {
+    __shared__ int s_cnt[MAX_TABLES * SPLIT];      // clamped used entries per slot
+    __shared__ int s_pre[MAX_TABLES * SPLIT + 1];  // dense exclusive prefix of s_cnt
+    __shared__ int s_dst[MAX_TABLES * SPLIT];      // payload entry of each slot's first entry
     __shared__ float s_sc[MAX_TABLES];
+    __shared__ int s_wsum[8 + 1];
     const int D = LPR * 4;
+    const int TS = T * SPLIT;
     const PayloadLayout pl = payload_layout(T, cap_total, D, bits);
     const bool quant = bits >= 2 && bits <= 16;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        int run = 0;
-        for (int s = 0; s < SPLIT; ++s) { s_pre[t * SPLIT + s] = run; run += ws_ucount[t * SPLIT + s]; }
         const int cap = (int)(cap_base[t + 1] - cap_base[t]);
-        if (blockIdx.x == 0) reinterpret_cast<int32_t*>(payload)[t] = run < cap ? run : cap;
+        int run = 0;
+        for (int k = t * SPLIT; k < (t + 1) * SPLIT; ++k) {
+            int c = ws_ucount[k];
+            c = c < cap - run ? c : cap - run;  // overflow: the table's payload is truncated
+            c = c < 0 ? 0 : c;
+            s_cnt[k] = c;
+            s_dst[k] = (int)cap_base[t] + run;
+            if (blockIdx.x == 0) reinterpret_cast<int32_t*>(payload)[k] = c;
+            run += c;
+        }
         if (quant) {
             const float sv = average_scale(absmax_all, T, N, t, bits);
             s_sc[t] = sv;
@@ -1408,18 +1521,48 @@ __global__ void k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base, int
         }
     }
     __syncthreads();
+    {  // dense prefix: thread i owns slots [i*PER, i*PER + PER)
+        constexpr int PER = MAX_TABLES * SPLIT / 256;
+        const int k0 = threadIdx.x * PER;
+        int loc = 0;
+        for (int c = 0; c < PER; ++c) loc += (k0 + c < TS) ? s_cnt[k0 + c] : 0;
+        const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+        int v = loc;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            int y = __shfl_up(v, o, WAVE);
+            if (lane >= o) v += y;
+        }
+        if (lane == WAVE - 1) s_wsum[w] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int run = 0;
+            for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
+            s_pre[TS] = run;
+        }
+        __syncthreads();
+        int run = s_wsum[w] + v - loc;
+        for (int c = 0; c < PER; ++c)
+            if (k0 + c < TS) { s_pre[k0 + c] = run; run += s_cnt[k0 + c]; }
+        __syncthreads();
+    }
+    const int total = s_pre[TS];
     const int lane = threadIdx.x % LPR;
     const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
     const float qlo = -(float)(1 << (bits - 1)), qhi = (float)((1 << (bits - 1)) - 1);
-    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < ws_cap_total; e += ngrp) {
-        const int slot = find_table(ws_cap_base, T * SPLIT, e);
-        const int64_t u = e - ws_cap_base[slot];
-        if (u >= ws_ucount[slot]) continue;
+    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < total; e += ngrp) {
+        int lo = 0, hi = TS - 1;  // last slot with s_pre <= e
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= (int)e) lo = mid; else hi = mid - 1;
+        }
+        const int slot = lo;
+        const int u = (int)e - s_pre[slot];
         const int t = slot / SPLIT;
-        const int64_t q = cap_base[t] + s_pre[slot] + u;  // dense payload entry
-        if (q >= cap_base[t + 1]) continue;
-        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = ws_rows[e];
-        float4 v = reinterpret_cast<const float4*>(ws_vals + e * D)[lane];
+        const int64_t src = ws_cap_base[slot] + u;
+        const int64_t q = s_dst[slot] + u;  // dense payload entry
+        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = ws_rows[src];
+        float4 v = reinterpret_cast<const float4*>(ws_vals + src * D)[lane];
         if (!quant) {
             reinterpret_cast<float4*>(payload + pl.vals_off + q * D * 4)[lane] = v;
             continue;
@@ -1475,6 +1618,7 @@ struct PayloadSource {
     int64_t payload_bytes;
     PayloadLayout pl;
     int64_t cap_base_t;
+    int off4;  // first float4 of the row this slot owns (dimension-split tables)
     using Raw = uint4;
     DQRM_INLINE uint4 fetch(uint32_t lo, int sub) const {
         constexpr int D = LPR * 4;
@@ -1482,12 +1626,12 @@ struct PayloadSource {
         const int64_t e = cap_base_t + (int64_t)(lo & 0xFFFFFF);
         uint4 x = make_uint4(0u, 0u, 0u, 0u);
         if (pl.elem == 1) {
-            x.x = reinterpret_cast<const uint32_t*>(p + e * D)[sub];
+            x.x = reinterpret_cast<const uint32_t*>(p + e * D)[off4 + sub];
         } else if (pl.elem == 2) {
-            const uint2 y = reinterpret_cast<const uint2*>(p + e * D * 2)[sub];
+            const uint2 y = reinterpret_cast<const uint2*>(p + e * D * 2)[off4 + sub];
             x.x = y.x; x.y = y.y;
         } else {
-            x = reinterpret_cast<const uint4*>(p + e * D * 4)[sub];
+            x = reinterpret_cast<const uint4*>(p + e * D * 4)[off4 + sub];
         }
         return x;
     }
@@ -1507,12 +1651,91 @@ struct PayloadSource {
     DQRM_INLINE float4 load(uint32_t lo, int sub) const { return finish(fetch(lo, sub)); }
 };
 
+// dequantize + SGD of one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
+struct ApplyUpdate {
+    int mode;
+    float inv_n, sc, sim_f, nlr;
+    DQRM_INLINE float operator()(float w, float acc) const {
+        float v;
+        if (mode == DQRM_UPD_DP) v = (acc * inv_n) * sc;                  // s_q_g_p_c.py:885,618-622
+        else if (mode == DQRM_UPD_SIMULATED) v = acc * sim_f;            // sgd_quantized_gradients.py:366-371
+        else v = acc * inv_n;                                            // FP32 sparse all_reduce (:319-327)
+        return w + nlr * v;  // separately rounded product, then add
+    }
+};
+
+template <int LPR, int LPRS>
+DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t* s_long, int* s_wsum, const Meta& m,
+                                int t, int U, int n, int off4, bool dsplit, const PayloadLayout& pl) {
+    constexpr int D = LPR * 4;
+    uint64_t* keys = sl.keys;
+    const uint16_t* heads = sl.heads;
+    const int64_t rb = m.row_base[t];
+    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const ApplyUpdate update{a.mode, (float)(1.0 / (double)a.N), sc, (float)((double)sc / (double)a.N), a.nlr};
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, a.cap_base[t], off4};
+
+    auto finit = [&](int, int i, int sub, SegState& st) {
+        const int64_t grow = rb + key_row(keys[i]);
+        st.w = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
+        st.aux = dsplit ? 0.0f : a.rowmax[grow];
+        st.acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
+    // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
+    auto ffin = [&](int, int i, int sub, SegState& st) {
+        const int64_t grow = rb + key_row(keys[i]);
+        float4 w = st.w;
+        w.x = update(w.x, st.acc.x); w.y = update(w.y, st.acc.y);
+        w.z = update(w.z, st.acc.z); w.w = update(w.w, st.acc.w);
+        reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = w;
+        if (a.repack) pack4_row(w, a.packed + grow * (D / 2), off4 + sub, r_pack);
+        if (!dsplit) {
+            const float rm = group_max<LPRS>(abs_max4(w));
+            if (sub == 0) {
+                a.rowmax[grow] = rm;
+                keys[i] = with_lo(keys[i], __float_as_uint(st.aux));
+            }
+        }
+    };
+    short_segments<LPRS, OP_SUM, 4>(keys, heads, U, n, src, 0.0f, finit, ffin);
+
+    using DL = DimLane<LPRS>;
+    auto fbegin = [&](int, int, float (&acc)[DL::NDL]) {
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) acc[d] = 0.0f;
+    };
+    auto fend = [&](int, int i, int lig, float (&acc)[DL::NDL]) {
+        const int64_t grow = rb + key_row(keys[i]);
+        float w[DL::NDL];
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) w[d] = update(a.W[grow * D + off4 * 4 + lig + DL::GD * d], acc[d]);
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = w[d];
+        if (a.repack) dl_pack_int4<LPRS>(w, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
+        if (!dsplit) {
+            const float old_rm = a.rowmax[grow];
+            const float rm = dl_absmax<LPRS>(w);
+            if (lig == 0) {
+                a.rowmax[grow] = rm;
+                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+            }
+        }
+    };
+    const int nlong = compact_long(heads, U, n, s_long, s_wsum);
+    DIAG_T(3);
+    staged_long_segments<LPRS, OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, 0.0f, fbegin, fend);
+    __syncthreads();
+    DIAG_T(4);
+    if (!dsplit) maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
+}
+
 template <int LPR>
 __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const SlotLds sl(lds);
     uint64_t* keys = sl.keys;
-    uint16_t* heads = sl.heads;
     __shared__ int s_wsum[TWG / WAVE + 8];
     __shared__ int s_e0[68];
     __shared__ int s_start[68];
@@ -1523,26 +1746,37 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     const int D = LPR * 4;
     Meta m = make_meta(a.meta, T);
     const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
+    DIAG_T(0);
     const int64_t cap = a.cap_base[t + 1] - a.cap_base[t];
-    const int64_t rb = m.row_base[t];
     const int64_t nrows = m.num_rows[t];
+    const bool dsplit = narrow_table(nrows);
+    using DS = DimSplit<LPR>;
     int64_t r0, r1;
-    slot_rows(nrows, s, r0, r1);
-    if (threadIdx.x < a.N) {  // this slot's entry range in rank r's ascending row list
-        const unsigned char* p = a.payloads + (int64_t)threadIdx.x * a.payload_bytes;
-        int c = reinterpret_cast<const int32_t*>(p)[t];
-        if (c < 0 || c > cap) {
-            if (s == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-            c = c < 0 ? 0 : (int)cap;
+    int off4 = 0, ps = s;  // ps: the payload slot holding this workgroup's rows
+    if (dsplit) {
+        if (s >= DS::ACTIVE) return;
+        r0 = 0;
+        r1 = nrows;
+        off4 = s * DS::LPRS;
+        ps = SPLIT - 1;
+    } else {
+        slot_rows(nrows, s, r0, r1);
+    }
+    if (threadIdx.x < a.N) {  // this slot's entries in rank r's payload: header counts, no search
+        const int32_t* cnt = reinterpret_cast<const int32_t*>(a.payloads + (int64_t)threadIdx.x * a.payload_bytes);
+        int pre = 0, c = 0;
+        for (int k = 0; k < SPLIT; ++k) {
+            int x = cnt[t * SPLIT + k];
+            x = x < 0 ? 0 : x;
+            if (k < ps) pre += x; else if (k == ps) c = x;
         }
-        const int32_t* rows = reinterpret_cast<const int32_t*>(p + pl.rows_off) + a.cap_base[t];
-        int lo = 0, hi = c;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (rows[mid] < r0) lo = mid + 1; else hi = mid; }
-        const int e0 = lo;
-        hi = c;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (rows[mid] < r1) lo = mid + 1; else hi = mid; }
-        s_e0[threadIdx.x] = e0;
-        s_start[threadIdx.x] = lo - e0;  // count, prefix-summed below
+        if (pre + c > cap) {  // cannot happen for payloads this library packed
+            if (s == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+            pre = pre < cap ? pre : (int)cap;
+            c = (int)cap - pre;
+        }
+        s_e0[threadIdx.x] = pre;
+        s_start[threadIdx.x] = c;  // count, prefix-summed below
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1562,7 +1796,7 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
         const int e = s_e0[r] + (i - s_start[r]);
         const unsigned char* p = a.payloads + (int64_t)r * a.payload_bytes;
         int64_t row = reinterpret_cast<const int32_t*>(p + pl.rows_off)[a.cap_base[t] + e];
-        if (row < 0 || row >= nrows) {  // cannot happen for payloads this library packed
+        if (row < r0 || row >= r1) {  // cannot happen for payloads this library packed
             flag_error(a.err, DQRM_ERRF_INDEX);
             row = r0;
         }
@@ -1570,67 +1804,15 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     }
     __syncthreads();
     const int n = M;
-    const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum);
-
-    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
-    const float inv_n = (float)(1.0 / (double)a.N);
-    const float sim_f = (float)((double)sc / (double)a.N);
-    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
-    PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, a.cap_base[t]};
-
-    const int mode = a.mode;
-    const float nlr = a.nlr;
-    // dequantize + SGD, one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
-    auto update = [=](float w, float acc) {
-        float v;
-        if (mode == DQRM_UPD_DP) v = (acc * inv_n) * sc;                  // s_q_g_p_c.py:885,618-622
-        else if (mode == DQRM_UPD_SIMULATED) v = acc * sim_f;            // sgd_quantized_gradients.py:366-371
-        else v = acc * inv_n;                                            // FP32 sparse all_reduce (:319-327)
-        return w + nlr * v;  // separately rounded product, then add
-    };
-    auto group_fn = [&](int u, int i, int len, int sub) {
-        (void)u;
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        float4 w = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
-        const float old_rm = a.rowmax[grow];
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
-        // FP32 path: rank-ordered sum, as Gloo's sparse allreduce + coalesce
-        acc = seg_reduce_group<LPR, OP_SUM>(keys, i, len, acc, src, 0.0f, sub);
-        w.x = update(w.x, acc.x); w.y = update(w.y, acc.y); w.z = update(w.z, acc.z); w.w = update(w.w, acc.w);
-        const float rm = group_max<LPR>(abs_max4(w));
-        reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
-        if (a.repack) pack_row_int4<LPR>(w, a.packed, grow, sub, r_pack);
-        if (sub == 0) {
-            a.rowmax[grow] = rm;
-            keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-        }
-    };
-    using DL = DimLane<LPR>;
-    auto fbegin = [&](int, int, float (&acc)[DL::NDL]) {
-#pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) acc[d] = 0.0f;
-    };
-    auto fend = [&](int, int i, int lig, float (&acc)[DL::NDL]) {
-        const int64_t grow = rb + key_row(keys[i]);
-        float w[DL::NDL];
-#pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) w[d] = update(a.W[grow * D + lig + DL::GD * d], acc[d]);
-        const float old_rm = a.rowmax[grow];
-        const float rm = dl_absmax<LPR>(w);
-#pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + lig + DL::GD * d] = w[d];
-        if (a.repack) dl_pack_int4<LPR>(w, a.packed, grow, lig, r_pack);
-        if (lig == 0) {
-            a.rowmax[grow] = rm;
-            keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
-        }
-    };
-    const int nlong = short_segments<LPR>(heads, U, n, s_long, s_wsum, group_fn);
-    staged_long_segments<LPR, OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, 0.0f, fbegin, fend);
-    __syncthreads();
-    maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
+    DIAG_T(1);
+    // one rank's rows arrive ascending and unique: already sorted
+    const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum, a.N == 1);
+    DIAG_T(2);
+    if (dsplit)
+        apply_segments<LPR, DS::LPRS>(a, sl, s_long, s_wsum, m, t, U, n, off4, true, pl);
+    else
+        apply_segments<LPR, LPR>(a, sl, s_long, s_wsum, m, t, U, n, 0, false, pl);
+    DIAG_T(5);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1680,8 +1862,10 @@ int allow_lds(K kernel, size_t bytes) {
 }
 
 int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
-    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(256), 0, st, set->blkmax, set->sblkmax,
-                       set->sdirty, set->tmax, set->meta, set->num_tables);
+    static_assert(BLK == 256, "finalize: one thread per row of a narrow table");
+    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(256), 0, st, set->W, set->rowmax,
+                       set->blkmax, set->sblkmax, set->sdirty, set->tmax, set->meta, set->num_tables,
+                       set->dim);
     LAUNCH_CHECK();
     return DQRM_OK;
 }
@@ -1692,6 +1876,14 @@ int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
 // C ABI
 // ======================================================================================
 extern "C" {
+
+#ifdef DQRM_DIAG_CLOCK
+int dqrm_diag_clock_read(unsigned long long* host, int n) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag_clk), (size_t)n * sizeof(unsigned long long)));
+    return DQRM_OK;
+}
+#endif
 
 const char* dqrm_last_error(void) { return g_last_error; }
 int dqrm_abi_version(void) { return DQRM_ABI_VERSION; }

@@ -180,9 +180,11 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
                           int32_t* ws_ucount, float* ws_absmax, void* stream);
 
 /* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
- *   [counts i32 T | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
+ *   [counts i32 T*S | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
  *   int8 (bits<=8) / int16 (bits<=16) / f32 (bits==32, unquantized path)]
- * table t's entries sit at [cap_base[t], cap_base[t] + counts[t]), rows ascending. */
+ * counts[t*S+s] = entries of table t in row-range slot s (S = DQRM_TABLE_SPLIT); table t's
+ * entries sit at [cap_base[t], cap_base[t] + sum_s counts[t*S+s]), rows ascending, slot
+ * after slot (so a receiving slot finds its entries without searching). */
 size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits);
 
 /* Scale average + quantize-pack (s_q_g_p_c.py:861-869). absmax_all = the N ranks'

@@ -71,23 +71,24 @@ class OracleExchangeKernels:
         T, D = self.t.T, self.t.D
         cb = cap_base.numpy()
         elem = 1 if grad_bits <= 8 else (2 if grad_bits <= 16 else 4)
-        rows_off = a16(4 * T)
+        rows_off = a16(4 * T * SPLIT)
         vals_off = rows_off + a16(4 * cap_total)
         p = payload.numpy()
         p[:] = 0
         if grad_bits != 32:  # FP32 payloads carry no scale (absmax_all is not gathered)
             amax = absmax_all.numpy().reshape(num_ranks, T, SPLIT).max(axis=2)
         for t in range(T):
-            rows, vals = [], []
+            rows, vals, counts = [], [], []
             for s in range(SPLIT):
                 k = t * SPLIT + s
                 b, u = ws.slot_base[k], int(ws.ucount[k])
                 rows.append(ws.rows[b: b + u].numpy())
                 vals.append(ws.vals[b: b + u].numpy())
+                counts.append(u)
             rows, vals = np.concatenate(rows), np.concatenate(vals)
             U = len(rows)
             assert U <= cb[t + 1] - cb[t]
-            p[4 * t: 4 * t + 4] = np.array([U], np.int32).view(np.uint8)
+            p[4 * t * SPLIT: 4 * (t + 1) * SPLIT] = np.array(counts, np.int32).view(np.uint8)
             p[rows_off + 4 * cb[t]: rows_off + 4 * (cb[t] + U)] = rows.astype(np.int32).view(np.uint8)
             if grad_bits == 32:
                 q = vals.astype(f32)
@@ -104,14 +105,14 @@ class OracleExchangeKernels:
         cb = cap_base.numpy()
         elem = 1 if grad_bits <= 8 else (2 if grad_bits <= 16 else 4)
         dt = {1: np.int8, 2: np.int16, 4: f32}[elem]
-        rows_off = a16(4 * T)
+        rows_off = a16(4 * T * SPLIT)
         vals_off = rows_off + a16(4 * cap_total)
         g = gathered.numpy()
         for t in range(T):
             rr, qq = [], []
             for r in range(num_ranks):
                 p = g[r]
-                U = int(p[4 * t: 4 * t + 4].view(np.int32)[0])
+                U = int(p[4 * t * SPLIT: 4 * (t + 1) * SPLIT].view(np.int32).sum())
                 rr.append(p[rows_off + 4 * cb[t]: rows_off + 4 * (cb[t] + U)].view(np.int32).astype(np.int64))
                 lo = vals_off + cb[t] * D * elem
                 qq.append(p[lo: lo + U * D * elem].view(dt).reshape(U, D).astype(f32))

@@ -171,8 +171,9 @@ def _decode_payload(p, T, cap_base, D, bits, t):
     p = p.cpu().numpy()
     a16 = lambda x: (x + 15) & ~15  # noqa: E731
     CAP = int(cap_base[-1])
-    cnt = p[: 4 * T].view(np.int32)[t]
-    rows_off = a16(4 * T)
+    S = 8  # DQRM_TABLE_SPLIT: the header holds per-(table, slot) counts
+    cnt = int(p[: 4 * T * S].view(np.int32)[t * S: (t + 1) * S].sum())
+    rows_off = a16(4 * T * S)
     vals_off = rows_off + a16(4 * CAP)
     rows = p[rows_off: rows_off + 4 * CAP].view(np.int32)[cap_base[t]: cap_base[t] + cnt]
     dt = np.int8 if bits <= 8 else np.int16
