@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--gather-iters", type=int, default=50)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--seed", type=int, default=123)
+    p.add_argument("--sample-every", type=int, default=8,
+                   help="bracket the dominant kernel with HIP events on every k-th timed step")
     p.add_argument("--traffic-profile", default=None,
                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; "
                         "default profiles/r1_<config>_summary.json when present")
@@ -142,48 +144,61 @@ def main():
     torch.cuda.synchronize()
     setup_s = time.time() - t0
 
-    def step(i, ev=None):
+    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
+
+    def step(i, ev=None, only=None):
+        """One QAT step. ev: per-phase (start, end) events; only: bracket just that phase."""
         b = batches[i % len(batches)]
-        if ev is not None:
-            ev[0][0].record()
+
+        def mark(j, k):
+            if ev is not None and (only is None or only == j):
+                ev[j][k].record()
+
+        mark(0, 0)
         ts.forward(b, bits=4, refresh_scale=True, out=y)
-        if ev is not None:
-            ev[0][1].record()
-            ev[1][0].record()
+        mark(0, 1)
+        mark(1, 0)
         kern.coalesce(b, dy, ex.ws, True, "tbd")
-        if ev is not None:
-            ev[1][1].record()
+        mark(1, 1)
         if ex.world == 1:
             absmax_all = ex.ws.absmax.view(1, -1)
         else:
             ex._all_gather(ex.absmax_all, ex.ws.absmax)
             absmax_all = ex.absmax_all
-        if ev is not None:
-            ev[2][0].record()
+        mark(2, 0)
         kern.quant_pack(ex.ws, absmax_all, ex.world, a.grad_bits, ex.cap_base, ex.cap_total, ex.s_avg, ex.payload)
-        if ev is not None:
-            ev[2][1].record()
+        mark(2, 1)
         if ex.world == 1:
             gathered = ex.payload.view(1, -1)
         else:
             ex._all_gather(ex.gathered, ex.payload)
             gathered = ex.gathered
-        if ev is not None:
-            ev[3][0].record()
+        mark(3, 0)
         kern.apply(ex.cap_base, ex.cap_total, gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg, a.lr,
                    L.DQRM_UPD_DP, False)
-        if ev is not None:
-            ev[3][1].record()
+        mark(3, 1)
 
     for i in range(a.warmup):
         step(i)
+    # per-phase breakdown (untimed): every kernel bracketed by events; picks the dominant one
+    nb = max(10, min(50, a.steps))
+    bev = [timed_events(4) for _ in range(nb)]
+    for i in range(nb):
+        step(i, bev[i])
+    torch.cuda.synchronize()
+    kms = {n: float(np.mean([bev[i][j][0].elapsed_time(bev[i][j][1]) for i in range(nb)])) for j, n in enumerate(names)}
+    dom = max(kms, key=kms.get)
+    dj = names.index(dom)
+    # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
+    # it runs on) on every sample_every-th step, so the events barely perturb the timing
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [timed_events(4) for _ in range(a.steps)]
+    sampled = [i for i in range(a.steps) if i % a.sample_every == 0]
     t_start = time.perf_counter()
     for i in range(a.steps):
-        step(a.warmup + i, evs[i])
+        step(a.warmup + i, evs[i] if i % a.sample_every == 0 else None, only=dj)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -192,8 +207,7 @@ def main():
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
-    kms = {n: float(np.mean([evs[i][j][0].elapsed_time(evs[i][j][1]) for i in range(a.steps)])) for j, n in enumerate(names)}
+    dom_ms = float(np.mean([evs[i][dj][0].elapsed_time(evs[i][dj][1]) for i in sampled]))
 
     # algorithmic bytes per launch; unique counts from the last step
     U = int(ex.ws.ucount.sum().item())
@@ -204,8 +218,7 @@ def main():
         "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
         "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4,
     }
-    dom = max(kms, key=kms.get)
-    achieved = alg[dom] / (kms[dom] * 1e-3) / 1e9
+    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     err = ts.read_errors()
 
     # INT4 packed-gather bandwidth phase (north-star gather metric), outside the timed step
@@ -263,8 +276,10 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes"] if traffic else None, "traffic_unit": "bytes/launch",
                          "traffic_src": traffic,
-                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": round(kms[dom], 5)},
+                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": round(dom_ms, 5),
+                         "timed_launches": len(sampled)},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
+            "kernels_ms_note": "untimed breakdown pass, every kernel bracketed by events",
             "int4_gather": gather,
             "cpu_baseline": cpu,
             "device_errors": err,

@@ -1009,11 +1009,23 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
 // atomicMax on the (non-negative) float bits, a holder that shrank flags the superblock,
 // and k_table_finalize re-reduces flagged superblocks and the table max.
 // ------------------------------------------------------------------------------------
-DQRM_INLINE void maintain_blocks(const Meta& m, int t, const uint64_t* keys, const uint16_t* heads,
-                                 int U, const float* rowmax, float* blkmax, float* sblkmax,
-                                 uint8_t* sdirty) {
+DQRM_INLINE void update_superblock(float* sblkmax, uint8_t* sdirty, int64_t sb, float old_blk, float nb) {
+    const float old_sb = sblkmax[sb];
+    if (old_blk == old_sb && nb < old_blk) sdirty[sb] = 1;
+    if (nb > old_sb) atomicMax(reinterpret_cast<unsigned int*>(sblkmax) + sb, __float_as_uint(nb));
+}
+
+// Blocks whose max may have dropped are queued in LDS (the stage region, free by now) and
+// re-reduced by whole waves (64 lanes x 4 rows = one 256-row block per round trip).
+DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U, const float* rowmax,
+                                 float* blkmax, float* sblkmax, uint8_t* sdirty, int* s_cnt) {
+    const uint64_t* keys = sl.keys;
+    const uint16_t* heads = sl.heads;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(sl.stage);
     const int64_t nrows = m.num_rows[t];
     const int64_t rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    if (threadIdx.x == 0) *s_cnt = 0;
+    __syncthreads();
     for (int u = threadIdx.x; u < U; u += blockDim.x) {
         const uint32_t blk = key_row(keys[heads[u]]) >> 8;
         if (u > 0 && (key_row(keys[heads[u - 1]]) >> 8) == blk) continue;  // not a block start
@@ -1025,46 +1037,55 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const uint64_t* keys, con
         }
         const int cnt = lo - u;
         const float old_blk = blkmax[bb + blk];
-        bool dec = false;
+        bool dec = cnt > 32;  // many touched rows: re-reading the block is cheaper than walking
         float cand = 0.0f;
-        if (cnt <= 32) {
-            for (int k = u; k < lo; ++k) {
-                const uint64_t kk = keys[heads[k]];
-                const float old_rm = __uint_as_float(key_lo(kk));
-                const float new_rm = rowmax[rb + key_row(kk)];
-                dec |= (old_rm == old_blk) && (new_rm < old_rm);
-                cand = fmaxf(cand, new_rm);
+        for (int k = u; k < lo && !dec; k += 4) {
+            float onew[4], oold[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {  // four rows' loads in flight
+                const uint64_t kk = keys[heads[k + c < lo ? k + c : k]];
+                oold[c] = __uint_as_float(key_lo(kk));
+                onew[c] = rowmax[rb + key_row(kk)];
             }
-        } else {
-            dec = true;  // many touched rows: re-reading the block is cheaper than walking
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                dec |= (oold[c] == old_blk) && (onew[c] < oold[c]);
+                cand = fmaxf(cand, onew[c]);
+            }
         }
-        float nb;
         if (dec) {
-            const int64_t r0 = (int64_t)blk * BLK;
-            const int64_t r1 = r0 + BLK < nrows ? r0 + BLK : nrows;
-            float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
-            int64_t r = r0;
-            for (; r + 4 <= r1; r += 4) {
-                v0 = fmaxf(v0, rowmax[rb + r]); v1 = fmaxf(v1, rowmax[rb + r + 1]);
-                v2 = fmaxf(v2, rowmax[rb + r + 2]); v3 = fmaxf(v3, rowmax[rb + r + 3]);
-            }
-            for (; r < r1; ++r) v0 = fmaxf(v0, rowmax[rb + r]);
-            nb = fmaxf(fmaxf(v0, v1), fmaxf(v2, v3));
-        } else {
-            nb = fmaxf(old_blk, cand);
+            queue[atomicAdd(s_cnt, 1)] = blk;
+            continue;
         }
+        const float nb = fmaxf(old_blk, cand);
         blkmax[bb + blk] = nb;
-        const int64_t sb = sbb + (blk >> 8);
-        const float old_sb = sblkmax[sb];
-        if (old_blk == old_sb && nb < old_blk) sdirty[sb] = 1;
-        if (nb > old_sb) atomicMax(reinterpret_cast<unsigned int*>(sblkmax) + sb, __float_as_uint(nb));
+        update_superblock(sblkmax, sdirty, sbb + (blk >> 8), old_blk, nb);
+    }
+    __syncthreads();
+    const int nq = *s_cnt;
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    for (int k = w; k < nq; k += TWG / WAVE) {
+        const uint32_t blk = queue[k];
+        const int64_t r0 = (int64_t)blk * BLK;
+        float v = 0.0f;
+#pragma unroll
+        for (int j = 0; j < BLK / WAVE; ++j) {
+            const int64_t r = r0 + lane + j * WAVE;
+            if (r < nrows) v = fmaxf(v, rowmax[rb + r]);
+        }
+        v = wave_max(v);
+        if (lane == 0) {
+            const float old_blk = blkmax[bb + blk];
+            blkmax[bb + blk] = v;
+            update_superblock(sblkmax, sdirty, sbb + (blk >> 8), old_blk, v);
+        }
     }
 }
 
 // one workgroup per table: re-reduce flagged superblocks, then tmax over all superblocks.
 // Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their rowmax, block,
 // superblock and table maxima rebuilt from W here (at most 256 rows x D floats).
-__global__ void k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
+__global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
                                  float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                  uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
                                  const int64_t* __restrict__ meta, int T, int D) {
@@ -1096,24 +1117,45 @@ __global__ void k_table_finalize(const float* __restrict__ W, float* __restrict_
     const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
     const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    for (int64_t k0 = (int64_t)w * WAVE; k0 < ns; k0 += (int64_t)nw * WAVE) {
-        const int64_t k = k0 + lane;
-        const bool d = k < ns && sdirty[sbb + k];
-        uint64_t msk = __ballot(d);
-        while (msk) {  // rare: a superblock's max holder shrank
-            const int l = __ffsll((long long)msk) - 1;
-            msk &= msk - 1;
-            const int64_t sb = k0 + l;
-            const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-            float v = 0.0f;
-            for (int64_t b = b0 + lane; b < b1; b += WAVE) v = fmaxf(v, blkmax[bb + b]);
-            v = wave_max(v);
-            if (lane == 0) { sblkmax[sbb + sb] = v; sdirty[sbb + sb] = 0; }
+    constexpr int U4 = 4;  // loads in flight per thread
+    for (int64_t k0 = (int64_t)w * WAVE * U4; k0 < ns; k0 += (int64_t)nw * WAVE * U4) {
+        bool d[U4];
+#pragma unroll
+        for (int j = 0; j < U4; ++j) {
+            const int64_t k = k0 + j * WAVE + lane;
+            d[j] = k < ns && sdirty[sbb + k];
+        }
+#pragma unroll
+        for (int j = 0; j < U4; ++j) {
+            uint64_t msk = __ballot(d[j]);
+            while (msk) {  // rare: a superblock's max holder shrank
+                const int l = __ffsll((long long)msk) - 1;
+                msk &= msk - 1;
+                const int64_t sb = k0 + j * WAVE + l;
+                const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+                float v = 0.0f;
+#pragma unroll
+                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+                    const int64_t b = b0 + lane + q * WAVE;
+                    if (b < b1) v = fmaxf(v, blkmax[bb + b]);
+                }
+                v = wave_max(v);
+                if (lane == 0) { sblkmax[sbb + sb] = v; sdirty[sbb + sb] = 0; }
+            }
         }
     }
     __syncthreads();
     float v = 0.0f;
-    for (int64_t k = threadIdx.x; k < ns; k += blockDim.x) v = fmaxf(v, sblkmax[sbb + k]);
+    for (int64_t k0 = threadIdx.x; k0 < ns; k0 += (int64_t)blockDim.x * U4) {
+        float x[U4];
+#pragma unroll
+        for (int j = 0; j < U4; ++j) {
+            const int64_t k = k0 + (int64_t)j * blockDim.x;
+            x[j] = k < ns ? sblkmax[sbb + k] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < U4; ++j) v = fmaxf(v, x[j]);
+    }
     v = wave_max(v);
     if (lane == 0) red[w] = v;
     __syncthreads();
@@ -1180,9 +1222,18 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
     const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
     const int64_t per = (B + blockDim.x - 1) / blockDim.x;
     const int64_t b0 = (int64_t)tid * per, b1 = b0 + per < B ? b0 + per : B;
+    constexpr int RC = 8;  // matches kept in registers (pass 2 re-reads only past RC)
+    uint64_t cache[RC];
     int cnt = 0;
-    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err,
-                       [&](int64_t r, int64_t) { cnt += (r >= r0 && r < r1); });
+    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err, [&](int64_t r, int64_t b) {
+        if (r >= r0 && r < r1) {
+            const uint64_t key = ((uint64_t)r << 32) | (uint64_t)b;
+#pragma unroll
+            for (int c = 0; c < RC; ++c)
+                if (c == cnt) cache[c] = key;
+            ++cnt;
+        }
+    });
     int v = cnt;
 #pragma unroll
     for (int o = 1; o < WAVE; o <<= 1) {
@@ -1203,10 +1254,15 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
         return -1;
     }
     int pos = s_wsum[w] + v - cnt;
-    if (cnt > 0)
+    if (cnt <= RC) {
+#pragma unroll
+        for (int c = 0; c < RC; ++c)
+            if (c < cnt) keys[pos + c] = cache[c];
+    } else {
         visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, false, err, [&](int64_t r, int64_t b) {
             if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
         });
+    }
     __syncthreads();
     return n;
 }
@@ -1364,7 +1420,8 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
     }
     __syncthreads();
     if (MODE == 0) {
-        if (!dsplit) maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
+        if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty,
+                                     reinterpret_cast<int*>(&s_misc[2]));
     } else if (threadIdx.x == 0) {
         if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
         const int32_t used = U < cap ? U : (int32_t)cap;
@@ -1699,7 +1756,7 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
             }
         }
     };
-    short_segments<LPRS, OP_SUM, 4>(keys, heads, U, n, src, 0.0f, finit, ffin);
+    short_segments<LPRS, OP_SUM, 3>(keys, heads, U, n, src, 0.0f, finit, ffin);
 
     using DL = DimLane<LPRS>;
     auto fbegin = [&](int, int, float (&acc)[DL::NDL]) {
@@ -1728,7 +1785,7 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
     staged_long_segments<LPRS, OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, 0.0f, fbegin, fend);
     __syncthreads();
     DIAG_T(4);
-    if (!dsplit) maintain_blocks(m, t, keys, heads, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty);
+    if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, s_wsum + TWG / WAVE + 2);
 }
 
 template <int LPR>
@@ -1855,15 +1912,24 @@ int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
 // allow the per-table kernels more than the default 64 KiB of dynamic LDS (gfx950: 160 KiB/CU)
 template <typename K>
 int allow_lds(K kernel, size_t bytes) {
+    // once per kernel instantiation and size (the attribute is per-function, process-wide;
+    // re-setting it on every call costs host time on the launch path)
+    // (keyed by the kernel's address: several kernels share one function-pointer type)
     if (bytes <= 65536) return DQRM_OK;
-    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    static const void* seen[64];
+    static size_t seen_bytes[64];
+    static int nseen = 0;
+    const void* f = reinterpret_cast<const void*>(kernel);
+    for (int i = 0; i < nseen; ++i)
+        if (seen[i] == f && seen_bytes[i] >= bytes) return DQRM_OK;
+    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    if (nseen < 64) { seen[nseen] = f; seen_bytes[nseen] = bytes; ++nseen; }
     return DQRM_OK;
 }
 
 int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
-    static_assert(BLK == 256, "finalize: one thread per row of a narrow table");
-    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(256), 0, st, set->W, set->rowmax,
+    static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
+    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
                        set->blkmax, set->sblkmax, set->sdirty, set->tmax, set->meta, set->num_tables,
                        set->dim);
     LAUNCH_CHECK();

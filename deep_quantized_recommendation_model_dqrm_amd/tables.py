@@ -25,9 +25,16 @@ def _ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream_handle(stream: torch.cuda.Stream | None = None) -> int:
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return s.cuda_stream
+    """hipStream_t of `stream` (default: torch's current stream on the current device)."""
+    if stream is not None:
+        return stream.cuda_stream
+    if _raw_stream is not None:  # no Stream object construction on the launch path
+        return _raw_stream(torch.cuda.current_device())
+    return torch.cuda.current_stream().cuda_stream
 
 
 def _ceil_div(a: int, b: int) -> int:
