@@ -30,9 +30,9 @@ namespace {
 // Diagnostic build only (-DDQRM_DIAG_CLOCK, tools/diag_clock.py): thread 0 of every slot
 // workgroup stamps the 100 MHz wall clock at phase boundaries.
 #ifdef DQRM_DIAG_CLOCK
-__device__ unsigned long long g_diag_clk[8192 * 8];
+__device__ unsigned long long g_diag_clk[8192 * 16];
 #define DIAG_T(k) \
-    do { if (threadIdx.x == 0) g_diag_clk[blockIdx.x * 8 + (k)] = wall_clock64(); } while (0)
+    do { if (threadIdx.x == 0) g_diag_clk[blockIdx.x * 16 + (k)] = wall_clock64(); } while (0)
 #else
 #define DIAG_T(k) do { } while (0)
 #endif
@@ -793,28 +793,36 @@ DQRM_INLINE void dl_pack_int4(const float (&v)[DimLane<LPR>::NDL], uint8_t* prow
 }
 
 // Short segments (<= LONG_SEG entries): one float4 lane group (LPRS lanes) per segment, SB
-// segments of a group in flight together: heads, the first 4 entries' rows of all SB
-// segments and their initial values are loaded before anything is combined (one HBM
-// round trip per SB segments instead of per segment). finit(u, i, sub, st) loads the
+// segments of a group in flight together: heads, the first entry's row of all SB segments
+// and their initial values are loaded before anything is combined (one HBM round trip per
+// SB segments instead of per segment); further entries follow 4 at a time. finit(u, i, sub, st) loads the
 // initial state, ffin(u, i, sub, st) stores the result; combination is strictly in key order.
 struct SegState {
     float4 acc;   // running value (W row for SGD, sum otherwise)
     float4 w;     // apply: the W row being updated
-    float aux;    // old rowmax
+    float blk;    // old max of the row's 256-row block
 };
+
+// After a wide-table row is updated its head key's low word holds the row's new max |W|
+// (a non-negative float) with bit 31 set iff the row held its block's max and shrank;
+// maintain_blocks reads only these (no rowmax loads; rowmax is store-only on the hot path).
+DQRM_INLINE uint32_t row_record(float new_rm, float old_rm, float old_blk) {
+    return __float_as_uint(new_rm) | ((old_rm == old_blk && new_rm < old_rm) ? 0x80000000u : 0u);
+}
 
 template <int LPRS, int OP, int SB, class Src, class FI, class FF>
 DQRM_INLINE void short_segments(const uint64_t* keys, const uint16_t* heads, int U, int n, const Src& src,
-                                float nlr, FI&& finit, FF&& ffin) {
+                                float nlr, FI&& finit, FF&& ffin, int ubeg = 0, int uend = -1) {
     const int sub = threadIdx.x % LPRS, grp = threadIdx.x / LPRS;
     constexpr int NGRP = TWG / LPRS;
-    for (int u0 = grp; u0 < U; u0 += NGRP * SB) {
+    if (uend < 0) uend = U;
+    for (int u0 = ubeg + grp; u0 < uend; u0 += NGRP * SB) {
         int ii[SB], ll[SB];
 #pragma unroll
         for (int b = 0; b < SB; ++b) {
             const int u = u0 + b * NGRP;
             int i = 0, len = 0;
-            if (u < U) {
+            if (u < uend) {
                 i = heads[u];
                 len = seg_end(heads, U, n, u) - i;
                 if (len > LONG_SEG) len = 0;  // long: block-cooperative path
@@ -823,21 +831,20 @@ DQRM_INLINE void short_segments(const uint64_t* keys, const uint16_t* heads, int
             ll[b] = len;
         }
         SegState st[SB];
-        typename Src::Raw r[SB][4];
+        typename Src::Raw r[SB];
 #pragma unroll
-        for (int b = 0; b < SB; ++b) {
-            if (ll[b]) finit(u0 + b * NGRP, ii[b], sub, st[b]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < ll[b]) r[b][c] = src.fetch(key_lo(keys[ii[b] + c]), sub);
+        for (int b = 0; b < SB; ++b) {  // initial values + the first entry of all SB segments
+            if (ll[b]) {
+                finit(u0 + b * NGRP, ii[b], sub, st[b]);
+                r[b] = src.fetch(key_lo(keys[ii[b]]), sub);
+            }
         }
 #pragma unroll
         for (int b = 0; b < SB; ++b) {
+            if (!ll[b]) continue;
             bool first = true;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (c < ll[b]) st[b].acc = combine<OP>(st[b].acc, src.finish(r[b][c]), first, nlr);
-            for (int j = 4; j < ll[b]; j += 4) {  // 5..LONG_SEG entries
+            st[b].acc = combine<OP>(st[b].acc, src.finish(r[b]), first, nlr);
+            for (int j = 1; j < ll[b]; j += 4) {  // the rest (most segments of wide tables have one entry)
                 typename Src::Raw q[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
@@ -920,6 +927,7 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
         __syncthreads();
     }
     const int E = lpre[nlong];
+    DIAG_T(8);
     // largest k in [lo, hi] with lpre[k] <= e
     auto seg_of = [&](int e, int lo, int hi) {
         while (lo < hi) {
@@ -953,6 +961,7 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
             if (c0 + q / LPR < E) reinterpret_cast<float4*>(L.stage)[q] = src.finish(raw[f]);
         }
         __syncthreads();
+        if (c0 == 0) DIAG_T(9);
         if (c0 + CE < E) fetch(c0 + CE);
         const int ce = min(CE, E - c0);
         const int kf = seg_of(c0, 0, nlong - 1), kl = seg_of(c0 + ce - 1, kf, nlong - 1);
@@ -996,18 +1005,20 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
                 for (int d = 0; d < NDL; ++d) L.carry[par * 256 + lig + GD * d] = acc[d];
             }
         }
+        if (c0 == 0) DIAG_T(10);
         __syncthreads();
     }
 }
 
 // ------------------------------------------------------------------------------------
 // Incremental |W| hierarchy maintenance (exact), per slot.
-// Before it runs, every head key carries its row's OLD rowmax in the low bits. A block's
-// new max is max(old blkmax, new rowmax of its touched rows) unless one of those rows held
-// the old max and shrank (then the block's 256 rowmax are re-read). The slot owns its
+// Before it runs, every head key carries its row's record (row_record: new max |W| and a
+// "held the block max and shrank" bit). A block's new max is max(old blkmax, new maxima of
+// its touched rows) unless a flagged row is among them (then the block's 256 rowmax, which
+// the segment phase keeps current, are re-read). The slot owns its
 // blocks; superblocks can be shared between slots: increases go in with an order-free
 // atomicMax on the (non-negative) float bits, a holder that shrank flags the superblock,
-// and k_table_finalize re-reduces flagged superblocks and the table max.
+// and the table's last workgroup (finalize_table) re-reduces flagged superblocks and tmax.
 // ------------------------------------------------------------------------------------
 DQRM_INLINE void update_superblock(float* sblkmax, uint8_t* sdirty, int64_t sb, float old_blk, float nb) {
     const float old_sb = sblkmax[sb];
@@ -1035,25 +1046,15 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
             const int mid = (lo + hi) >> 1;
             if ((key_row(keys[heads[mid]]) >> 8) == blk) lo = mid + 1; else hi = mid;
         }
-        const int cnt = lo - u;
         const float old_blk = blkmax[bb + blk];
-        bool dec = cnt > 32;  // many touched rows: re-reading the block is cheaper than walking
+        bool dec = lo - u > 32;  // crowded block: one wave re-reducing it beats a serial walk
         float cand = 0.0f;
-        for (int k = u; k < lo && !dec; k += 4) {
-            float onew[4], oold[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {  // four rows' loads in flight
-                const uint64_t kk = keys[heads[k + c < lo ? k + c : k]];
-                oold[c] = __uint_as_float(key_lo(kk));
-                onew[c] = rowmax[rb + key_row(kk)];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                dec |= (oold[c] == old_blk) && (onew[c] < oold[c]);
-                cand = fmaxf(cand, onew[c]);
-            }
+        for (int k = u; k < lo && !dec; ++k) {  // the block's row records (LDS)
+            const uint32_t rec = key_lo(keys[heads[k]]);
+            dec |= (rec >> 31) != 0u;
+            cand = fmaxf(cand, __uint_as_float(rec & 0x7FFFFFFFu));
         }
-        if (dec) {
+        if (dec) {  // re-reduce the block's rowmax (kept current by the segment phase)
             queue[atomicAdd(s_cnt, 1)] = blk;
             continue;
         }
@@ -1082,16 +1083,13 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
     }
 }
 
-// one workgroup per table: re-reduce flagged superblocks, then tmax over all superblocks.
-// Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their rowmax, block,
-// superblock and table maxima rebuilt from W here (at most 256 rows x D floats).
-__global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
-                                 float* __restrict__ blkmax, float* __restrict__ sblkmax,
-                                 uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
-                                 const int64_t* __restrict__ meta, int T, int D) {
-    Meta m = make_meta(meta, T);
+// Per table, after its slot workgroups: re-reduce flagged superblocks, then tmax over all
+// superblocks. Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their
+// rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats).
+DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
+                               float* __restrict__ blkmax, float* __restrict__ sblkmax,
+                               uint8_t* __restrict__ sdirty, float* __restrict__ tmax, int D) {
     __shared__ float red[16];
-    const int t = blockIdx.x;
     if (m.num_rows[t] <= BLK) {
         const int64_t grow = m.row_base[t] + threadIdx.x;
         float v = 0.0f;
@@ -1164,6 +1162,17 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
         for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
         tmax[t] = r;
     }
+}
+
+// One workgroup per table after the slot kernels (a kernel boundary is the cheap way to
+// make the slots' writes visible here: an agent-scope fence inside the slot kernel, e.g. a
+// "last workgroup finalizes" counter, writes back the XCD's L2 and measured 2x slower).
+__global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
+                                                         float* __restrict__ blkmax, float* __restrict__ sblkmax,
+                                                         uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
+                                                         const int64_t* __restrict__ meta, int T, int D) {
+    const Meta m = make_meta(meta, T);
+    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, tmax, D);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -1321,7 +1330,7 @@ struct DySource {
 // split across the SPLIT slots by DIMENSION instead: slot s owns float4s
 // [s*LPRS, (s+1)*LPRS) of every row. All slots gather and sort the same keys, each streams
 // only its slice of the rows, so the long ordered segments of tiny hot tables run on 8
-// CUs at once. Per-row maxima of such tables are rebuilt by k_table_finalize; in the
+// CUs at once. Per-row maxima of such tables are rebuilt by finalize_table; in the
 // coalesced workspace / payload the table's entries sit in slot SPLIT-1 (which owns the
 // table's single block in the row split).
 template <int LPR>
@@ -1349,7 +1358,8 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
         const int64_t grow = rb + key_row(keys[i]);
         if (MODE == 0) {
             st.acc = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
-            st.aux = dsplit ? 0.0f : a.rowmax[grow];
+            st.w = st.acc;  // old row (its max is taken in ffin, after every load is in flight)
+            if (!dsplit) st.blk = a.blkmax[m.blk_base[t] + (key_row(keys[i]) >> 8)];
         } else {
             st.acc = make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -1361,10 +1371,11 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
             reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = st.acc;
             if (a.repack) pack4_row(st.acc, a.packed + grow * (D / 2), off4 + sub, r_pack);
             if (!dsplit) {
+                const float old_rm = group_max<LPRS>(abs_max4(st.w));
                 const float rm = group_max<LPRS>(abs_max4(st.acc));
                 if (sub == 0) {
                     a.rowmax[grow] = rm;
-                    keys[i] = with_lo(keys[i], __float_as_uint(st.aux));
+                    keys[i] = with_lo(keys[i], row_record(rm, old_rm, st.blk));
                 }
             }
         } else {
@@ -1377,7 +1388,7 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
         }
     };
     constexpr int OP = MODE == 0 ? OP_FMA : OP_SUM;
-    short_segments<LPRS, OP, 4>(keys, heads, U, n, src, a.nlr, finit, ffin);
+    short_segments<LPRS, OP, 8>(keys, heads, U, n, src, a.nlr, finit, ffin);
 
     using DL = DimLane<LPRS>;
     auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
@@ -1389,15 +1400,22 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
         const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
         if (MODE == 0) {
+            float old_rm = 0.0f, old_blk = 0.0f;
+            if (!dsplit) {  // the row is still unwritten (and cached since fbegin): its old max
+                float w0[DL::NDL];
+#pragma unroll
+                for (int d = 0; d < DL::NDL; ++d) w0[d] = a.W[grow * D + lig + DL::GD * d];
+                old_rm = dl_absmax<LPRS>(w0);
+                old_blk = a.blkmax[m.blk_base[t] + (row >> 8)];
+            }
 #pragma unroll
             for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = v[d];
             if (a.repack) dl_pack_int4<LPRS>(v, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
             if (!dsplit) {
-                const float old_rm = a.rowmax[grow];
                 const float rm = dl_absmax<LPRS>(v);
                 if (lig == 0) {
                     a.rowmax[grow] = rm;
-                    keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+                    keys[i] = with_lo(keys[i], row_record(rm, old_rm, old_blk));
                 }
             }
         } else {
@@ -1538,104 +1556,99 @@ DQRM_INLINE float average_scale(const float* absmax_all, int T, int N, int t, in
     return acc * inv_n;
 }
 
-// The slots' used entries are enumerated densely (e in [0, sum ucount)): every block builds
-// the clamped per-slot counts, their dense prefix and the per-table scales in LDS, then
-// LPR lanes handle one entry (slot found by a binary search in LDS). Payload header =
-// the entries of each (table, slot), so the receiver needs no search.
+// One workgroup per (table, slot): the table's 8 slot counts are clamped in slot order
+// against the table's payload capacity (overflow truncates the table), the N ranks'
+// per-slot max|grad| are staged in LDS and averaged in Gloo's order, then LPR lanes per
+// entry quantize and store the slot's entries at their dense payload position. Workgroup
+// (t, 0) also writes the table's header counts and s_avg[t].
 template <int LPR>
-__global__ void __launch_bounds__(256) k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base,
+__global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __restrict__ ws_cap_base,
                                                     int64_t ws_cap_total, const int32_t* __restrict__ ws_rows,
                                                     const float* __restrict__ ws_vals,
                                                     const int32_t* __restrict__ ws_ucount,
                                                     const float* __restrict__ absmax_all, int N, int bits,
                                                     const int64_t* __restrict__ cap_base, int64_t cap_total,
                                                     float* __restrict__ s_avg, unsigned char* __restrict__ payload) {
-    __shared__ int s_cnt[MAX_TABLES * SPLIT];      // clamped used entries per slot
-    __shared__ int s_pre[MAX_TABLES * SPLIT + 1];  // dense exclusive prefix of s_cnt
-    __shared__ int s_dst[MAX_TABLES * SPLIT];      // payload entry of each slot's first entry
-    __shared__ float s_sc[MAX_TABLES];
-    __shared__ int s_wsum[8 + 1];
+    __shared__ int s_cnt[SPLIT];
+    __shared__ float s_am[64 * SPLIT];
+    __shared__ int s_pre, s_my;
+    __shared__ float s_sc;
+    (void)ws_cap_total;
+    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
     const int D = LPR * 4;
-    const int TS = T * SPLIT;
     const PayloadLayout pl = payload_layout(T, cap_total, D, bits);
     const bool quant = bits >= 2 && bits <= 16;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+    if (threadIdx.x < SPLIT) s_cnt[threadIdx.x] = ws_ucount[t * SPLIT + threadIdx.x];
+    if (quant)
+        for (int j = threadIdx.x; j < N * SPLIT; j += blockDim.x)
+            s_am[j] = absmax_all[((int64_t)(j / SPLIT) * T + t) * SPLIT + (j % SPLIT)];
+    __syncthreads();
+    if (threadIdx.x == 0) {
         const int cap = (int)(cap_base[t + 1] - cap_base[t]);
         int run = 0;
-        for (int k = t * SPLIT; k < (t + 1) * SPLIT; ++k) {
-            int c = ws_ucount[k];
+        for (int ss = 0; ss < SPLIT; ++ss) {
+            int c = s_cnt[ss];
             c = c < cap - run ? c : cap - run;  // overflow: the table's payload is truncated
             c = c < 0 ? 0 : c;
-            s_cnt[k] = c;
-            s_dst[k] = (int)cap_base[t] + run;
-            if (blockIdx.x == 0) reinterpret_cast<int32_t*>(payload)[k] = c;
+            if (ss == s) { s_pre = run; s_my = c; }
+            if (s == 0) reinterpret_cast<int32_t*>(payload)[t * SPLIT + ss] = c;
             run += c;
         }
-        if (quant) {
-            const float sv = average_scale(absmax_all, T, N, t, bits);
-            s_sc[t] = sv;
-            if (blockIdx.x == 0) s_avg[t] = sv;
+        if (quant) {  // rank scales, then Gloo's one-element all_reduce order
+            const float inv_n = (float)(1.0 / (double)N);
+            float acc = 0.0f;
+            for (int r = N - 1; r >= 0; --r) {
+                float am = 0.0f;
+                for (int ss = 0; ss < SPLIT; ++ss) am = fmaxf(am, s_am[r * SPLIT + ss]);
+                const float sr = sym_scale(am, bits);
+                acc = r == N - 1 ? sr : acc + sr;
+            }
+            const float sv = acc * inv_n;
+            s_sc = sv;
+            if (s == 0) s_avg[t] = sv;
         }
     }
     __syncthreads();
-    {  // dense prefix: thread i owns slots [i*PER, i*PER + PER)
-        constexpr int PER = MAX_TABLES * SPLIT / 256;
-        const int k0 = threadIdx.x * PER;
-        int loc = 0;
-        for (int c = 0; c < PER; ++c) loc += (k0 + c < TS) ? s_cnt[k0 + c] : 0;
-        const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
-        int v = loc;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            int y = __shfl_up(v, o, WAVE);
-            if (lane >= o) v += y;
-        }
-        if (lane == WAVE - 1) s_wsum[w] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int run = 0;
-            for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
-            s_pre[TS] = run;
-        }
-        __syncthreads();
-        int run = s_wsum[w] + v - loc;
-        for (int c = 0; c < PER; ++c)
-            if (k0 + c < TS) { s_pre[k0 + c] = run; run += s_cnt[k0 + c]; }
-        __syncthreads();
-    }
-    const int total = s_pre[TS];
+    const int cnt = s_my;
+    const int64_t src0 = ws_cap_base[k], dst0 = cap_base[t] + s_pre;
+    const float rr = quant ? 1.0f / s_sc : 0.0f;
     const int lane = threadIdx.x % LPR;
-    const int64_t ngrp = (int64_t)gridDim.x * blockDim.x / LPR;
+    constexpr int QU = 4;                 // entries in flight per lane group
+    constexpr int EPI = 512 / LPR;        // lane groups per workgroup
     const float qlo = -(float)(1 << (bits - 1)), qhi = (float)((1 << (bits - 1)) - 1);
-    for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR; e < total; e += ngrp) {
-        int lo = 0, hi = TS - 1;  // last slot with s_pre <= e
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pre[mid] <= (int)e) lo = mid; else hi = mid - 1;
+    for (int u0 = threadIdx.x / LPR; u0 < cnt; u0 += QU * EPI) {
+        float4 v[QU];
+        int32_t row[QU];
+#pragma unroll
+        for (int h = 0; h < QU; ++h) {  // QU entries' loads in flight
+            const int u = u0 + h * EPI;
+            if (u < cnt) {
+                v[h] = reinterpret_cast<const float4*>(ws_vals + (src0 + u) * D)[lane];
+                row[h] = ws_rows[src0 + u];
+            }
         }
-        const int slot = lo;
-        const int u = (int)e - s_pre[slot];
-        const int t = slot / SPLIT;
-        const int64_t src = ws_cap_base[slot] + u;
-        const int64_t q = s_dst[slot] + u;  // dense payload entry
-        if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = ws_rows[src];
-        float4 v = reinterpret_cast<const float4*>(ws_vals + src * D)[lane];
-        if (!quant) {
-            reinterpret_cast<float4*>(payload + pl.vals_off + q * D * 4)[lane] = v;
-            continue;
-        }
-        const float rr = 1.0f / s_sc[t];
-        const float q0 = fake_quant(v.x, rr, qlo, qhi), q1 = fake_quant(v.y, rr, qlo, qhi);
-        const float q2 = fake_quant(v.z, rr, qlo, qhi), q3 = fake_quant(v.w, rr, qlo, qhi);
-        if (pl.elem == 1) {
-            uint32_t pk = ((uint32_t)(uint8_t)(int8_t)(int)q0) | ((uint32_t)(uint8_t)(int8_t)(int)q1 << 8) |
-                          ((uint32_t)(uint8_t)(int8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int8_t)(int)q3 << 24);
-            reinterpret_cast<uint32_t*>(payload + pl.vals_off + q * D)[lane] = pk;
-        } else {
-            uint2 pk;
-            pk.x = ((uint32_t)(uint16_t)(int16_t)(int)q0) | ((uint32_t)(uint16_t)(int16_t)(int)q1 << 16);
-            pk.y = ((uint32_t)(uint16_t)(int16_t)(int)q2) | ((uint32_t)(uint16_t)(int16_t)(int)q3 << 16);
-            reinterpret_cast<uint2*>(payload + pl.vals_off + q * D * 2)[lane] = pk;
+#pragma unroll
+        for (int h = 0; h < QU; ++h) {
+            const int u = u0 + h * EPI;
+            if (u >= cnt) continue;
+            const int64_t q = dst0 + u;  // dense payload entry
+            if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = row[h];
+            if (!quant) {
+                reinterpret_cast<float4*>(payload + pl.vals_off + q * D * 4)[lane] = v[h];
+                continue;
+            }
+            const float q0 = fake_quant(v[h].x, rr, qlo, qhi), q1 = fake_quant(v[h].y, rr, qlo, qhi);
+            const float q2 = fake_quant(v[h].z, rr, qlo, qhi), q3 = fake_quant(v[h].w, rr, qlo, qhi);
+            if (pl.elem == 1) {
+                uint32_t pk = ((uint32_t)(uint8_t)(int8_t)(int)q0) | ((uint32_t)(uint8_t)(int8_t)(int)q1 << 8) |
+                              ((uint32_t)(uint8_t)(int8_t)(int)q2 << 16) | ((uint32_t)(uint8_t)(int8_t)(int)q3 << 24);
+                reinterpret_cast<uint32_t*>(payload + pl.vals_off + q * D)[lane] = pk;
+            } else {
+                uint2 pk;
+                pk.x = ((uint32_t)(uint16_t)(int16_t)(int)q0) | ((uint32_t)(uint16_t)(int16_t)(int)q1 << 16);
+                pk.y = ((uint32_t)(uint16_t)(int16_t)(int)q2) | ((uint32_t)(uint16_t)(int16_t)(int)q3 << 16);
+                reinterpret_cast<uint2*>(payload + pl.vals_off + q * D * 2)[lane] = pk;
+            }
         }
     }
 }
@@ -1736,7 +1749,7 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
     auto finit = [&](int, int i, int sub, SegState& st) {
         const int64_t grow = rb + key_row(keys[i]);
         st.w = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
-        st.aux = dsplit ? 0.0f : a.rowmax[grow];
+        if (!dsplit) st.blk = a.blkmax[m.blk_base[t] + (key_row(keys[i]) >> 8)];
         st.acc = make_float4(0.f, 0.f, 0.f, 0.f);
     };
     // integer-valued sums are exact in f32 (|sum| <= 2^15 * N << 2^24);
@@ -1749,14 +1762,15 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
         reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = w;
         if (a.repack) pack4_row(w, a.packed + grow * (D / 2), off4 + sub, r_pack);
         if (!dsplit) {
+            const float old_rm = group_max<LPRS>(abs_max4(st.w));
             const float rm = group_max<LPRS>(abs_max4(w));
             if (sub == 0) {
                 a.rowmax[grow] = rm;
-                keys[i] = with_lo(keys[i], __float_as_uint(st.aux));
+                keys[i] = with_lo(keys[i], row_record(rm, old_rm, st.blk));
             }
         }
     };
-    short_segments<LPRS, OP_SUM, 3>(keys, heads, U, n, src, 0.0f, finit, ffin);
+    short_segments<LPRS, OP_SUM, 8>(keys, heads, U, n, src, 0.0f, finit, ffin);
 
     using DL = DimLane<LPRS>;
     auto fbegin = [&](int, int, float (&acc)[DL::NDL]) {
@@ -1767,16 +1781,19 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
         const int64_t grow = rb + key_row(keys[i]);
         float w[DL::NDL];
 #pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) w[d] = update(a.W[grow * D + off4 * 4 + lig + DL::GD * d], acc[d]);
+        for (int d = 0; d < DL::NDL; ++d) w[d] = a.W[grow * D + off4 * 4 + lig + DL::GD * d];
+        const float old_rm = dsplit ? 0.0f : dl_absmax<LPRS>(w);
+        const float old_blk = dsplit ? 0.0f : a.blkmax[m.blk_base[t] + (key_row(keys[i]) >> 8)];
+#pragma unroll
+        for (int d = 0; d < DL::NDL; ++d) w[d] = update(w[d], acc[d]);
 #pragma unroll
         for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = w[d];
         if (a.repack) dl_pack_int4<LPRS>(w, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
         if (!dsplit) {
-            const float old_rm = a.rowmax[grow];
             const float rm = dl_absmax<LPRS>(w);
             if (lig == 0) {
                 a.rowmax[grow] = rm;
-                keys[i] = with_lo(keys[i], __float_as_uint(old_rm));
+                keys[i] = with_lo(keys[i], row_record(rm, old_rm, old_blk));
             }
         }
     };
@@ -1890,6 +1907,15 @@ int check_set(const dqrm_table_set* s) {
     return DQRM_OK;
 }
 
+int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
+    static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
+    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
+                       set->blkmax, set->sblkmax, set->sdirty, set->tmax, set->meta, set->num_tables,
+                       set->dim);
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
 int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
     int64_t b = (work_items + threads - 1) / threads;
     if (b < 1) b = 1;
@@ -1927,14 +1953,6 @@ int allow_lds(K kernel, size_t bytes) {
     return DQRM_OK;
 }
 
-int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
-    static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
-    hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
-                       set->blkmax, set->sblkmax, set->sdirty, set->tmax, set->meta, set->num_tables,
-                       set->dim);
-    LAUNCH_CHECK();
-    return DQRM_OK;
-}
 
 }  // namespace
 
@@ -2164,7 +2182,7 @@ int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, in
         return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_grad_quant_pack");
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_LPR(dim, {
-        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(grid_for(ws_cap_total * LPR, 256, 2048)), dim3(256), 0, st,
+        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
                            num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, absmax_all,
                            num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload);
     });

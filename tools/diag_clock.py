@@ -29,12 +29,13 @@ P = torch.stack([torch.randint(0, n, (B,), device="cuda") for n in rows])
 b = dq.LookupBatch.pooling_one(P)
 dy = torch.randn(T, B, D, device="cuda") * 0.05
 ex = dq.SparseGradExchange(ts, B, grad_bits=8)
-buf = np.zeros(T * 8 * 8, dtype=np.uint64)
+buf = np.zeros(T * 8 * 16, dtype=np.uint64)
 
 
 def report(name):
+    buf[:] = 0
     lib.dqrm_diag_clock_read(buf.ctypes.data, buf.size)
-    c = buf.reshape(T, 8, 8).astype(np.int64)
+    c = buf.reshape(T, 8, 16).astype(np.int64)
     k0 = c[:, :, 0].min()
     print(f"== {name}: kernel span {(c[:, :, 5].max() - k0) / 100:.1f} us "
           "(per table, slowest slot: start gather sort short long tail | end)")
@@ -44,7 +45,9 @@ def report(name):
         p = c[t, s]
         ph = [(p[0] - k0)] + [p[i + 1] - p[i] for i in range(5)]
         print(f"t{t:2d} n={rows[t]:>10d} slot{s}: " + " ".join(f"{x / 100:6.1f}" for x in ph) +
-              f" | {(p[5] - k0) / 100:6.1f}   (sort proper {(p[6] - p[1]) / 100:5.1f}, heads {(p[2] - p[6]) / 100:5.1f})")
+              f" | {(p[5] - k0) / 100:6.1f}   (sort {(p[6] - p[1]) / 100:4.1f} heads {(p[2] - p[6]) / 100:4.1f})" +
+              (f" long: prefix {(p[8] - p[3]) / 100:4.1f} fetch+stage {(p[9] - p[8]) / 100:4.1f} "
+               f"reduce0 {(p[10] - p[9]) / 100:4.1f} rest {(p[4] - p[10]) / 100:4.1f}" if p[4] - p[3] > 200 else ""))
 
 
 for _ in range(3):
