@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--gather-iters", type=int, default=50)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--seed", type=int, default=123)
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl (= RCCL on ROCm) for measurements; gloo only to rehearse N>1 on one GPU")
     p.add_argument("--sample-every", type=int, default=8,
                    help="bracket the dominant kernel with HIP events on every k-th timed step")
     p.add_argument("--traffic-profile", default=None,
@@ -126,10 +128,15 @@ def main():
         if world == 1 and a.gpus > 1:
             print("N>1 must be launched with torch.distributed.run", file=sys.stderr)
             sys.exit(2)
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":  # RCCL over xGMI, one process per GPU
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # gloo: functional rehearsal of the N>1 path (e.g. several ranks on one GPU)
+            dist.init_process_group("gloo")
     cfg = CONFIGS[a.config]
     rows, D, B = cfg["rows"], cfg["dim"], a.batch_per_gpu
     T = len(rows)
@@ -248,6 +255,16 @@ def main():
     if rank == 0 and a.cpu_baseline:
         cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
 
+    # replicas must stay bit-identical (deterministic kernels, same exchanged data): compare a
+    # checksum of every rank's W bit patterns and table maxima (outside the timed region)
+    cs = torch.stack([ts.W.view(torch.int32).sum(dtype=torch.int64),
+                      ts.tmax.view(torch.int32).sum(dtype=torch.int64)])
+    if world > 1:
+        allcs = [torch.zeros_like(cs) for _ in range(world)]
+        dist.all_gather(allcs, cs)
+        replicas_match = all(torch.equal(allcs[0], c) for c in allcs)
+    else:
+        replicas_match = True
     prof = a.traffic_profile or os.path.join(ROOT, "profiles", f"r1_{PROFILE_TAG[a.config]}_summary.json")
     traffic = pmc_traffic(prof, dom, D)
     if rank == 0:
@@ -283,6 +300,7 @@ def main():
             "int4_gather": gather,
             "cpu_baseline": cpu,
             "device_errors": err,
+            "replicas_bit_identical": replicas_match,
             "setup_s": round(setup_s, 1),
         }
         print(json.dumps(line), flush=True)

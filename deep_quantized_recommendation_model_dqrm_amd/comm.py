@@ -124,6 +124,10 @@ class SparseGradExchange:
         backend = dist.get_backend(self.group)
         if backend == "nccl":  # RCCL on ROCm: one all-gather straight into the output
             dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group)
+        elif out.is_cuda:  # Gloo gathers host tensors: stage through host memory (debug / rehearsal)
+            host = out.cpu()
+            dist.all_gather(list(host.unbind(0)), inp.cpu(), group=self.group)
+            out.copy_(host)
         else:
             dist.all_gather(list(out.unbind(0)), inp, group=self.group)
 
