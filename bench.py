@@ -257,8 +257,9 @@ def main():
 
     # replicas must stay bit-identical (deterministic kernels, same exchanged data): compare a
     # checksum of every rank's W bit patterns and table maxima (outside the timed region)
-    cs = torch.stack([ts.W.view(torch.int32).sum(dtype=torch.int64),
-                      ts.tmax.view(torch.int32).sum(dtype=torch.int64)])
+    wbits = ts.W.view(-1).view(torch.int32)
+    wsum = sum(c.sum(dtype=torch.int64) for c in wbits.split(1 << 26))  # 512 MB int64 temporaries
+    cs = torch.stack([wsum, ts.tmax.view(torch.int32).sum(dtype=torch.int64)])
     if world > 1:
         allcs = [torch.zeros_like(cs) for _ in range(world)]
         dist.all_gather(allcs, cs)
