@@ -17,6 +17,7 @@ DQRM_E_HIP = -2
 DQRM_E_CAPACITY = -3
 DQRM_E_WORKSPACE = -4
 
+DQRM_BATCH_POOLING_ONE = 1
 DQRM_ERRF_INDEX = 1
 DQRM_ERRF_OFFSET = 2
 DQRM_ERRF_OVERFLOW = 4
@@ -88,6 +89,8 @@ class Batch(C.Structure):
         ("idx_base", C.c_void_p),
         ("num_bags", C.c_int64),
         ("max_lookups", C.c_int64),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

@@ -296,6 +296,7 @@ struct FwdArgs {
     int T;
     int bits;
     uint32_t flags;
+    int pool1;  // DQRM_BATCH_POOLING_ONE: bag b of every table is lookup b (offsets unread)
 };
 
 template <int LPR, int UNR>
@@ -332,8 +333,9 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
             const int64_t b = b0 + k * G + grp;
             const bool valid = b < B;
             const int64_t bb = valid ? b : 0;
-            int64_t s0 = off[bb];
-            int64_t s1 = (bb + 1 < B) ? off[bb + 1] : L;
+            const bool p1 = a.pool1 && L == B;
+            int64_t s0 = p1 ? bb : off[bb];
+            int64_t s1 = p1 ? bb + 1 : ((bb + 1 < B) ? off[bb + 1] : L);
             if (s0 < 0 || s1 > L || s1 < s0) {
                 if (valid && lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
                 s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
@@ -446,8 +448,9 @@ __global__ void __launch_bounds__(256) k_emb_fwd_packed(FwdArgs a) {
         int len = -1;
         int64_t row = -1;
         if (b < B) {
-            s0 = off[b];
-            s1 = (b + 1 < B) ? off[b + 1] : L;
+            const bool p1 = a.pool1 && L == B;
+            s0 = p1 ? b : off[b];
+            s1 = p1 ? b + 1 : ((b + 1 < B) ? off[b + 1] : L);
             if (s0 < 0 || s1 > L || s1 < s0) {
                 flag_error(a.err, DQRM_ERRF_OFFSET);
                 s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
@@ -546,12 +549,14 @@ constexpr int SLOT_KEYS = DQRM_SLOT_KEYS;      // keys one slot sorts on chip (6
 constexpr int LONG_SEG = 8;   // longer segments are combined block-cooperatively
 constexpr int LONG_SEGS_MAX = SLOT_KEYS / (LONG_SEG + 1) + 1;
 constexpr int STAGE_FLOATS = 16384;                        // 64 KiB
+constexpr int STAGE_PAD = 1024;                            // dim-major stage: +4 floats per dim row
 constexpr int STAGE_F4 = STAGE_FLOATS / 4 / TWG;           // 8 float4 per thread per chunk
 constexpr int CARRY_FLOATS = 2 * 256;                      // two rows of max D
 constexpr int LPRE_INTS = (LONG_SEGS_MAX + 1 + 3) / 4 * 4;
 // dynamic LDS of a slot workgroup: keys u64 | heads u16 | stage | carry | long prefix
-constexpr int SLOT_LDS = SLOT_KEYS * 8 + SLOT_KEYS * 2 + STAGE_FLOATS * 4 + CARRY_FLOATS * 4 + LPRE_INTS * 4;
-static_assert(SLOT_LDS + 4096 <= 160 * 1024, "slot LDS budget");
+constexpr int SLOT_LDS =
+    SLOT_KEYS * 8 + SLOT_KEYS * 2 + (STAGE_FLOATS + STAGE_PAD) * 4 + CARRY_FLOATS * 4 + LPRE_INTS * 4;
+static_assert(SLOT_LDS + 3072 <= 160 * 1024, "slot LDS budget (dynamic + static)");
 
 struct SlotLds {
     uint64_t* keys;
@@ -563,8 +568,8 @@ struct SlotLds {
         : keys(reinterpret_cast<uint64_t*>(lds)),
           heads(reinterpret_cast<uint16_t*>(lds + SLOT_KEYS * 8)),
           stage(reinterpret_cast<float*>(lds + SLOT_KEYS * 10)),
-          carry(reinterpret_cast<float*>(lds + SLOT_KEYS * 10 + STAGE_FLOATS * 4)),
-          lpre(reinterpret_cast<int*>(lds + SLOT_KEYS * 10 + STAGE_FLOATS * 4 + CARRY_FLOATS * 4)) {}
+          carry(reinterpret_cast<float*>(lds + SLOT_KEYS * 10 + (STAGE_FLOATS + STAGE_PAD) * 4)),
+          lpre(reinterpret_cast<int*>(lds + SLOT_KEYS * 10 + (STAGE_FLOATS + STAGE_PAD) * 4 + CARRY_FLOATS * 4)) {}
 };
 
 DQRM_INLINE uint32_t key_row(uint64_t k) { return (uint32_t)(k >> 32); }
@@ -900,7 +905,9 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
     using DL = DimLane<LPR>;
     constexpr int GD = DL::GD, NDL = DL::NDL;
     constexpr int CE = STAGE_FLOATS / D;          // entries per chunk
-    constexpr int EPF = TWG / LPR;                // entries between a thread's fetches
+    constexpr int SP = CE + 4;                    // stage row pitch (floats) of one dim
+    static_assert(D * SP <= STAGE_FLOATS + STAGE_PAD, "dim-major stage");
+    static_assert(STAGE_F4 <= LONG_SEG + 1, "forward walk: at most one segment boundary per lane group");
     const uint64_t* keys = L.keys;
     const uint16_t* heads = L.heads;
     int* lpre = L.lpre;
@@ -938,16 +945,25 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
     };
     const int sub = threadIdx.x % LPR;
     typename Src::Raw raw[STAGE_F4];
+    // lane group g stages entries [c0 + g*STAGE_F4, +STAGE_F4): one segment search, then a
+    // forward walk (segments are > LONG_SEG >= STAGE_F4 entries long)
     auto fetch = [&](int c0) {
-        const int e0 = c0 + threadIdx.x / LPR;
-        int k = e0 < E ? seg_of(e0, 0, nlong - 1) : 0;
+        const int e0 = c0 + (threadIdx.x / LPR) * STAGE_F4;
+        if (e0 >= E) return;
+        int k = seg_of(e0, 0, nlong - 1);
+        int kstart = lpre[k], kend = lpre[k + 1];
+        int hk = heads[s_long[k]];
 #pragma unroll
         for (int f = 0; f < STAGE_F4; ++f) {
-            const int e = e0 + f * EPF;
+            const int e = e0 + f;
             if (e < E) {
-                if (f) k = seg_of(e, k, min(nlong - 1, k + EPF / (LONG_SEG + 1) + 1));
-                const int ki = heads[s_long[k]] + (e - lpre[k]);
-                raw[f] = src.fetch(key_lo(keys[ki]), sub);
+                if (e >= kend) {
+                    ++k;
+                    kstart = kend;
+                    kend = lpre[k + 1];
+                    hk = heads[s_long[k]];
+                }
+                raw[f] = src.fetch(key_lo(keys[hk + (e - kstart)]), sub);
             }
         }
     };
@@ -955,10 +971,25 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
     fetch(0);
     int par = 0;
     for (int c0 = 0; c0 < E; c0 += CE, par ^= 1) {
+        {  // dim-major stage[dim * SP + entry]: the lane group's 8 consecutive entries of each
+           // of its 4 dims go out as two 16-B writes per dim (transposed in registers)
+            static_assert(STAGE_F4 == 8, "two float4 per dim row");
+            const int el0 = (threadIdx.x / LPR) * STAGE_F4;
+            float4 v[STAGE_F4];
 #pragma unroll
-        for (int f = 0; f < STAGE_F4; ++f) {
-            const int q = threadIdx.x + f * TWG;  // float4 slot = entry * LPR + sub
-            if (c0 + q / LPR < E) reinterpret_cast<float4*>(L.stage)[q] = src.finish(raw[f]);
+            for (int f = 0; f < STAGE_F4; ++f)
+                v[f] = c0 + el0 + f < E ? src.finish(raw[f]) : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c0 + el0 < E) {
+                float* base = L.stage + (4 * sub) * SP + el0;
+                *reinterpret_cast<float4*>(base) = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
+                *reinterpret_cast<float4*>(base + 4) = make_float4(v[4].x, v[5].x, v[6].x, v[7].x);
+                *reinterpret_cast<float4*>(base + SP) = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
+                *reinterpret_cast<float4*>(base + SP + 4) = make_float4(v[4].y, v[5].y, v[6].y, v[7].y);
+                *reinterpret_cast<float4*>(base + 2 * SP) = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
+                *reinterpret_cast<float4*>(base + 2 * SP + 4) = make_float4(v[4].z, v[5].z, v[6].z, v[7].z);
+                *reinterpret_cast<float4*>(base + 3 * SP) = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
+                *reinterpret_cast<float4*>(base + 3 * SP + 4) = make_float4(v[4].w, v[5].w, v[6].w, v[7].w);
+            }
         }
         __syncthreads();
         if (c0 == 0) DIAG_T(9);
@@ -977,27 +1008,64 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
 #pragma unroll
                 for (int d = 0; d < NDL; ++d) acc[d] = L.carry[(par ^ 1) * 256 + lig + GD * d];
             }
-            const float* sp = L.stage + (a0 - c0) * D + lig;
-            const int len = a1 - a0;
+            // the piece's entries of this lane's dims: col[d][e0 + j], j < len
+            const int e0 = a0 - c0, len = a1 - a0;
+            const float* col[NDL];
+#pragma unroll
+            for (int d = 0; d < NDL; ++d) col[d] = L.stage + (lig + GD * d) * SP + e0;
+            auto op = [&](float x, float y) { return OP == OP_FMA ? fmaf(y, nlr, x) : x + y; };
             int j = 0;
-            for (; j + 8 <= len; j += 8) {
-                float v[8][NDL];
+            if (OP == OP_SUM && first && len > 0) {  // peel: the chain below is adds only
 #pragma unroll
-                for (int c = 0; c < 8; ++c)
+                for (int d = 0; d < NDL; ++d) acc[d] = col[d][0];
+                j = 1;
+            }
+            for (; j < len && ((e0 + j) & 3); ++j)  // up to a 16-B boundary
 #pragma unroll
-                    for (int d = 0; d < NDL; ++d) v[c][d] = sp[(j + c) * D + GD * d];
+                for (int d = 0; d < NDL; ++d) acc[d] = op(acc[d], col[d][j]);
+            // strictly ordered chain over 4-entry float4 reads; the next VB float4s per dim
+            // are in flight while the current ones are added (ping-pong, no copies)
+            constexpr int VB = NDL >= 4 ? 1 : 4 / NDL;
+            constexpr int BE = 4 * VB;  // entries per batch
+            float4 xa[VB][NDL], xb[VB][NDL];
+            auto loadb = [&](float4 (&x)[VB][NDL], int jj) {
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
+                for (int v = 0; v < VB; ++v)
 #pragma unroll
-                    for (int d = 0; d < NDL; ++d) acc[d] = combine1<OP>(acc[d], v[c][d], first, nlr);
-                    first = false;
+                    for (int d = 0; d < NDL; ++d) x[v][d] = *reinterpret_cast<const float4*>(col[d] + jj + 4 * v);
+            };
+            auto addb = [&](const float4 (&x)[VB][NDL]) {
+#pragma unroll
+                for (int v = 0; v < VB; ++v)
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d)
+                        acc[d] = op(op(op(op(acc[d], x[v][d].x), x[v][d].y), x[v][d].z), x[v][d].w);
+            };
+            if (j + BE <= len) {
+                loadb(xa, j);
+                while (true) {
+                    const bool m1 = j + 2 * BE <= len;
+                    if (m1) loadb(xb, j + BE);
+                    addb(xa);
+                    j += BE;
+                    if (!m1) break;
+                    const bool m2 = j + 2 * BE <= len;
+                    if (m2) loadb(xa, j + BE);
+                    addb(xb);
+                    j += BE;
+                    if (!m2) break;
                 }
             }
-            for (; j < len; ++j) {
+            for (; j + 4 <= len; j += 4) {
 #pragma unroll
-                for (int d = 0; d < NDL; ++d) acc[d] = combine1<OP>(acc[d], sp[j * D + GD * d], first, nlr);
-                first = false;
+                for (int d = 0; d < NDL; ++d) {
+                    const float4 x = *reinterpret_cast<const float4*>(col[d] + j);
+                    acc[d] = op(op(op(op(acc[d], x.x), x.y), x.z), x.w);
+                }
             }
+            for (; j < len; ++j)
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) acc[d] = op(acc[d], col[d][j]);
             if (se <= c0 + ce) {
                 fend(u, i, lig, acc);
             } else {
@@ -1183,8 +1251,25 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
 template <class Visit>
 DQRM_INLINE void visit_slot_lookups(const int64_t* off, const int64_t* idx, int64_t B, int64_t L,
                                     int64_t nrows, int64_t b0, int64_t b1, bool report, uint32_t* err,
-                                    Visit&& visit) {
+                                    bool pool1, Visit&& visit) {
     constexpr int GB = 8;
+    if (pool1 && L == B) {  // Criteo form: bag b = lookup b, no offsets round trip
+        for (int64_t bs = b0; bs < b1; bs += GB) {
+            int64_t r[GB];
+#pragma unroll
+            for (int k = 0; k < GB; ++k) r[k] = bs + k < b1 ? idx[bs + k] : -1;
+#pragma unroll
+            for (int k = 0; k < GB; ++k) {
+                if (bs + k >= b1) continue;
+                if (r[k] < 0 || r[k] >= nrows) {
+                    if (report) flag_error(err, DQRM_ERRF_INDEX);
+                    continue;
+                }
+                visit(r[k], bs + k);
+            }
+        }
+        return;
+    }
     for (int64_t bs = b0; bs < b1; bs += GB) {
         int64_t o[GB + 1];
 #pragma unroll
@@ -1223,7 +1308,7 @@ DQRM_INLINE void visit_slot_lookups(const int64_t* off, const int64_t* idx, int6
 
 DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* idx, const int64_t* off,
                                    const int64_t* idx_base, int64_t B, int t, int64_t nrows,
-                                   int64_t r0, int64_t r1, bool report, uint32_t* err) {
+                                   int64_t r0, int64_t r1, bool report, uint32_t* err, bool pool1) {
     const int64_t ib = idx_base[t];
     const int64_t L = idx_base[t + 1] - ib;
     const int64_t* __restrict__ toff = off + (int64_t)t * B;
@@ -1234,7 +1319,7 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
     constexpr int RC = 8;  // matches kept in registers (pass 2 re-reads only past RC)
     uint64_t cache[RC];
     int cnt = 0;
-    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err, [&](int64_t r, int64_t b) {
+    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err, pool1, [&](int64_t r, int64_t b) {
         if (r >= r0 && r < r1) {
             const uint64_t key = ((uint64_t)r << 32) | (uint64_t)b;
 #pragma unroll
@@ -1268,7 +1353,7 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
         for (int c = 0; c < RC; ++c)
             if (c < cnt) keys[pos + c] = cache[c];
     } else {
-        visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, false, err, [&](int64_t r, int64_t b) {
+        visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, false, err, pool1, [&](int64_t r, int64_t b) {
             if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
         });
     }
@@ -1277,6 +1362,7 @@ DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* i
 }
 
 struct BwdArgs {
+    int pool1;  // DQRM_BATCH_POOLING_ONE
     float* W;
     uint8_t* packed;
     float* rowmax;
@@ -1489,7 +1575,7 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     DIAG_T(0);
 
     const int n = gather_lookup_keys(sl.keys, s_wsum, a.idx, a.off, a.idx_base, a.B, t, nrows, r0, r1, s == 0,
-                                     a.err);
+                                     a.err, a.pool1 != 0);
     if (n < 0) {
         if (MODE == 1 && threadIdx.x == 0) {
             if (off4 == 0) a.ws_ucount[own] = 0;
@@ -2046,6 +2132,7 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, u
     a.W = set->W; a.packed = set->packed; a.tmax = set->tmax; a.scale = set->scale;
     a.meta = set->meta; a.err = set->err;
     a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base;
+    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
     a.out = out; a.B = batch->num_bags; a.ost_t = out_stride_t; a.ost_b = out_stride_b;
     a.T = set->num_tables; a.bits = bits; a.flags = flags;
     hipStream_t st = (hipStream_t)stream;
@@ -2104,6 +2191,7 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.scale = set->scale; a.pscale = set->pscale;
     a.meta = set->meta; a.err = set->err;
     a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
+    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
     a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
     a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4;
     hipStream_t st = (hipStream_t)stream;
@@ -2152,6 +2240,7 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
     memset(&a, 0, sizeof(a));
     a.W = set->W; a.scale = set->scale; a.meta = set->meta; a.err = set->err;
     a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
+    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
     a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables; a.ste = ste;
     a.ws_cap_base = ws_cap_base; a.ws_rows = ws_rows; a.ws_vals = ws_vals; a.ws_ucount = ws_ucount;
     a.ws_absmax = ws_absmax;

@@ -50,7 +50,9 @@ class LookupBatch:
     Offsets are nn.EmbeddingBag offsets (bag b = [off[b], off[b+1]), last bag ends at L_t).
     """
 
-    def __init__(self, indices, offsets, device: torch.device | str | None = None):
+    def __init__(self, indices, offsets, device: torch.device | str | None = None, pooling_one: bool = False):
+        """pooling_one: promise that every table has one lookup per bag (offsets = arange(B),
+        the Criteo collate form) -- the kernels then skip reading the offsets."""
         if isinstance(indices, torch.Tensor):
             if indices.dim() != 2:
                 raise ValueError("stacked indices must be [T, L]")
@@ -84,8 +86,12 @@ class LookupBatch:
         self.idx = idx.to(device=dev, dtype=torch.int64).contiguous()
         self.off = off.to(device=dev, dtype=torch.int64).contiguous()
         self.idx_base = torch.tensor(base, dtype=torch.int64, device=dev)
+        if pooling_one and any(n != self.num_bags for n in lens):
+            raise ValueError("pooling_one needs exactly one lookup per bag in every table")
+        self.pooling_one = bool(pooling_one)
         self._c = L.Batch(
-            _ptr(self.idx), _ptr(self.off), _ptr(self.idx_base), self.num_bags, self.max_lookups
+            _ptr(self.idx), _ptr(self.off), _ptr(self.idx_base), self.num_bags, self.max_lookups,
+            L.DQRM_BATCH_POOLING_ONE if pooling_one else 0, 0,
         )
 
     @property
@@ -97,7 +103,7 @@ class LookupBatch:
         """Criteo form: one index per (table, sample); offsets = arange(B) per table."""
         T, B = indices.shape
         off = torch.arange(B, dtype=torch.int64, device=indices.device).expand(T, B)
-        return cls(indices, off.contiguous())
+        return cls(indices, off.contiguous(), pooling_one=True)
 
 
 class EmbeddingTableSet:

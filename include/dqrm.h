@@ -100,7 +100,14 @@ typedef struct dqrm_batch {
     const int64_t* idx_base;
     int64_t  num_bags;        /* B */
     int64_t  max_lookups;     /* host upper bound on any L_t (capacity planning) */
+    uint32_t flags;           /* DQRM_BATCH_* */
+    uint32_t reserved;
 } dqrm_batch;
+
+/* Criteo form (dlrm_data_pytorch.py:328-345): every table has L_t == B and
+ * off[t][b] == b, i.e. bag b is lookup b. The kernels then skip the offsets round trip
+ * (a table whose L_t != B is still read through its offsets). */
+#define DQRM_BATCH_POOLING_ONE 1u
 
 /* forward flags */
 #define DQRM_FWD_REFRESH_SCALE 1u  /* s_t = clamp(tmax_t, 1e-8)/(2^(bits-1)-1), write scale[] */

@@ -43,7 +43,7 @@ def test_payload_bytes_agree(lib):
 def test_struct_layouts():
     # dqrm_table_set: 2 x i32 + 3 x i64 + 12 pointers; dqrm_batch: 3 pointers + 2 x i64
     assert C.sizeof(L.TableSet) == 8 + 24 + 12 * 8
-    assert C.sizeof(L.Batch) == 5 * 8
+    assert C.sizeof(L.Batch) == 6 * 8
 
 
 def test_invalid_arguments_rejected_without_device(lib):

@@ -389,3 +389,24 @@ def test_exchange_many_ranks_long_segments(dq, grad_bits):
     assert ts.read_errors() == 0
     for t in range(len(rows)):
         np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Ws[t])
+
+
+def test_pooling_one_flag_matches_offsets_path(dq):
+    """DQRM_BATCH_POOLING_ONE (offsets not read) gives the same forward, SGD and coalesce as
+    the general offsets path on the same Criteo-form batch."""
+    rows, D = [5, 3000, 200000], 64
+    Ws = G.table_weights(rows, D, 71)
+    P = torch.from_numpy(G.pooling_one(rows, 2048, 72, dist="zipf")).cuda()
+    dy = torch.from_numpy(G.upstream_grad(len(rows), 2048, D, 73)).cuda()
+    off = torch.arange(2048, device="cuda").expand(len(rows), 2048).contiguous()
+    outs = []
+    for b in (dq.LookupBatch.pooling_one(P), dq.LookupBatch(P, off)):
+        assert b.c.flags == (1 if b.pooling_one else 0)
+        ts = make_set(dq, Ws)
+        y = ts.forward(b)
+        ws = dq.CoalescedGrad.allocate(rows, 2048, D, "cuda")
+        ts.backward_coalesce(b, dy, ws)
+        ts.backward_sgd(b, dy, lr=0.1)
+        outs.append((y.clone(), ws.vals.clone(), ws.rows.clone(), ts.W.clone()))
+    for x, z in zip(*outs):
+        assert torch.equal(x, z)
