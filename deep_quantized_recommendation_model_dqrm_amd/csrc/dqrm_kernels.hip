@@ -844,6 +844,7 @@ DQRM_INLINE void short_segments(const uint64_t* keys, const uint16_t* heads, int
                 r[b] = src.fetch(key_lo(keys[ii[b]]), sub);
             }
         }
+        if (u0 == ubeg + grp) DIAG_T(11);  // first batch: loads issued
 #pragma unroll
         for (int b = 0; b < SB; ++b) {
             if (!ll[b]) continue;
@@ -859,10 +860,13 @@ DQRM_INLINE void short_segments(const uint64_t* keys, const uint16_t* heads, int
                     if (j + c < ll[b]) st[b].acc = combine<OP>(st[b].acc, src.finish(q[c]), first, nlr);
             }
         }
+        if (u0 == ubeg + grp) DIAG_T(12);  // first batch combined (its loads have landed)
 #pragma unroll
         for (int b = 0; b < SB; ++b)
             if (ll[b]) ffin(u0 + b * NGRP, ii[b], sub, st[b]);
+        if (u0 == ubeg + grp) DIAG_T(13);  // first batch's stores issued
     }
+    DIAG_T(14);
 }
 
 // ordered compaction of the long segments' indices u into s_long (ballots); returns their number
@@ -876,6 +880,7 @@ DQRM_INLINE int compact_long(const uint16_t* heads, int U, int n, uint16_t* s_lo
     for (int k = 0; k < kpl; ++k) c += __popcll(__ballot(is_long(u0 + k * WAVE)));
     if (lane == 0) s_wsum[w] = c;
     __syncthreads();
+    DIAG_T(15);  // every thread's short work done and its stores drained
     int run = 0, total = 0;
     for (int k = 0; k < TWG / WAVE; ++k) { const int x = s_wsum[k]; run += k < w ? x : 0; total += x; }
     for (int k = 0; k < kpl; ++k) {

@@ -47,7 +47,10 @@ def report(name):
         print(f"t{t:2d} n={rows[t]:>10d} slot{s}: " + " ".join(f"{x / 100:6.1f}" for x in ph) +
               f" | {(p[5] - k0) / 100:6.1f}   (sort {(p[6] - p[1]) / 100:4.1f} heads {(p[2] - p[6]) / 100:4.1f})" +
               (f" long: prefix {(p[8] - p[3]) / 100:4.1f} fetch+stage {(p[9] - p[8]) / 100:4.1f} "
-               f"reduce0 {(p[10] - p[9]) / 100:4.1f} rest {(p[4] - p[10]) / 100:4.1f}" if p[4] - p[3] > 200 else ""))
+               f"reduce0 {(p[10] - p[9]) / 100:4.1f} rest {(p[4] - p[10]) / 100:4.1f}" if p[4] - p[3] > 200 else "") +
+              (f" short: issue {(p[11] - p[2]) / 100:4.1f} land {(p[12] - p[11]) / 100:4.1f} "
+               f"store {(p[13] - p[12]) / 100:4.1f} loop {(p[14] - p[13]) / 100:4.1f} drain {(p[15] - p[14]) / 100:4.1f}"
+               if p[11] > p[2] > 0 else ""))
 
 
 for _ in range(3):
