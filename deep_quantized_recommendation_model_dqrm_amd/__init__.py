@@ -4,6 +4,7 @@ Drop-in for the reference's hot path (YangZhou08/Deep_Quantized_Recommendation_M
   * ``quant_modules_not_quantize_grad.QuantEmbeddingBagTwo``  (INT4 fake-quant EmbeddingBag)
   * ``sgd_quantized_gradients_parallel_comm`` hooks            (INT8 sparse-grad all-reduce + SGD)
   * ``sgd_quantized_gradients`` simulated-DP buffer helpers
+  * ``quantized_ops.ops.quantized.embedding_bag_{4bit,byte}_*``  (row-wise PTQ inference formats)
 backed by hand-written HIP kernels behind the C ABI in ``include/dqrm.h`` (libdqrm.so).
 """
 from . import _lib
@@ -12,6 +13,7 @@ from .tables import CoalescedGrad, EmbeddingTableSet, LookupBatch, default_caps,
 from .comm import SparseGradExchange, get_my_slice, payload_bytes
 from . import quant_modules_not_quantize_grad, sgd_quantized_gradients, sgd_quantized_gradients_parallel_comm
 from .quant_modules_not_quantize_grad import QuantEmbeddingBagCollection, QuantEmbeddingBagTwo
+from . import quantized_ops
 
 __all__ = [
     "LIB_PATH",
@@ -30,4 +32,5 @@ __all__ = [
     "quant_modules_not_quantize_grad",
     "sgd_quantized_gradients",
     "sgd_quantized_gradients_parallel_comm",
+    "quantized_ops",
 ]

@@ -47,6 +47,9 @@ EXPORTED_SYMBOLS = (
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
     "dqrm_apply_sparse_update",
+    "dqrm_rowwise_row_bytes",
+    "dqrm_rowwise_prepack",
+    "dqrm_rowwise_bag",
     "dqrm_init_uniform",
     "dqrm_read_errors",
     "dqrm_last_error",
@@ -135,6 +138,12 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_apply_sparse_update": (
             C.c_int,
             [TS, P, C.c_int64, P, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
+        ),
+        "dqrm_rowwise_row_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+        "dqrm_rowwise_prepack": (C.c_int, [C.c_int, P, C.c_int64, C.c_int, P, P]),
+        "dqrm_rowwise_bag": (
+            C.c_int,
+            [C.c_int, P, C.c_int64, C.c_int, P, C.c_int64, P, C.c_int64, C.c_int, P, P, P, P],
         ),
         "dqrm_init_uniform": (C.c_int, [TS, C.c_uint64, P]),
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),

@@ -1981,6 +1981,146 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Row-wise PTQ formats of the reference's inference path:
+//   prepack   torch.ops.quantized.embedding_bag_{4bit,byte}_prepack
+//             (DLRM_Net.quantize_embedding, dlrm_s_pytorch_single_gpu_documentingp.py:689-704)
+//   gather    torch.ops.quantized.embedding_bag_{4bit,byte}_rowwise_offsets, mode sum
+//             (DLRM_Net.apply_emb, dlrm_s_pytorch_single_gpu_documentingp.py:648-663)
+// Row layout (FBGEMM fused row-wise): 4-bit: D/2 nibble bytes (element 2j in the low
+// nibble), fp16 scale, fp16 bias; 8-bit: D bytes, f32 scale, f32 bias. A row's scale and
+// bias are read once per lookup next to its payload; G = D/8 lanes per row, 8 dims per lane.
+// ------------------------------------------------------------------------------------
+__host__ __device__ inline int rowwise_row_bytes(int bits, int D) { return bits == 4 ? D / 2 + 4 : D + 8; }
+
+template <int G>
+DQRM_INLINE float group_min(float v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+
+template <int G>
+DQRM_INLINE float group_fmax(float v) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+
+template <int BITS, int G>
+__global__ void __launch_bounds__(256) k_rowwise_prepack(const float* __restrict__ W, int64_t n,
+                                                         uint8_t* __restrict__ out) {
+    constexpr int D = G * 8;
+    constexpr int RB = BITS == 4 ? D / 2 + 4 : D + 8;
+    const int lane = threadIdx.x % G;
+    const int64_t rows_per_pass = (int64_t)gridDim.x * (256 / G);
+    for (int64_t r = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; r < n; r += rows_per_pass) {
+        const float4* src = reinterpret_cast<const float4*>(W + r * D) + lane * 2;
+        const float4 a = src[0], b = src[1];
+        float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        float mn = x[0], mx = x[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) { mn = fminf(mn, x[j]); mx = fmaxf(mx, x[j]); }
+        mn = group_min<G>(mn);
+        mx = group_fmax<G>(mx);
+        uint8_t* orow = out + r * RB;
+        if (BITS == 4) {  // FloatOrHalfToFusedNBitRowwiseQuantizedSBHalf, bit_rate 4
+            const _Float16 mn16 = (_Float16)mn;  // round-to-nearest-even
+            const float mnh = (float)mn16;
+            const float range = mx - mnh;
+            const float scale = range == 0.0f ? 1.0f : range / 15.0f;
+            _Float16 s16 = (_Float16)scale;
+            const float sh = (float)s16;
+            float inv = sh == 0.0f ? 1.0f : 1.0f / sh;
+            if (sh == 0.0f || isinf(inv)) { s16 = (_Float16)1.0f; inv = 1.0f; }
+            uint32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float q = fminf(fmaxf(rintf((x[j] - mnh) * inv), 0.0f), 15.0f);
+                word |= (uint32_t)q << (4 * j);
+            }
+            reinterpret_cast<uint32_t*>(orow)[lane] = word;
+            if (lane == 0)
+                reinterpret_cast<uint32_t*>(orow + D / 2)[0] =
+                    (uint32_t)__builtin_bit_cast(uint16_t, s16) | ((uint32_t)__builtin_bit_cast(uint16_t, mn16) << 16);
+        } else {          // FloatToFused8BitRowwiseQuantizedSBFloat
+            const float range = mx - mn;
+            const float scale = range / 255.0f;
+            const float inv = 255.0f / (range + 1e-8f);
+            uint2 words = make_uint2(0u, 0u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float q = fminf(fmaxf(rintf((x[j] - mn) * inv), 0.0f), 255.0f);
+                if (j < 4) words.x |= (uint32_t)q << (8 * j); else words.y |= (uint32_t)q << (8 * (j - 4));
+            }
+            reinterpret_cast<uint2*>(orow)[lane] = words;
+            if (lane == 0) reinterpret_cast<uint2*>(orow + D)[0] = make_uint2(__float_as_uint(scale), __float_as_uint(mn));
+        }
+    }
+}
+
+// EmbeddingSpMDM(NBit) reference semantics, mode sum: per lookup, in bag order,
+//   acc = fma(scale * w, q, acc + bias * w)     (w = per-sample weight, omitted when null)
+template <int BITS, int G>
+__global__ void __launch_bounds__(256) k_rowwise_bag(const uint8_t* __restrict__ packed, int64_t n,
+                                                     const int64_t* __restrict__ idx, int64_t L,
+                                                     const int64_t* __restrict__ off, int64_t B,
+                                                     const float* __restrict__ psw, int last_offset,
+                                                     float* __restrict__ out, uint32_t* __restrict__ err) {
+    constexpr int D = G * 8;
+    constexpr int RB = BITS == 4 ? D / 2 + 4 : D + 8;
+    const int lane = threadIdx.x % G;
+    const int64_t bags_per_pass = (int64_t)gridDim.x * (256 / G);
+    for (int64_t b = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G; b < B; b += bags_per_pass) {
+        int64_t s0 = off[b], s1 = (b + 1 < B || last_offset) ? off[b + 1] : L;
+        if (s0 < 0 || s1 > L || s1 < s0) {
+            if (lane == 0) flag_error(err, DQRM_ERRF_OFFSET);
+            s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+            s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+        }
+        float acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = 0.0f;
+        for (int64_t i = s0; i < s1; ++i) {
+            const int64_t r = idx[i];
+            if (r < 0 || r >= n) {
+                if (lane == 0) flag_error(err, DQRM_ERRF_INDEX);
+                continue;
+            }
+            const uint8_t* row = packed + r * RB;
+            float sc, bi;
+            uint32_t w0, w1 = 0;
+            if (BITS == 4) {
+                const uint32_t sb = *reinterpret_cast<const uint32_t*>(row + D / 2);
+                sc = (float)__builtin_bit_cast(_Float16, (uint16_t)(sb & 0xFFFFu));
+                bi = (float)__builtin_bit_cast(_Float16, (uint16_t)(sb >> 16));
+                w0 = reinterpret_cast<const uint32_t*>(row)[lane];
+            } else {
+                const uint2 sb = *reinterpret_cast<const uint2*>(row + D);
+                sc = __uint_as_float(sb.x);
+                bi = __uint_as_float(sb.y);
+                const uint2 w = reinterpret_cast<const uint2*>(row)[lane];
+                w0 = w.x;
+                w1 = w.y;
+            }
+            if (psw) {
+                const float wt = psw[i];
+                sc = sc * wt;
+                bi = bi * wt;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float q = BITS == 4 ? (float)((w0 >> (4 * j)) & 15u)
+                                          : (float)(((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 255u);
+                acc[j] = fmaf(sc, q, acc[j] + bi);
+            }
+        }
+        float4* o = reinterpret_cast<float4*>(out + b * D) + lane * 2;
+        o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // host helpers
 // ------------------------------------------------------------------------------------
 int check_set(const dqrm_table_set* s) {
@@ -2320,6 +2460,68 @@ int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void
     HIP_TRY(hipMemcpyAsync(flags, set->err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (clear) HIP_TRY(hipMemsetAsync(set->err, 0, sizeof(uint32_t), st));
+    return DQRM_OK;
+}
+
+
+// ---------------------------------------------------------------------------------
+// Row-wise PTQ formats
+// ---------------------------------------------------------------------------------
+#define DISPATCH_G(D, ...)                                                               \
+    switch ((D) % 8 ? 0 : (D) / 8) {                                                     \
+        case 1: { constexpr int G = 1; __VA_ARGS__; } break;                             \
+        case 2: { constexpr int G = 2; __VA_ARGS__; } break;                             \
+        case 4: { constexpr int G = 4; __VA_ARGS__; } break;                             \
+        case 8: { constexpr int G = 8; __VA_ARGS__; } break;                             \
+        case 16: { constexpr int G = 16; __VA_ARGS__; } break;                           \
+        case 32: { constexpr int G = 32; __VA_ARGS__; } break;                           \
+        default: return set_error(DQRM_E_INVALID, "dqrm rowwise: dim %d unsupported", (int)(D)); \
+    }
+
+size_t dqrm_rowwise_row_bytes(int bits, int dim) {
+    if ((bits != 4 && bits != 8) || dim < 8 || (dim & 7)) return 0;
+    return (size_t)rowwise_row_bytes(bits, dim);
+}
+
+int dqrm_rowwise_prepack(int bits, const float* W, int64_t num_rows, int dim, uint8_t* packed, void* stream) {
+    if (bits != 4 && bits != 8) return set_error(DQRM_E_INVALID, "dqrm_rowwise_prepack: bits must be 4 or 8");
+    if (!W || !packed || num_rows < 0) return set_error(DQRM_E_INVALID, "dqrm_rowwise_prepack: bad arguments");
+    if (((uintptr_t)W) & 15) return set_error(DQRM_E_INVALID, "dqrm_rowwise_prepack: W must be 16-byte aligned");
+    if (num_rows == 0) return DQRM_OK;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_G(dim, {
+        const int rows_per_wg = 256 / G;
+        const int grid = grid_for(num_rows, rows_per_wg, 65536);
+        if (bits == 4)
+            hipLaunchKernelGGL((k_rowwise_prepack<4, G>), dim3(grid), dim3(256), 0, st, W, num_rows, packed);
+        else
+            hipLaunchKernelGGL((k_rowwise_prepack<8, G>), dim3(grid), dim3(256), 0, st, W, num_rows, packed);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_rowwise_bag(int bits, const uint8_t* packed, int64_t num_rows, int dim, const int64_t* idx,
+                     int64_t num_lookups, const int64_t* off, int64_t num_bags, int include_last_offset,
+                     const float* per_sample_weights, float* out, uint32_t* err, void* stream) {
+    if (bits != 4 && bits != 8) return set_error(DQRM_E_INVALID, "dqrm_rowwise_bag: bits must be 4 or 8");
+    if (!packed || !off || !out || !err || (num_lookups > 0 && !idx) || num_rows < 0 || num_lookups < 0)
+        return set_error(DQRM_E_INVALID, "dqrm_rowwise_bag: bad arguments");
+    if (((uintptr_t)packed) & 3 || ((uintptr_t)out) & 15)
+        return set_error(DQRM_E_INVALID, "dqrm_rowwise_bag: packed must be 4-B and out 16-B aligned");
+    if (num_bags <= 0) return DQRM_OK;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_G(dim, {
+        const int bags_per_wg = 256 / G;
+        const int grid = grid_for(num_bags, bags_per_wg, 65536);
+        if (bits == 4)
+            hipLaunchKernelGGL((k_rowwise_bag<4, G>), dim3(grid), dim3(256), 0, st, packed, num_rows, idx,
+                               num_lookups, off, num_bags, per_sample_weights, include_last_offset, out, err);
+        else
+            hipLaunchKernelGGL((k_rowwise_bag<8, G>), dim3(grid), dim3(256), 0, st, packed, num_rows, idx,
+                               num_lookups, off, num_bags, per_sample_weights, include_last_offset, out, err);
+    });
+    LAUNCH_CHECK();
     return DQRM_OK;
 }
 

@@ -224,6 +224,35 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              int mode, int repack_bits, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Row-wise PTQ formats of the reference's inference path.
+ * DLRM_Net.quantize_embedding (dlrm_s_pytorch_single_gpu_documentingp.py:689-704) packs
+ * each trained table with torch.ops.quantized.embedding_bag_{4bit,byte}_prepack and
+ * apply_emb (:648-663) gathers with embedding_bag_{4bit,byte}_rowwise_offsets (mode sum,
+ * optional per-sample weights). Byte-identical to those ops (FBGEMM fused row-wise):
+ *   bits 4: row = D/2 bytes (element 2j low nibble, 2j+1 high) | fp16 scale | fp16 bias
+ *   bits 8: row = D bytes | f32 scale | f32 bias
+ * dim must be 8, 16, 32, 64, 128 or 256. W is 16-byte aligned, packed 4-byte aligned.
+ * ------------------------------------------------------------------------------ */
+/* Bytes per packed row (0 if bits/dim unsupported). */
+size_t dqrm_rowwise_row_bytes(int bits, int dim);
+
+/* packed[num_rows * row_bytes] <- prepack(W[num_rows, dim] f32).
+ * Replaces torch.ops.quantized.embedding_bag_4bit_prepack / embedding_bag_byte_prepack. */
+int dqrm_rowwise_prepack(int bits, const float* W, int64_t num_rows, int dim, uint8_t* packed,
+                         void* stream);
+
+/* out[num_bags, dim] f32 <- sum over bag b of dequant(packed[idx[i]]) (* per_sample_weights[i]),
+ * accumulated in bag order as acc = fma(scale*w, q, acc + bias*w) (FBGEMM EmbeddingSpMDM).
+ * Bag b covers idx[off[b] .. off[b+1]); with include_last_offset == 0 the last bag ends at
+ * num_lookups, otherwise off has num_bags+1 entries. per_sample_weights may be NULL. Out-of-range indices are
+ * skipped and flag DQRM_ERRF_INDEX in *err, bad offsets flag DQRM_ERRF_OFFSET (device
+ * word, cleared by the caller). Replaces torch.ops.quantized.embedding_bag_4bit_rowwise_offsets /
+ * embedding_bag_byte_rowwise_offsets (mode=0 sum). */
+int dqrm_rowwise_bag(int bits, const uint8_t* packed, int64_t num_rows, int dim, const int64_t* idx,
+                     int64_t num_lookups, const int64_t* off, int64_t num_bags, int include_last_offset,
+                     const float* per_sample_weights, float* out, uint32_t* err, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Misc
  * ------------------------------------------------------------------------------ */
 /* Synthetic on-device init U(-sqrt(1/n_t), +sqrt(1/n_t)) from a counter-based hash
