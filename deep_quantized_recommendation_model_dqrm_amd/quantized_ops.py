@@ -46,11 +46,16 @@ def _err_word(device: torch.device) -> torch.Tensor:
     return w
 
 
-def _cuda(t: torch.Tensor, device: torch.device | None = None) -> torch.Tensor:
+def _cuda(t: torch.Tensor, device: torch.device | None = None, dtype: torch.dtype | None = None) -> torch.Tensor:
+    """`t` on the GPU (`device`) as a contiguous flat-or-2D tensor of `dtype`; a no-op for
+    tensors already in that form (the common case on the serving path)."""
+    if t.is_cuda and (device is None or t.device == device) and (dtype is None or t.dtype == dtype) \
+            and t.is_contiguous():
+        return t
     if not torch.cuda.is_available():
         raise L.DQRMError("row-wise quantized embedding ops run on the GPU only (no CPU path)")
     dev = device if device is not None else (t.device if t.is_cuda else torch.device("cuda"))
-    return t.to(dev)
+    return t.to(device=dev, dtype=dtype or t.dtype).contiguous()
 
 
 def _prepack(weight: torch.Tensor, bits: int) -> torch.Tensor:
@@ -60,7 +65,7 @@ def _prepack(weight: torch.Tensor, bits: int) -> torch.Tensor:
     if D not in SUPPORTED_DIMS:
         raise ValueError(f"embedding dim {D} unsupported (built for {SUPPORTED_DIMS})")
     lib = L.load()
-    w = _cuda(weight.detach()).to(torch.float32).contiguous()
+    w = _cuda(weight.detach(), dtype=torch.float32)
     rb = int(lib.dqrm_rowwise_row_bytes(bits, D))
     out = torch.empty((n, rb), dtype=torch.uint8, device=w.device)
     with torch.cuda.device(w.device):
@@ -94,34 +99,36 @@ def _rowwise_offsets(bits, weight, indices, offsets, scale_grad_by_freq, mode, p
     if D not in SUPPORTED_DIMS:
         raise ValueError(f"packed row of {rb} bytes does not match a supported {bits}-bit dim")
     dev = weight.device
-    idx = _cuda(indices, dev).to(torch.int64).contiguous().view(-1)
-    off = _cuda(offsets, dev).to(torch.int64).contiguous().view(-1)
+    idx = _cuda(indices, dev, torch.int64)
+    off = _cuda(offsets, dev, torch.int64)
+    if idx.dim() != 1 or off.dim() != 1:
+        raise ValueError("indices and offsets must be 1-D")
     B = off.numel() - (1 if include_last_offset else 0)
     if B < 0:
         raise ValueError("include_last_offset needs at least one offset")
     psw = None
     if per_sample_weights is not None:
-        psw = _cuda(per_sample_weights, dev).to(torch.float32).contiguous().view(-1)
+        psw = _cuda(per_sample_weights, dev, torch.float32)
         if psw.numel() != idx.numel():
             raise ValueError("per_sample_weights must have one weight per index")
     out = torch.empty((B, D), dtype=torch.float32, device=dev)
     lib = L.load()
     err = _err_word(dev)
-    with torch.cuda.device(dev):
-        L.check(
-            lib.dqrm_rowwise_bag(bits, weight.data_ptr(), n, D, idx.data_ptr() if idx.numel() else None,
-                                 idx.numel(), off.data_ptr(), B, int(bool(include_last_offset)),
-                                 psw.data_ptr() if psw is not None else None, out.data_ptr(), err.data_ptr(),
-                                 _stream_handle()),
-            "dqrm_rowwise_bag",
-        )
-        if check:
-            flags = int(err.item())
-            if flags:
-                err.zero_()
-                if flags & L.DQRM_ERRF_INDEX:
-                    raise IndexError(f"embedding_bag: an index is out of range [0, {n})")
-                raise ValueError("embedding_bag: offsets must be non-decreasing and within [0, len(indices)]")
+    L.check(
+        lib.dqrm_rowwise_bag(bits, weight.data_ptr(), n, D, idx.data_ptr() if idx.numel() else None,
+                             idx.numel(), off.data_ptr(), B, int(bool(include_last_offset)),
+                             psw.data_ptr() if psw is not None else None, out.data_ptr(), err.data_ptr(),
+                             _stream_handle() if dev.index == torch.cuda.current_device()
+                             else torch.cuda.current_stream(dev).cuda_stream),
+        "dqrm_rowwise_bag",
+    )
+    if check:
+        flags = int(err.item())
+        if flags:
+            err.zero_()
+            if flags & L.DQRM_ERRF_INDEX:
+                raise IndexError(f"embedding_bag: an index is out of range [0, {n})")
+            raise ValueError("embedding_bag: offsets must be non-decreasing and within [0, len(indices)]")
     return out
 
 

@@ -187,3 +187,39 @@ def test_simulated_dp_module_api(dq):
         b_rows = np.array(sorted(buf), dtype=np.int64)
         O.simulated_dp_apply(Wo[t], b_rows, np.stack([buf[r] for r in b_rows.tolist()]), s, N, 0.1)
         np.testing.assert_array_equal(model.emb_l.table_weight(t).detach().cpu().numpy(), Wo[t])
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_periodic_scale_refresh(dq, packed):
+    """The period counters of q_m_n_q_g.py:303-315,354-363 (bound = P after the first
+    refresh): the scale is recomputed at training calls 1, P+2, 2P+3, ... and frozen in
+    between, while fused SGD keeps moving W (and, on the packed-INT4 path, repacks touched
+    rows with the frozen scale). Pooling one, so the packed and FP32 forwards agree."""
+    n, D, B, P, steps = 2000, 16, 256, 3, 9
+    W = G.table_weights([n], D, 51)[0]
+    m = _qebt(n, D, W, grad_mode="fused_sgd", lr=0.2, scale_period=P, use_packed_int4=packed)
+    Wo = W.copy()
+    s = None
+    now = bound = nt = 0
+    off = torch.arange(B, device="cuda")
+    for k in range(steps):
+        due = now == bound  # reference counter update
+        if due:
+            nt, now = nt + 1, 0
+            if nt == 1 and bound == 0:
+                bound += P
+        else:
+            nt, now = nt + 1, now + 1
+        if due:
+            s = O.table_scale(Wo, 4)
+        Pk = G.pooling_one([n], B, 60 + k, dist="zipf")[0]
+        y = m(torch.from_numpy(Pk).cuda(), off)
+        y_o, _ = O.emb_fwd(Wo, Pk, np.arange(B), s)
+        np.testing.assert_array_equal(y.detach().cpu().numpy(), y_o, err_msg=f"step {k}")
+        assert m.eb_scaling_factor.item() == s
+        assert (m.now_iteration.item(), m.iteration_bound.item(), m.iteration_nt.item()) == (now, bound, nt)
+        dy = G.upstream_grad(1, B, D, 70 + k)[0] * f32(40.0)  # large enough to move the table max
+        y.backward(torch.from_numpy(dy).cuda())
+        O.emb_bwd_sgd(Wo, Pk, np.arange(B), dy, s, 0.2)
+    np.testing.assert_array_equal(m.embedding_bag.weight.detach().cpu().numpy(), Wo)
+    assert O.table_scale(Wo, 4) != s, "the table max should have moved while the scale was frozen"
