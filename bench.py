@@ -43,6 +43,14 @@ CONFIGS = {
     # BASELINE.json configs[2-3]: Criteo-Kaggle, D=16
     "kaggle": dict(rows=G.KAGGLE_ROWS, dim=16),
 }
+# the reference scripts' MLPs (bash_scripts/): Kaggle --arch-mlp-bot=13-512-256-64-16
+# --arch-mlp-top=512-256-1; Terabyte 13-512-256-64 / 512-512-256-1; the top MLP's input is
+# D + T(T+1)/2 (dot interaction of T+1 vectors, dlrm_s_pytorch_single_gpu.py create_mlp)
+MLPS = {
+    "terabyte": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
+    "terabyte_ref": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
+    "kaggle": ([13, 512, 256, 64, 16], [16 + 351, 512, 256, 1]),
+}
 
 
 def parse():
@@ -60,6 +68,8 @@ def parse():
     p.add_argument("--gather-batch", type=int, default=65536,
                    help="bags per table for the INT4 packed-gather bandwidth phase (0 = skip)")
     p.add_argument("--gather-iters", type=int, default=50)
+    p.add_argument("--mlp-iters", type=int, default=50,
+                   help="iterations of the MLP INT8 gradient exchange phase (0 = skip)")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--seed", type=int, default=123)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -251,6 +261,8 @@ def main():
                   "bytes_per_lookup": D // 2 + 8 + 8 + D * 4}
         del yg, gb
 
+    mlp = dense_phase(a, dev, world, rank) if a.mlp_iters > 0 else None
+
     cpu = None
     if rank == 0 and a.cpu_baseline:
         cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
@@ -299,6 +311,7 @@ def main():
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "kernels_ms_note": "untimed breakdown pass, every kernel bracketed by events",
             "int4_gather": gather,
+            "mlp_grad_exchange": mlp,
             "cpu_baseline": cpu,
             "device_errors": err,
             "replicas_bit_identical": replicas_match,
@@ -308,6 +321,50 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def dense_phase(a, dev, world, rank):
+    """MLP half of the DP step, outside the timed embedding step:
+    per-channel INT8 quantize of every bot_l/top_l gradient, scale all-gather, fp16-wire
+    all-reduce (RCCL at N>1), decode, SGD update -- DenseGradExchange.exchange + apply.
+    Algorithmic bytes per step (P params, w wire bytes/elem): 4P (scale) + 4P + wP (quant)
+    + wP + 4P (decode) + 12P (update)."""
+    from deep_quantized_recommendation_model_dqrm_amd.dense import DenseGradExchange
+
+    bot, top = MLPS[a.config]
+    g = torch.Generator(device=dev).manual_seed(a.seed + 101 * rank)
+    layers = []
+    for dims in (bot, top):
+        for i, o in zip(dims[:-1], dims[1:]):
+            l = torch.nn.Linear(i, o).to(dev)
+            l.weight.grad = torch.randn(o, i, device=dev, generator=g) * 1e-3
+            l.bias.grad = torch.randn(o, device=dev, generator=g) * 1e-3
+            layers.append(l)
+    ex = DenseGradExchange(layers, grad_bits=8)
+    P = ex.channels.total_elems
+    wire_b = ex.wire.element_size()
+    with torch.no_grad():
+        for _ in range(5):
+            ex.exchange()
+            ex.apply(1e-6)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev = timed_events(a.mlp_iters)
+        for i in range(a.mlp_iters):
+            ev[i][0].record()
+            ex.exchange()
+            ex.apply(1e-6)
+            ev[i][1].record()
+        torch.cuda.synchronize()
+    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in ev]))
+    # scale: read g; quant: read g, write wire; decode: read wire, write g; update: read g, p, write p
+    alg = P * 4 + (P * 4 + P * wire_b) + (P * wire_b + P * 4) + 3 * P * 4
+    return {"layers": f"bot {'-'.join(map(str, bot))}, top {'-'.join(map(str, top))}", "params": P,
+            "channels": ex.channels.num_channels, "wire": str(ex.wire.dtype).replace("torch.", ""),
+            "wire_bytes_per_rank": P * wire_b, "ms": round(ms, 4), "alg_bytes": alg,
+            "GBps": round(alg / (ms * 1e-3) / 1e9, 1), "launches": 4, "collectives": 2 if world > 1 else 0,
+            "note": "median of per-iteration HIP events; exchange+apply of all layers"}
 
 
 def cpu_baseline(rows, D, B, seed):

@@ -13,7 +13,8 @@ import sys
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-CSRC = os.path.join(PKG_DIR, "csrc", "dqrm_kernels.hip")
+CSRC_DIR = os.path.join(PKG_DIR, "csrc")
+SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_dense.hip")]
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
 LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
 
@@ -22,7 +23,6 @@ HIPCC_FLAGS = [
     "-O3",
     "-std=c++17",
     "-fPIC",
-    "-shared",
     # The reference's `1/s*x + 0`, `(g*s)/s` and `W + (-lr*v)` are separately rounded
     # operations; contraction would change bits. Intended FMAs are explicit fmaf().
     "-ffp-contract=off",
@@ -38,19 +38,36 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libdqrm)")
 
 
+def _obj(src: str) -> str:
+    return os.path.splitext(src)[0] + ".o"
+
+
+def _stale(out: str, deps) -> bool:
+    return not os.path.exists(out) or any(os.path.getmtime(p) > os.path.getmtime(out) for p in deps)
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in (CSRC, HEADER, __file__))
+    return _stale(LIB_PATH, [*SOURCES, HEADER, __file__])
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    """Compile csrc/dqrm_kernels.hip into libdqrm.so next to this file."""
+    """Compile csrc/*.hip (one object per translation unit, rebuilt when stale) and link
+    libdqrm.so next to this file."""
     if not force and not needs_build():
         return LIB_PATH
+    objs = []
+    for src in SOURCES:
+        obj = _obj(src)
+        if force or _stale(obj, [src, HEADER, __file__]):
+            tmp = obj + ".tmp.o"
+            cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-c", src, "-o", tmp]
+            if verbose:
+                print("[dqrm] " + " ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, obj)
+        objs.append(obj)
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), CSRC, "-o", tmp]
+    cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:
         print("[dqrm] " + " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -36,6 +36,10 @@ DQRM_UPD_DP = 0
 DQRM_UPD_SIMULATED = 1
 DQRM_UPD_FP32 = 2
 
+DQRM_WIRE_F16 = 1
+DQRM_WIRE_I32 = 2
+DQRM_WIRE_F32 = 3
+
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
     "dqrm_refresh_absmax",
@@ -47,6 +51,11 @@ EXPORTED_SYMBOLS = (
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
     "dqrm_apply_sparse_update",
+    "dqrm_dense_wire_type",
+    "dqrm_dense_grad_scale",
+    "dqrm_dense_grad_quant",
+    "dqrm_dense_grad_decode",
+    "dqrm_dense_update",
     "dqrm_rowwise_row_bytes",
     "dqrm_rowwise_prepack",
     "dqrm_rowwise_bag",
@@ -97,6 +106,20 @@ class Batch(C.Structure):
     ]
 
 
+class DenseSet(C.Structure):
+    """Mirror of ``dqrm_dense_set`` (include/dqrm.h)."""
+
+    _fields_ = [
+        ("num_channels", C.c_int32),
+        ("max_len", C.c_int32),
+        ("total_elems", C.c_int64),
+        ("grad", C.c_void_p),
+        ("param", C.c_void_p),
+        ("len", C.c_void_p),
+        ("wire_off", C.c_void_p),
+    ]
+
+
 class DQRMError(RuntimeError):
     pass
 
@@ -120,6 +143,7 @@ def load(path: str | None = None) -> C.CDLL:
     P = C.c_void_p
     TS = C.POINTER(TableSet)
     BA = C.POINTER(Batch)
+    DS = C.POINTER(DenseSet)
     sig = {
         "dqrm_refresh_absmax": (C.c_int, [TS, P]),
         "dqrm_refresh_scale_and_pack": (C.c_int, [TS, C.c_int, P]),
@@ -139,6 +163,11 @@ def load(path: str | None = None) -> C.CDLL:
             C.c_int,
             [TS, P, C.c_int64, P, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
         ),
+        "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
+        "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),
+        "dqrm_dense_grad_quant": (C.c_int, [DS, C.c_int, P, C.c_int, P, C.c_int, P, P]),
+        "dqrm_dense_grad_decode": (C.c_int, [DS, P, C.c_int, C.c_int, P]),
+        "dqrm_dense_update": (C.c_int, [DS, P, C.c_float, P]),
         "dqrm_rowwise_row_bytes": (C.c_size_t, [C.c_int, C.c_int]),
         "dqrm_rowwise_prepack": (C.c_int, [C.c_int, P, C.c_int64, C.c_int, P, P]),
         "dqrm_rowwise_bag": (

@@ -2201,6 +2201,11 @@ int dqrm_diag_clock_read(unsigned long long* host, int n) {
 #endif
 
 const char* dqrm_last_error(void) { return g_last_error; }
+
+// other translation units of libdqrm (dqrm_dense.hip) report through the same slot
+__attribute__((visibility("hidden"))) int dqrm_internal_set_error(int code, const char* msg) {
+    return set_error(code, "%s", msg);
+}
 int dqrm_abi_version(void) { return DQRM_ABI_VERSION; }
 
 int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream) {

@@ -14,10 +14,11 @@ the reference's 2 blocking Gloo collectives per table. Results per table are the
 reference's: the averaged scale lands in ``emb_scaling_factor`` and the update applied by
 ``weight_update_parallel_comm`` is W += -lr * ((sum_r q_r) * 1/N) * s  (integer sums exact).
 
-The MLP branch (QuantLinear / nn.Linear layers of bot_l, top_l) is dense PyTorch on the
-layers' own device -- it is not part of the accelerated path -- and
-follows quantize_linear_grad / quantize_bias_grad (s_q_g_p_c.py:892-961) op for op, with
-every layer's scales in one all-reduce and every layer's gradients in one all-reduce.
+The MLP branch (QuantLinear / nn.Linear layers of bot_l, top_l) runs
+quantize_linear_grad / quantize_bias_grad (s_q_g_p_c.py:892-961) for all layers as one
+channel table through libdqrm's dense kernels (dense.DenseGradExchange): one all-gather of
+the per-channel scales and one exact integer-valued fp16 all-reduce per step instead of 4
+blocking collectives per layer. The layers must live on the GPU (no CPU path).
 """
 from __future__ import annotations
 
@@ -27,6 +28,7 @@ from torch import nn
 
 from . import _lib as L
 from .comm import SparseGradExchange
+from .dense import DenseGradExchange
 from .quant_modules_not_quantize_grad import _QuantEmbeddingBase
 
 
@@ -58,38 +60,6 @@ def _detach_grad(g: torch.Tensor) -> None:
         g.detach_()
     else:
         g.requires_grad_(False)
-
-
-def _all_reduce_mean(tensors: list[torch.Tensor], n: int, group=None) -> None:
-    """dist.all_reduce(SUM) then mul_(1/n), for a list of same-device tensors in one call."""
-    if not tensors:
-        return
-    if _world(group) > 1:
-        flat = torch.cat([t.reshape(-1) for t in tensors])
-        dist.all_reduce(flat, dist.ReduceOp.SUM, group=group)
-        off = 0
-        for t in tensors:
-            k = t.numel()
-            t.copy_(flat[off: off + k].view_as(t))
-            off += k
-    for t in tensors:
-        t.mul_(1.0 / n)
-
-
-def _sym_quantize(x: torch.Tensor, scale: torch.Tensor, bits: int) -> torch.Tensor:
-    """SymmetricQuantFunction.forward (quant_utils.py:322-346 with linear_quantize :75-101):
-    round(1/scale * x + 0), clamped to [-2^(b-1), 2^(b-1)-1]; per-row scale for 2-D x."""
-    n = 2 ** (bits - 1) - 1
-    if x.dim() == 2 and (scale.dim() != 1 or scale.shape[0] != 1):
-        scale = scale.view(-1, 1)
-    else:
-        scale = scale.view(-1)
-    return torch.clamp(torch.round(1.0 / scale * x + 0.0), -n - 1, n)
-
-
-def _sym_scale(absmax: torch.Tensor, bits: int) -> torch.Tensor:
-    """symmetric_linear_quantization_params (quant_utils.py:196-220)."""
-    return torch.clamp(absmax, min=1e-8) / (2 ** (bits - 1) - 1)
 
 
 # ---------------------------------------------------------------------------- embedding branch
@@ -128,40 +98,33 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
         _mlp_grad_update(model, number_of_gpus, mlp_layer_quantized, group)
 
 
-def _mlp_grad_update(model, n: int, quantized: bool, group) -> None:
+def _mlp_exchange(model, n: int, quantized: bool, group) -> DenseGradExchange | None:
     layers = _linear_layers(model, "bot_l") + _linear_layers(model, "top_l")
     layers = [l for l in layers if l.weight.grad is not None]
-    for l in layers:
-        _detach_grad(l.weight.grad)
-        if l.bias is not None and l.bias.grad is not None:
-            _detach_grad(l.bias.grad)
-    if not quantized:  # :358-369 / :385-396
-        grads = [l.weight.grad for l in layers] + [l.bias.grad for l in layers
-                                                    if l.bias is not None and l.bias.grad is not None]
-        _all_reduce_mean(grads, n, group)
+    if not layers:
+        return None
+    bits = 8 if quantized else 32  # the reference hard-codes num_bits=8 (s_q_g_p_c.py:341,350)
+    key = (tuple(id(l) for l in layers), bits, id(group), _world(group))
+    ex = getattr(model, "_dqrm_dense_exchange", None)
+    if ex is None or ex[0] != key:
+        ex = (key, DenseGradExchange(layers, grad_bits=bits, group=group))
+        model._dqrm_dense_exchange = ex
+    return ex[1]
+
+
+def _mlp_grad_update(model, n: int, quantized: bool, group) -> None:
+    """MLP branch (s_q_g_p_c.py:337-409): quantize_linear_grad / quantize_bias_grad for
+    every layer, as one channel table (libdqrm dense kernels + 2 collectives)."""
+    if _world(group) != n:
+        raise ValueError(f"number_of_gpus={n} but the process group has {_world(group)} ranks")
+    ex = _mlp_exchange(model, n, quantized, group)
+    if ex is None:
         return
-    # quantize_linear_grad (per-channel, 8 bits) + quantize_bias_grad (:892-961)
-    scales = []
-    for l in layers:
-        g = l.weight.grad
-        w_min, _ = torch.min(g, dim=1)
-        w_max, _ = torch.max(g, dim=1)
-        scales.append(_sym_scale(torch.max(torch.stack([w_min.abs(), w_max.abs()], dim=1), dim=1)[0], 8))
-        b = l.bias.grad
-        scales.append(_sym_scale(torch.max(b.min().abs(), b.max().abs()), 8).reshape(1))
-    _all_reduce_mean(scales, n, group)
-    qs = []
-    for k, l in enumerate(layers):
-        qs.append(_sym_quantize(l.weight.grad, scales[2 * k], 8))
-        qs.append(_sym_quantize(l.bias.grad, scales[2 * k + 1], 8))
-    _all_reduce_mean(qs, n, group)
-    for k, l in enumerate(layers):
-        l.weight_scaling_factor = scales[2 * k]
-        l.weight.grad.zero_()
-        l.weight.grad.add_(qs[2 * k])
-        l.bias_scaling_factor = scales[2 * k + 1].view(())
-        l.bias.grad.zero_()
-        l.bias.grad.add_(qs[2 * k + 1])
+    for l in ex.channels.layers:
+        _detach_grad(l.weight.grad)
+        _detach_grad(l.bias.grad)
+    ex.exchange()
+    model._dqrm_dense_ready = ex
 
 
 def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embedding=True, num_gpus=1,
@@ -183,15 +146,12 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
                 mode = L.DQRM_UPD_DP if ready != 32 else L.DQRM_UPD_FP32
                 m._exchange.apply(lr, mode=mode, repack=m._use_packed(False))
             m._ready = None
-        for l in _linear_layers(model, "bot_l") + _linear_layers(model, "top_l"):
-            if l.weight.grad is None:
-                continue
-            if mlp_layer_quantized:
-                l.weight.data.add_(-lr * l.weight.grad * l.weight_scaling_factor.view(-1, 1))
-                l.bias.data.add_(-lr * l.bias.grad * l.bias_scaling_factor)
-            else:
-                l.weight.data.add_(-lr * l.weight.grad)
-                l.bias.data.add_(-lr * l.bias.grad)
+        ex = getattr(model, "_dqrm_dense_ready", None)
+        if ex is not None:  # MLP branch (:630-668), one libdqrm launch for all layers
+            if (ex.grad_bits != 32) != bool(mlp_layer_quantized):
+                raise ValueError("mlp_layer_quantized differs from the one used by grad_update_parallel_comm")
+            ex.apply(lr)
+            model._dqrm_dense_ready = None
 
 
 def clear_gradients(model) -> None:

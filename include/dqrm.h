@@ -224,6 +224,59 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              int mode, int repack_bits, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Dense (MLP) layer gradients, data-parallel:
+ *   quantize_linear_grad (per-channel) / quantize_bias_grad   s_q_g_p_c.py:892-961
+ *   MLP branch of grad_update_parallel_comm                   s_q_g_p_c.py:337-409
+ *   MLP branch of weight_update_parallel_comm                 s_q_g_p_c.py:630-668
+ * A dense set is C "channels" over the bot_l/top_l Linear layers: every weight row is a
+ * channel (per_channel=True, one scale per output feature) and every bias vector is one
+ * channel (one scale per bias). Channel c is len[c] contiguous floats at grad[c] (the
+ * layer's .grad) and param[c] (the layer's .data); its quantized values sit at
+ * [wire_off[c], +len[c]) of the wire buffer. The arrays are device arrays.
+ * Per step: scale -> all-gather of s_loc [C] -> quant -> all-reduce(SUM) of the wire ->
+ * decode (grad_update_parallel_comm) ; update (weight_update_parallel_comm).
+ * ------------------------------------------------------------------------------ */
+typedef struct dqrm_dense_set {
+    int32_t  num_channels;    /* C */
+    int32_t  max_len;         /* max_c len[c] (host-side hint) */
+    int64_t  total_elems;     /* wire elements = sum_c len[c] */
+    float* const*  grad;      /* [C] device pointers to each channel's gradient */
+    float* const*  param;     /* [C] device pointers to each channel's parameter */
+    const int32_t* len;       /* [C] */
+    const int64_t* wire_off;  /* [C] element offset of the channel in the wire */
+} dqrm_dense_set;
+
+/* wire element types of the quantized-gradient all-reduce */
+#define DQRM_WIRE_F16 1  /* integer-valued fp16: exact sums for bits <= 8 and N <= 16 (|sum| <= 2048) */
+#define DQRM_WIRE_I32 2  /* int32: exact for bits <= 16 */
+#define DQRM_WIRE_F32 3  /* unquantized FP32 gradients (mlp_layer_quantized=False, :358-369) */
+
+/* Host helper: the narrowest exact wire type for (bits, num_ranks); bits == 32 -> F32;
+ * <0 if unsupported. */
+int dqrm_dense_wire_type(int bits, int num_ranks);
+
+/* Local per-channel scale (:905-912, quant_utils.py:196-220):
+ *   s_loc[c] = clamp(max(|min_j g|, |max_j g|), 1e-8) / (2^(bits-1)-1). */
+int dqrm_dense_grad_scale(const dqrm_dense_set* set, int bits, float* s_loc, void* stream);
+
+/* Scale average + quantize into the wire (:913-918 / :945-950). s_all = the N ranks'
+ * s_loc gathered [N][C]:
+ *   s_avg[c] = (((s_{N-1} + s_{N-2}) + ...) + s_0) * (1/N)   (same order on every rank)
+ *   wire     = clamp(round(1/s_avg[c] * g + 0), -2^(bits-1), 2^(bits-1)-1)
+ * wire_type F32 copies the gradient unquantized (s_all, s_avg unused, may be NULL). */
+int dqrm_dense_grad_quant(const dqrm_dense_set* set, int bits, const float* s_all, int num_ranks,
+                          float* s_avg, int wire_type, void* wire, void* stream);
+
+/* After the wire's all-reduce(SUM): grad = 0 + wire * (1/N)  (:920-922 then the hook's
+ * grad.zero_(); grad.add_(buffer_changes), :345-351). */
+int dqrm_dense_grad_decode(const dqrm_dense_set* set, const void* wire, int wire_type, int num_ranks,
+                           void* stream);
+
+/* weight_update_parallel_comm, MLP branch (:641-642 / :659-660):
+ *   param += (-lr * grad) * s[c]     (s == NULL: param += -lr * grad, :644-645). */
+int dqrm_dense_update(const dqrm_dense_set* set, const float* s, float lr, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Row-wise PTQ formats of the reference's inference path.
  * DLRM_Net.quantize_embedding (dlrm_s_pytorch_single_gpu_documentingp.py:689-704) packs
  * each trained table with torch.ops.quantized.embedding_bag_{4bit,byte}_prepack and

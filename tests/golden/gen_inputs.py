@@ -85,3 +85,34 @@ def checksum(*arrays) -> str:
 
     feed(arrays)
     return h.hexdigest()[:16]
+
+
+# ---------------------------------------------------------------- dense (MLP) layers
+# Small DLRM-shaped MLPs for the dense-gradient fixtures: bot_l 13-32-16, top_l 24-16-1
+# (the reference's ln_bot / ln_top structure, dlrm_s_pytorch_single_gpu.py create_mlp).
+MLP_SHAPES = [(32, 13), (16, 32), (16, 24), (1, 16)]
+
+
+def mlp_params(shapes, seed):
+    """[(W [out, in], b [out])] with nn.Linear-like U(+-1/sqrt(in)) init."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for o, i in shapes:
+        b = 1.0 / np.sqrt(i)
+        out.append((rs.uniform(-b, b, (o, i)).astype(np.float32), rs.uniform(-b, b, o).astype(np.float32)))
+    return out
+
+
+def mlp_grads(shapes, seed, rank, step):
+    """Per-rank synthetic dense gradients [(gW, gb)]: per-row magnitudes spread over three
+    decades (so per-channel scales differ), one all-zero weight row (the 1e-8 clamp)."""
+    rs = np.random.RandomState(seed + 7919 * rank + 104729 * step)
+    out = []
+    for k, (o, i) in enumerate(shapes):
+        mag = (10.0 ** rs.uniform(-4, -1, (o, 1))).astype(np.float32)
+        gW = (rs.standard_normal((o, i)) * mag).astype(np.float32)
+        if k == 1:
+            gW[3] = 0.0
+        gb = (rs.standard_normal(o) * 10.0 ** rs.uniform(-3, -1)).astype(np.float32)
+        out.append((gW, gb))
+    return out

@@ -125,11 +125,24 @@ def test_dp_hooks_single_rank_match_oracle(dq, emb_q, mlp_q):
         batch, dy, ste, layout = model.emb_l._pending
         assert layout == "btd"
         dy_np = dy.detach().permute(1, 0, 2).contiguous().cpu().numpy()
+        mlp = [model.bot_l[0], model.top_l[0]]
+        mlp_p = [(l.weight.detach().cpu().numpy().copy(), l.bias.detach().cpu().numpy().copy()) for l in mlp]
+        mlp_g = [(l.weight.grad.cpu().numpy().copy(), l.bias.grad.cpu().numpy().copy()) for l in mlp]
         H.grad_update_parallel_comm(model, 1, emb_grad_quantized=emb_q, num_bits=8, mlp_layer_quantized=mlp_q)
         H.weight_update_parallel_comm(model, 0.1, emb_grad_quantized=emb_q, num_gpus=1,
                                       mlp_layer_quantized=mlp_q)
         O.dp_step(Wo, [[(P[t], np.arange(B)) for t in range(len(rows))]], [[dy_np[t] for t in range(len(rows))]],
                   s_fwd, 0.1, grad_bits=8 if emb_q else 32)
+        # MLP branch through libdqrm's dense kernels (s_q_g_p_c.py:337-409, 630-668)
+        g_o, s_o = O.dense_dp_step(mlp_p, [mlp_g], 0.1, bits=8, quantized=mlp_q)
+        for l, (W, b), (gw, gb), (sw, sb) in zip(mlp, mlp_p, g_o, s_o):
+            np.testing.assert_array_equal(l.weight.detach().cpu().numpy(), W)
+            np.testing.assert_array_equal(l.bias.detach().cpu().numpy(), b)
+            np.testing.assert_array_equal(l.weight.grad.cpu().numpy(), gw)
+            np.testing.assert_array_equal(l.bias.grad.cpu().numpy(), gb)
+            if mlp_q:
+                np.testing.assert_array_equal(l.weight_scaling_factor.cpu().numpy(), sw)
+                assert float(l.bias_scaling_factor) == float(sb[0])
         if emb_q:
             s_avg = model.emb_l.emb_scaling_factor.cpu().numpy()
             for t in range(len(rows)):
