@@ -14,7 +14,7 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
-SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_dense.hip")]
+SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_dense.hip", "dqrm_input.hip")]
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
 LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
 

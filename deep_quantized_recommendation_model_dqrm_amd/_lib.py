@@ -36,6 +36,10 @@ DQRM_UPD_DP = 0
 DQRM_UPD_SIMULATED = 1
 DQRM_UPD_FP32 = 2
 
+DQRM_CRITEO_RECORD_INTS = 40
+DQRM_CRITEO_DENSE = 13
+DQRM_CRITEO_SPARSE = 26
+
 DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
@@ -56,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_dense_grad_quant",
     "dqrm_dense_grad_decode",
     "dqrm_dense_update",
+    "dqrm_criteo_unpack",
     "dqrm_rowwise_row_bytes",
     "dqrm_rowwise_prepack",
     "dqrm_rowwise_bag",
@@ -168,6 +173,7 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_dense_grad_quant": (C.c_int, [DS, C.c_int, P, C.c_int, P, C.c_int, P, P]),
         "dqrm_dense_grad_decode": (C.c_int, [DS, P, C.c_int, C.c_int, P]),
         "dqrm_dense_update": (C.c_int, [DS, P, C.c_float, P]),
+        "dqrm_criteo_unpack": (C.c_int, [P, C.c_int64, C.c_int32, P, P, P, P, P]),
         "dqrm_rowwise_row_bytes": (C.c_size_t, [C.c_int, C.c_int]),
         "dqrm_rowwise_prepack": (C.c_int, [C.c_int, P, C.c_int64, C.c_int, P, P]),
         "dqrm_rowwise_bag": (

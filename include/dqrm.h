@@ -306,6 +306,26 @@ int dqrm_rowwise_bag(int bits, const uint8_t* packed, int64_t num_rows, int dim,
                      const float* per_sample_weights, float* out, uint32_t* err, void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Criteo input path
+ * One record = 40 int32: label, 13 dense, 26 categorical (the flat binary file that
+ * data_loader_terabyte.numpy_to_binary writes, :243-280). dqrm_criteo_unpack replaces
+ * CriteoBinDataset.__getitem__'s _transform_features (data_loader_terabyte.py:68-87,
+ * :227-237) and the Kaggle collate (dlrm_data_pytorch.py:328-345) on a device-resident
+ * record block records[num_samples][40]:
+ *   dense  f32 [B][13]  = log(float(x_int) + 1)
+ *   lS_i   i64 [26][B]  = x_cat (% max_ind_range if > 0, Python remainder), transposed
+ *   labels f32 [B]      = float(label)
+ *   lS_o   i64 [26][B]  = b (nullable: DQRM_BATCH_POOLING_ONE makes it unnecessary)
+ * dense's log is the device logf (<= 2 ulp from torch's CPU log; integers bit-exact).
+ * ------------------------------------------------------------------------------ */
+#define DQRM_CRITEO_RECORD_INTS 40
+#define DQRM_CRITEO_DENSE       13
+#define DQRM_CRITEO_SPARSE      26
+
+int dqrm_criteo_unpack(const int32_t* records, int64_t num_samples, int32_t max_ind_range, float* dense,
+                       int64_t* lS_i, float* labels, int64_t* lS_o, void* stream);
+
+/* ---------------------------------------------------------------------------------
  * Misc
  * ------------------------------------------------------------------------------ */
 /* Synthetic on-device init U(-sqrt(1/n_t), +sqrt(1/n_t)) from a counter-based hash
