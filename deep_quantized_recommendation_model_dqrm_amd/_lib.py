@@ -54,6 +54,8 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_bwd_coalesce",
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
+    "dqrm_grad_quant_pack_ranked",
+    "dqrm_emb_local_update",
     "dqrm_apply_sparse_update",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
@@ -163,6 +165,14 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_grad_quant_pack": (
             C.c_int,
             [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, C.c_int64, P, P, P],
+        ),
+        "dqrm_grad_quant_pack_ranked": (
+            C.c_int,
+            [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, P, P, C.c_int64, P, P],
+        ),
+        "dqrm_emb_local_update": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, P, C.c_int, P],
         ),
         "dqrm_apply_sparse_update": (
             C.c_int,

@@ -41,6 +41,12 @@ class ExchangeKernels(Protocol):
     def apply(self, cap_base: torch.Tensor, cap_total: int, gathered: torch.Tensor, payload_bytes: int,
               num_ranks: int, grad_bits: int, s_avg: torch.Tensor, lr: float, mode: int, repack: bool) -> None: ...
 
+    def quant_pack_ranked(self, ws: CoalescedGrad, table_bits: torch.Tensor, table_scale: torch.Tensor,
+                          cap_base: torch.Tensor, cap_total: int, payload: torch.Tensor) -> None: ...
+
+    def local_update(self, batch: LookupBatch, dy: torch.Tensor, ste: bool, layout: str, lr: float,
+                     table_mask: torch.Tensor, repack: bool) -> None: ...
+
 
 class HipExchangeKernels:
     """libdqrm kernels; the only implementation the product uses."""
@@ -70,6 +76,18 @@ class HipExchangeKernels:
                 grad_bits, _ptr(s_avg), float(lr), mode, 4 if repack else 0, _stream_handle()),
             "dqrm_apply_sparse_update",
         )
+
+    def quant_pack_ranked(self, ws, table_bits, table_scale, cap_base, cap_total, payload):
+        t = self.tables
+        L.check(
+            self.lib.dqrm_grad_quant_pack_ranked(
+                t.T, t.D, _ptr(ws.slot_cap_base), ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount),
+                _ptr(table_bits), _ptr(table_scale), _ptr(cap_base), cap_total, _ptr(payload), _stream_handle()),
+            "dqrm_grad_quant_pack_ranked",
+        )
+
+    def local_update(self, batch, dy, ste, layout, lr, table_mask, repack):
+        self.tables.local_update(batch, dy, lr, table_mask, ste=ste, repack=repack, layout=layout)
 
 
 def payload_bytes(num_tables: int, cap_total: int, dim: int, grad_bits: int) -> int:
@@ -163,6 +181,41 @@ class SparseGradExchange:
         """grad_update_parallel_comm + weight_update_parallel_comm for all tables."""
         self.exchange(batch, dy, ste=ste, layout=layout)
         self.apply(lr, mode=mode, repack=repack)
+
+    # -------------------------------------------------------------- ranking range
+    def coalesce_ranges(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True, layout: str = "tbd"):
+        """grad_precision_and_scale's per-table range (s_q_g_p_c.py:184-193): coalesce, then
+        the all-gathered max |grad| of every rank, summed in descending rank order * 1/N.
+        Returns host f32 [T] (the reference reads each with .item())."""
+        import numpy as np
+
+        self.kernels.coalesce(batch, dy, self.ws, ste, layout)
+        if self.world > 1:
+            self._all_gather(self.absmax_all, self.ws.absmax)
+            am = self.absmax_all
+        else:
+            am = self.ws.absmax.view(1, -1)
+        a = am.view(self.world, self.tables.T, L.DQRM_TABLE_SPLIT).amax(dim=2).cpu().numpy().astype(np.float32)
+        acc = a[-1].copy()
+        for r in range(self.world - 2, -1, -1):
+            acc = (acc + a[r]).astype(np.float32)
+        return (acc * np.float32(1.0 / self.world)).astype(np.float32)
+
+    def exchange_ranked(self, table_bits: torch.Tensor, table_scale: torch.Tensor) -> None:
+        """grad_update_parallel_comm(ranking_range=True)'s embedding branch (:280-309,
+        quantize_emb_grad_two :836-848): 2..8-bit tables quantized with their own scale,
+        0 / 32-bit tables send nothing; one payload all-gather. Needs grad_bits == 8."""
+        if self.grad_bits != 8:
+            raise ValueError("the ranking-range exchange uses the 8-bit payload layout")
+        self.kernels.quant_pack_ranked(self.ws, table_bits, table_scale, self.cap_base, self.cap_total, self.payload)
+        if self.world > 1:
+            self._all_gather(self.gathered, self.payload)
+
+    def apply_ranked(self, lr: float, table_scale: torch.Tensor, repack: bool = False) -> None:
+        """weight_update_parallel_comm(ranking_range=True) for the quantized tables (:617-622)."""
+        gathered = self.payload.view(1, -1) if self.world == 1 else self.gathered
+        self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, 8, table_scale,
+                           lr, L.DQRM_UPD_DP, repack)
 
     def local_scales(self) -> torch.Tensor:
         """This rank's per-table gradient scale s_loc (host-side view for inspection)."""

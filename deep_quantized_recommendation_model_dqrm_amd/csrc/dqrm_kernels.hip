@@ -717,6 +717,7 @@ DQRM_INLINE int seg_end(const uint16_t* heads, int U, int n, int u) {
 // (ascending lookup position, or ascending rank) to reproduce the reference's rounding:
 //   OP_FMA  acc = fma(v, -lr, acc) per entry          (torch CPU sparse SGD axpy)
 //   OP_SUM  acc = v0; acc = acc + v_k                  (coalesce / sparse all_reduce)
+//   OP_AXPY acc = acc + (v * -lr), product rounded     (W.add_(-lr * grad), s_q_g_p_c.py:616)
 // Short segments: one lane group (LPR lanes x float4), 4 entries in flight per chunk.
 // Long segments (> LONG_SEG entries, tiny hot tables): a whole wave loads 4*WAVE/LPR
 // entries per chunk (the next chunk prefetched) and combines them in order via shuffles.
@@ -724,12 +725,16 @@ DQRM_INLINE int seg_end(const uint16_t* heads, int U, int n, int u) {
 // ------------------------------------------------------------------------------------
 constexpr int OP_FMA = 0;
 constexpr int OP_SUM = 1;
+constexpr int OP_AXPY = 2;
 
 template <int OP>
 DQRM_INLINE float4 combine(float4 acc, float4 v, bool& first, float nlr) {
     if (OP == OP_FMA) {
         acc.x = fmaf(v.x, nlr, acc.x); acc.y = fmaf(v.y, nlr, acc.y);
         acc.z = fmaf(v.z, nlr, acc.z); acc.w = fmaf(v.w, nlr, acc.w);
+    } else if (OP == OP_AXPY) {
+        acc.x = acc.x + v.x * nlr; acc.y = acc.y + v.y * nlr;
+        acc.z = acc.z + v.z * nlr; acc.w = acc.w + v.w * nlr;
     } else if (first) {
         acc = v;
         first = false;
@@ -772,6 +777,7 @@ struct DimLane {
 template <int OP>
 DQRM_INLINE float combine1(float acc, float v, bool first, float nlr) {
     if (OP == OP_FMA) return fmaf(v, nlr, acc);
+    if (OP == OP_AXPY) return acc + v * nlr;
     return first ? v : acc + v;
 }
 
@@ -1018,7 +1024,9 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
             const float* col[NDL];
 #pragma unroll
             for (int d = 0; d < NDL; ++d) col[d] = L.stage + (lig + GD * d) * SP + e0;
-            auto op = [&](float x, float y) { return OP == OP_FMA ? fmaf(y, nlr, x) : x + y; };
+            auto op = [&](float x, float y) {
+                return OP == OP_FMA ? fmaf(y, nlr, x) : (OP == OP_AXPY ? x + y * nlr : x + y);
+            };
             int j = 0;
             if (OP == OP_SUM && first && len > 0) {  // peel: the chain below is adds only
 #pragma unroll
@@ -1394,6 +1402,7 @@ struct BwdArgs {
     float* ws_vals;
     int32_t* ws_ucount;
     float* ws_absmax;
+    const int32_t* tmask;  // MODE 2: tables to update (nullable = all)
 };
 
 // dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363);
@@ -1442,12 +1451,12 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
     const uint16_t* heads = sl.heads;
     const int64_t rb = m.row_base[t];
     DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, off4};
-    const float r_pack = (MODE == 0 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+    const float r_pack = (MODE != 1 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
     float local_absmax = 0.0f;
 
     auto finit = [&](int, int i, int sub, SegState& st) {
         const int64_t grow = rb + key_row(keys[i]);
-        if (MODE == 0) {
+        if (MODE != 1) {
             st.acc = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
             st.w = st.acc;  // old row (its max is taken in ffin, after every load is in flight)
             if (!dsplit) st.blk = a.blkmax[m.blk_base[t] + (key_row(keys[i]) >> 8)];
@@ -1458,7 +1467,7 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
     auto ffin = [&](int u, int i, int sub, SegState& st) {
         const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
-        if (MODE == 0) {
+        if (MODE != 1) {
             reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = st.acc;
             if (a.repack) pack4_row(st.acc, a.packed + grow * (D / 2), off4 + sub, r_pack);
             if (!dsplit) {
@@ -1478,19 +1487,19 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
             local_absmax = fmaxf(local_absmax, abs_max4(st.acc));
         }
     };
-    constexpr int OP = MODE == 0 ? OP_FMA : OP_SUM;
+    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
     short_segments<LPRS, OP, 8>(keys, heads, U, n, src, a.nlr, finit, ffin);
 
     using DL = DimLane<LPRS>;
     auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
         const int64_t grow = rb + key_row(keys[i]);
 #pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE == 0 ? a.W[grow * D + off4 * 4 + lig + DL::GD * d] : 0.0f;
+        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE != 1 ? a.W[grow * D + off4 * 4 + lig + DL::GD * d] : 0.0f;
     };
     auto fend = [&](int u, int i, int lig, float (&v)[DL::NDL]) {
         const uint32_t row = key_row(keys[i]);
         const int64_t grow = rb + row;
-        if (MODE == 0) {
+        if (MODE != 1) {
             float old_rm = 0.0f, old_blk = 0.0f;
             if (!dsplit) {  // the row is still unwritten (and cached since fbegin): its old max
                 float w0[DL::NDL];
@@ -1528,7 +1537,7 @@ DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_l
         if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
     }
     __syncthreads();
-    if (MODE == 0) {
+    if (MODE != 1) {
         if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty,
                                      reinterpret_cast<int*>(&s_misc[2]));
     } else if (threadIdx.x == 0) {
@@ -1553,6 +1562,7 @@ __global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
     __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
 
     const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
+    if (MODE == 2 && a.tmask != nullptr && a.tmask[t] == 0) return;  // table not selected
     const int T = a.T;
     Meta m = make_meta(a.meta, T);
     const int64_t nrows = m.num_rows[t];
@@ -1659,7 +1669,9 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
                                                     const int32_t* __restrict__ ws_ucount,
                                                     const float* __restrict__ absmax_all, int N, int bits,
                                                     const int64_t* __restrict__ cap_base, int64_t cap_total,
-                                                    float* __restrict__ s_avg, unsigned char* __restrict__ payload) {
+                                                    float* __restrict__ s_avg, unsigned char* __restrict__ payload,
+                                                    const int32_t* __restrict__ tbits,
+                                                    const float* __restrict__ tscale) {
     __shared__ int s_cnt[SPLIT];
     __shared__ float s_am[64 * SPLIT];
     __shared__ int s_pre, s_my;
@@ -1668,8 +1680,13 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
     const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
     const int D = LPR * 4;
     const PayloadLayout pl = payload_layout(T, cap_total, D, bits);
-    const bool quant = bits >= 2 && bits <= 16;
-    if (threadIdx.x < SPLIT) s_cnt[threadIdx.x] = ws_ucount[t * SPLIT + threadIdx.x];
+    // ranking range (tbits != NULL): per-table bit width and scale; 0 / 32-bit tables send
+    // nothing (grad_update_parallel_comm skips them, s_q_g_p_c.py:280-289)
+    const int tb = tbits ? tbits[t] : bits;
+    const bool ranked = tbits != nullptr;
+    const bool send = !ranked || (tb >= 2 && tb <= 8);
+    const bool quant = !ranked && bits >= 2 && bits <= 16;
+    if (threadIdx.x < SPLIT) s_cnt[threadIdx.x] = send ? ws_ucount[t * SPLIT + threadIdx.x] : 0;
     if (quant)
         for (int j = threadIdx.x; j < N * SPLIT; j += blockDim.x)
             s_am[j] = absmax_all[((int64_t)(j / SPLIT) * T + t) * SPLIT + (j % SPLIT)];
@@ -1702,11 +1719,13 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
     __syncthreads();
     const int cnt = s_my;
     const int64_t src0 = ws_cap_base[k], dst0 = cap_base[t] + s_pre;
-    const float rr = quant ? 1.0f / s_sc : 0.0f;
+    const bool qv = quant || (ranked && send);  // values are quantized
+    const float rr = quant ? 1.0f / s_sc : (qv ? 1.0f / tscale[t] : 0.0f);
     const int lane = threadIdx.x % LPR;
     constexpr int QU = 4;                 // entries in flight per lane group
     constexpr int EPI = 512 / LPR;        // lane groups per workgroup
-    const float qlo = -(float)(1 << (bits - 1)), qhi = (float)((1 << (bits - 1)) - 1);
+    const int qb = ranked ? (send ? tb : 2) : bits;
+    const float qlo = -(float)(1 << (qb - 1)), qhi = (float)((1 << (qb - 1)) - 1);
     for (int u0 = threadIdx.x / LPR; u0 < cnt; u0 += QU * EPI) {
         float4 v[QU];
         int32_t row[QU];
@@ -1724,7 +1743,7 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
             if (u >= cnt) continue;
             const int64_t q = dst0 + u;  // dense payload entry
             if (lane == 0) reinterpret_cast<int32_t*>(payload + pl.rows_off)[q] = row[h];
-            if (!quant) {
+            if (!qv) {
                 reinterpret_cast<float4*>(payload + pl.vals_off + q * D * 4)[lane] = v[h];
                 continue;
             }
@@ -2423,10 +2442,60 @@ int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, in
     DISPATCH_LPR(dim, {
         hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
                            num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, absmax_all,
-                           num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload);
+                           num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload,
+                           (const int32_t*)nullptr, (const float*)nullptr);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
+}
+
+int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                                const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                                const int32_t* table_bits, const float* table_scale, const int64_t* cap_base,
+                                int64_t cap_total, void* payload, void* stream) {
+    if (num_tables <= 0 || num_tables > MAX_TABLES)
+        return set_error(DQRM_E_INVALID, "%s: bad num_tables", "dqrm_grad_quant_pack_ranked");
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !table_bits || !table_scale || !cap_base || !payload)
+        return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_grad_quant_pack_ranked");
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_LPR(dim, {
+        hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
+                           num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount,
+                           (const float*)nullptr, 1, 8, cap_base, cap_total, (float*)nullptr,
+                           (unsigned char*)payload, table_bits, table_scale);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                          int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, const int32_t* table_mask,
+                          int repack_bits, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_local_update"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_local_update");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_emb_local_update", repack_bits);
+    if (batch->num_bags <= 0) return DQRM_OK;
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
+    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.scale = set->scale; a.pscale = set->pscale;
+    a.meta = set->meta; a.err = set->err;
+    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
+    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
+    a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4; a.tmask = table_mask;
+    hipStream_t st = (hipStream_t)stream;
+    const int D = set->dim;
+    DISPATCH_LPR(D, {
+        if ((rc = allow_lds(k_table_bwd<LPR, 2>, SLOT_LDS))) return rc;
+        hipLaunchKernelGGL((k_table_bwd<LPR, 2>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
+    });
+    LAUNCH_CHECK();
+    return launch_finalize(set, st);
 }
 
 int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,

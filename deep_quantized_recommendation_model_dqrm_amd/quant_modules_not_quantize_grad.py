@@ -112,6 +112,7 @@ class _QuantEmbeddingBase(nn.Module):
         self._exchange = None     # SparseGradExchange used by the DP hooks
         self._ready = None        # grad bits of an exchanged, not yet applied update
         self._counters = None     # host mirror of (now_iteration, iteration_bound, iteration_nt)
+        self._rr = None           # ranking range: (bits host int32 [T], bits dev, scale dev) of this step
 
     # ------------------------------------------------------------ scale refresh logic
     def _refresh_due(self, fp: bool, test_mode: bool) -> bool:
@@ -283,6 +284,7 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         self.register_buffer("iteration_bound", torch.zeros(1, device=dev), persistent=True)
         self.register_buffer("iteration_nt", torch.zeros(1, device=dev), persistent=True)
         self.register_buffer("emb_scaling_factor", torch.zeros(T, device=dev), persistent=True)
+        self.register_buffer("gradient_bit_width", torch.zeros(T, device=dev), persistent=True)
         self.embedding_bag = _WeightHolder(nn.Parameter(self._tset.W, requires_grad=True))
 
     def table_weight(self, t: int) -> torch.Tensor:

@@ -63,6 +63,16 @@ def _detach_grad(g: torch.Tensor) -> None:
 
 
 # ---------------------------------------------------------------------------- embedding branch
+def _ensure_exchange(m: _QuantEmbeddingBase, grad_bits: int, group) -> SparseGradExchange:
+    batch = m._pending[0]
+    ex = m._exchange
+    if ex is None or ex.grad_bits != grad_bits or ex.max_lookups < batch.max_lookups or ex.group is not group:
+        ex = SparseGradExchange(m._tset, max(batch.max_lookups, 1), grad_bits=grad_bits, group=group,
+                                device=m._tset.device)
+        m._exchange = ex
+    return ex
+
+
 def _exchange_module(m: _QuantEmbeddingBase, number_of_gpus: int, grad_bits: int, group) -> None:
     if m.grad_mode != "dp":
         raise ValueError("grad_update_parallel_comm needs embedding modules built with grad_mode='dp'")
@@ -71,11 +81,7 @@ def _exchange_module(m: _QuantEmbeddingBase, number_of_gpus: int, grad_bits: int
     if _world(group) != number_of_gpus:
         raise ValueError(f"number_of_gpus={number_of_gpus} but the process group has {_world(group)} ranks")
     batch, dy, ste, layout = m._pending
-    ex = m._exchange
-    if ex is None or ex.grad_bits != grad_bits or ex.max_lookups < batch.max_lookups or ex.group is not group:
-        ex = SparseGradExchange(m._tset, max(batch.max_lookups, 1), grad_bits=grad_bits, group=group,
-                                device=m._tset.device)
-        m._exchange = ex
+    ex = _ensure_exchange(m, grad_bits, group)
     s_avg = ex.exchange(batch, dy, ste=ste, layout=layout)
     if grad_bits != 32:
         m.emb_scaling_factor.copy_(s_avg.view_as(m.emb_scaling_factor))
@@ -88,13 +94,20 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
     """s_q_g_p_c.py:257-409. Embedding tables: fused coalesce -> scale all-gather ->
     quantize-pack -> payload all-gather (emb_grad_quantized=False: FP32 payloads, the
     unquantized sparse all_reduce of :319-327). MLP layers: see module docstring."""
-    if ranking_range:
-        raise NotImplementedError("ranking_range mixed-precision gradients are not built yet (SURVEY.md 8(f) #3)")
-    if emb_grad_quantized and not 2 <= int(num_bits) <= 16:
+    if emb_grad_quantized and not ranking_range and not 2 <= int(num_bits) <= 16:
         raise ValueError("num_bits must be in 2..16 for quantized embedding gradients")
     with torch.no_grad():
         for m in _emb_modules(model):
-            _exchange_module(m, number_of_gpus, int(num_bits) if emb_grad_quantized else 32, group)
+            if ranking_range and emb_grad_quantized:  # :280-301, per-table bits from grad_precision_and_scale
+                if m._pending is None:
+                    continue
+                if m._rr is None:
+                    raise RuntimeError("ranking_range=True needs grad_precision_and_scale(...) first "
+                                       "(dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1897-1898)")
+                m._exchange.exchange_ranked(m._rr[1], m._rr[2])
+                m._ready = "ranked"
+            else:
+                _exchange_module(m, number_of_gpus, int(num_bits) if emb_grad_quantized else 32, group)
         _mlp_grad_update(model, number_of_gpus, mlp_layer_quantized, group)
 
 
@@ -131,14 +144,27 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
                                 rank_for_debug=None, ranking_range=False, use_ec=False, mlp_layer_quantized=True):
     """s_q_g_p_c.py:601-668: W += -lr * grad * s for the tables (one libdqrm launch for all
     tables of a module) and the MLP layers."""
-    if ranking_range:
-        raise NotImplementedError("ranking_range mixed-precision gradients are not built yet (SURVEY.md 8(f) #3)")
     if use_ec:
         raise NotImplementedError("error compensation (use_ec) is off in the reference's scripts and not built")
     with torch.no_grad():
         for m in _emb_modules(model):
             ready = getattr(m, "_ready", None)
             if ready is None:
+                continue
+            if ready == "ranked":  # :610-622
+                if not (ranking_range and emb_grad_quantized):
+                    raise ValueError("ranking_range differs from the one used by grad_update_parallel_comm")
+                if update_embedding:
+                    bits_h, bits_d, scale_d = m._rr
+                    repack = m._use_packed(False)
+                    m._exchange.apply_ranked(lr, scale_d, repack=repack)  # 8-bit tables: W += -lr * (g * s)
+                    if (bits_h == 32).any():  # 32-bit tables: W.add_(-lr * grad), the rank's own gradient
+                        batch, dy, ste, layout = m._pending
+                        mask = (bits_d == 32).to(torch.int32)
+                        m._exchange.kernels.local_update(batch, dy, ste, layout, lr, mask, repack)
+                m._pending = None
+                m._ready = None
+                m._rr = None
                 continue
             if update_embedding:
                 if (ready != 32) != bool(emb_grad_quantized):
@@ -166,6 +192,7 @@ def clear_gradients(model) -> None:
             for m in _emb_modules(model):
                 m._pending = None
                 m._ready = None
+                m._rr = None
 
 
 def weight_syncc(dlrm, num_gpus, group=None) -> None:
@@ -203,9 +230,69 @@ def quantized_gradients_update(model, arg, lr, num_gpus) -> None:
             param.add_(update * (-lr[-1]))
 
 
-def grad_precision_and_scale(*args, **kwargs):
-    """s_q_g_p_c.py:158-255 (ranking-range per-table bit widths): not built yet."""
-    raise NotImplementedError("ranking_range mixed-precision gradients are not built yet (SURVEY.md 8(f) #3)")
+def _rr_thresholds(T: int):
+    """Last positions of the 0-bit and 8-bit groups in the sampled order: (8, 22) for the
+    reference's 26 tables (:228-236); other table counts keep the same proportions."""
+    if T == 26:
+        return 8, 22
+    return int(round(T * 9 / 26)) - 1, int(round(T * 23 / 26)) - 1
+
+
+def grad_precision_and_scale(model, number_of_gpus, rank_for_debug=None, output_flag=False, group=None):
+    """s_q_g_p_c.py:158-255, ranking-range mixed precision (called after backward, before
+    grad_update/weight_update_parallel_comm(..., ranking_range=True)).
+
+    Per table: range = max |coalesced grad| (finding_range_for_gradient), all-reduced / N
+    (one all-gather of all tables' per-slot maxima, summed in descending rank order);
+    emb_scaling_factor = range. Rank 0 ranks the tables with numpy's global RNG,
+    np.random.choice(T, T, replace=False, p=range/(eb_scale*7) normalised)[::-1], and gives
+    the first 9 positions 0 bits, the next 14 8 bits and the rest 32 bits; the widths are
+    broadcast, and 8-bit tables get emb_scaling_factor = clamp(range, 1e-8) / 127."""
+    import numpy as np
+
+    with torch.no_grad():
+        if _world(group) != number_of_gpus:
+            raise ValueError(f"number_of_gpus={number_of_gpus} but the process group has {_world(group)} ranks")
+        per, range_list = [], []
+        for m in _emb_modules(model):
+            if m.grad_mode != "dp":
+                raise ValueError("grad_precision_and_scale needs embedding modules built with grad_mode='dp'")
+            if m._pending is None:
+                raise RuntimeError("grad_precision_and_scale needs a backward pass since the last update")
+            batch, dy, ste, layout = m._pending
+            ex = _ensure_exchange(m, 8, group)
+            rg = ex.coalesce_ranges(batch, dy, ste=ste, layout=layout)
+            eb = m._tset.scale.cpu().numpy().astype(np.float32)  # eb_scaling_factor of each table
+            range_list += [float(x) for x in (rg / (eb * np.float32(7))).astype(np.float32)]
+            per.append((m, rg))
+        Tt = len(range_list)
+        bits = torch.zeros(Tt, dtype=torch.int32)
+        rank = dist.get_rank(group) if _world(group) > 1 else 0
+        if rank == 0:
+            prob_l = np.asarray(range_list) / (np.sum(range_list))
+            list_id = np.random.choice(Tt, Tt, replace=False, p=prob_l)
+            list_id = list_id[::-1]
+            if rank_for_debug == 0 and output_flag:
+                print("rank {} ranking from least wide range to the widest range {}".format(rank_for_debug, list_id))
+            z, e = _rr_thresholds(Tt)
+            for j, t in enumerate(list_id):
+                bits[t] = 0 if j <= z else (8 if j <= e else 32)
+        if _world(group) > 1:
+            dist.barrier(group=group)
+            dev = per[0][0]._tset.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            bd = bits.to(dev)
+            dist.broadcast(bd, 0, group=group)
+            bits = bd.cpu()
+        off = 0
+        for m, rg in per:
+            b = bits[off: off + len(rg)].numpy()
+            off += len(rg)
+            n = np.float32(127.0)  # 2 ** (8 - 1) - 1: the only quantized width ranking assigns
+            scale = np.where(b == 8, (np.maximum(rg, np.float32(1e-8)) / n).astype(np.float32), rg).astype(np.float32)
+            m.emb_scaling_factor.copy_(torch.from_numpy(scale).view_as(m.emb_scaling_factor))
+            m.gradient_bit_width.copy_(torch.from_numpy(b.astype(np.float32)).view_as(m.gradient_bit_width))
+            dev = m._tset.device
+            m._rr = (b.copy(), torch.from_numpy(b.copy()).to(dev), torch.from_numpy(scale).to(dev))
 
 
 # the DP driver imports this misspelled name (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:121)

@@ -272,6 +272,17 @@ class EmbeddingTableSet:
             "dqrm_emb_bwd_sgd",
         )
 
+    def local_update(self, batch: LookupBatch, dy: torch.Tensor, lr: float, table_mask: torch.Tensor | None = None,
+                     ste: bool = True, repack: bool = False, layout: str = "tbd") -> None:
+        """W.add_(-lr * grad) with the rank's own uncoalesced gradient, product rounded, in
+        lookup order (ranking-range 32-bit tables, s_q_g_p_c.py:615-616); table_mask int32 [T]."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_local_update(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
+                                           float(lr), _ptr(table_mask), 4 if repack else 0, _stream_handle()),
+            "dqrm_emb_local_update",
+        )
+
     def backward_coalesce(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad",
                           ste: bool = True, layout: str = "tbd") -> None:
         """STE + sparse backward + coalesce + per-slot max |grad| (s_q_g_p_c.py:850-861)."""

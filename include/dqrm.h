@@ -208,6 +208,28 @@ int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, in
                          const int64_t* cap_base, int64_t cap_total, float* s_avg, void* payload,
                          void* stream);
 
+/* Ranking-range mixed-precision gradients (grad_precision_and_scale
+ * s_q_g_p_c.py:158-255 decides a bit width per table: 0, 8 or 32). Quantize-pack with a
+ * per-table bit width and scale (quantize_emb_grad_two, :836-848):
+ *   table_bits[t] in 2..8 : q = clamp(round(1/table_scale[t] * v + 0), -2^(b-1), 2^(b-1)-1)
+ *   table_bits[t] 0 or 32: the table sends no entries (grad_update_parallel_comm skips it, :280-289)
+ * The payload layout is that of grad_bits = 8 (int8 values); apply it with
+ * dqrm_apply_sparse_update(mode DQRM_UPD_DP, grad_bits 8, s_avg = table_scale). */
+int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                                const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                                const int32_t* table_bits, const float* table_scale, const int64_t* cap_base,
+                                int64_t cap_total, void* payload, void* stream);
+
+/* Local (uncommunicated) update of the ranking-range 32-bit tables,
+ * weight_update_parallel_comm :615-616  W.add_(-lr * grad)  with grad the rank's own sparse
+ * gradient: per lookup, in lookup order, W[r] = W[r] + (g' * -lr) with g' = (dy*s)/s
+ * (ste != 0), the product rounded separately. Only tables with table_mask[t] != 0
+ * (NULL = all) are touched; rowmax/blkmax/sblkmax/tmax and (repack_bits == 4) packed rows
+ * are maintained as in dqrm_emb_bwd_sgd. */
+int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                          int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, const int32_t* table_mask,
+                          int repack_bits, void* stream);
+
 /* update modes for dqrm_apply_sparse_update */
 #define DQRM_UPD_DP        0  /* v = ((Q * (1/N)) * s) ; W += -lr * v   (s_q_g_p_c.py:885,618-622) */
 #define DQRM_UPD_SIMULATED 1  /* v = Q * f32((double)s / N) ; W += -lr * v (sgd_quantized_gradients.py:366-371) */

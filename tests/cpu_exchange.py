@@ -118,3 +118,37 @@ class OracleExchangeKernels:
                 qq.append(p[lo: lo + U * D * elem].view(dt).reshape(U, D).astype(f32))
             O.dp_apply(self.t.Ws[t], rr, qq, f32(s_avg[t]), num_ranks, lr,
                        mode="fp32" if mode == L.DQRM_UPD_FP32 else "dp")
+
+    def quant_pack_ranked(self, ws, table_bits, table_scale, cap_base, cap_total, payload):
+        """dqrm_grad_quant_pack_ranked: per-table bits/scale; 0 / 32-bit tables send nothing."""
+        T, D = self.t.T, self.t.D
+        cb = cap_base.numpy()
+        rows_off = a16(4 * T * SPLIT)
+        vals_off = rows_off + a16(4 * cap_total)
+        p = payload.numpy()
+        p[:] = 0
+        tb, ts = table_bits.numpy(), table_scale.numpy()
+        for t in range(T):
+            if not 2 <= tb[t] <= 8:
+                continue
+            rows, vals, counts = [], [], []
+            for s in range(SPLIT):
+                k = t * SPLIT + s
+                b, u = ws.slot_base[k], int(ws.ucount[k])
+                rows.append(ws.rows[b: b + u].numpy())
+                vals.append(ws.vals[b: b + u].numpy())
+                counts.append(u)
+            rows, vals = np.concatenate(rows), np.concatenate(vals)
+            U = len(rows)
+            p[4 * t * SPLIT: 4 * (t + 1) * SPLIT] = np.array(counts, np.int32).view(np.uint8)
+            p[rows_off + 4 * cb[t]: rows_off + 4 * (cb[t] + U)] = rows.astype(np.int32).view(np.uint8)
+            q = O.quantize(vals, f32(ts[t]), int(tb[t])).astype(np.int8)
+            lo = vals_off + cb[t] * D
+            p[lo: lo + U * D] = np.ascontiguousarray(q).reshape(-1).view(np.uint8)
+
+    def local_update(self, batch, dy, ste, layout, lr, table_mask, repack):
+        assert layout == "tbd"
+        dy = dy.numpy()
+        for t in range(self.t.T):
+            if table_mask is None or int(table_mask[t]):
+                O.emb_local_update(self.t.Ws[t], batch.idxs[t], batch.offs[t], dy[t], batch.s_fwd[t], lr, ste)
