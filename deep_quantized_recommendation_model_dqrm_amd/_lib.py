@@ -35,6 +35,9 @@ DQRM_FWD_NT_STORE = 16
 DQRM_UPD_DP = 0
 DQRM_UPD_SIMULATED = 1
 DQRM_UPD_FP32 = 2
+DQRM_APPLY_AUTO = 0
+DQRM_APPLY_FLAT = 1
+DQRM_APPLY_SLOT = 2
 
 DQRM_CRITEO_RECORD_INTS = 40
 DQRM_CRITEO_DENSE = 13
@@ -69,6 +72,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_init_uniform",
     "dqrm_read_errors",
     "dqrm_last_error",
+    "dqrm_set_apply_kernel",
     "dqrm_abi_version",
 )
 
@@ -96,6 +100,7 @@ class TableSet(C.Structure):
         ("err", C.c_void_p),
         ("tflags", C.c_void_p),
         ("sdirty", C.c_void_p),
+        ("bdirty", C.c_void_p),
     ]
 
 
@@ -193,6 +198,7 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_init_uniform": (C.c_int, [TS, C.c_uint64, P]),
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
         "dqrm_last_error": (C.c_char_p, []),
+        "dqrm_set_apply_kernel": (C.c_int, [C.c_int]),
         "dqrm_abi_version": (C.c_int, []),
     }
     for name, (res, args) in sig.items():

@@ -20,6 +20,9 @@
 #include <stdarg.h>
 #include <string.h>
 #include <math.h>
+#include <stdlib.h>
+
+#include <atomic>
 
 #include "../../include/dqrm.h"
 
@@ -63,6 +66,7 @@ constexpr int WAVE = 64;
 constexpr int BLK = DQRM_BLOCK_ROWS;     // 256
 constexpr int SBLK_BLOCKS = 256;         // blocks per superblock
 constexpr int MAX_TABLES = 256;
+constexpr int DQRM_MAX_RANKS = 64;    // dqrm_apply_sparse_update: num_ranks <= 64
 
 // ------------------------------------------------------------------------------------
 // device helpers
@@ -1169,7 +1173,8 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
 // rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats).
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
-                               uint8_t* __restrict__ sdirty, float* __restrict__ tmax, int D) {
+                               uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
+                               int D) {
     __shared__ float red[16];
     if (m.num_rows[t] <= BLK) {
         const int64_t grow = m.row_base[t] + threadIdx.x;
@@ -1188,6 +1193,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             blkmax[m.blk_base[t]] = r;
             sblkmax[m.sblk_base[t]] = r;
             sdirty[m.sblk_base[t]] = 0;
+            bdirty[m.blk_base[t]] = 0;
             tmax[t] = r;
         }
         return;
@@ -1212,11 +1218,36 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
                 msk &= msk - 1;
                 const int64_t sb = k0 + j * WAVE + l;
                 const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+                // blocks the flat apply flagged (a max holder shrank): re-reduce their 256 rowmax
+                // (wave-cooperative; the owning lane keeps the new value in a register)
+                float nv[SBLK_BLOCKS / WAVE];
+                bool dq[SBLK_BLOCKS / WAVE];
+#pragma unroll
+                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+                    const int64_t b = b0 + lane + q * WAVE;
+                    dq[q] = b < b1 && bdirty[bb + b];
+                    nv[q] = 0.0f;
+                    uint64_t dm = __ballot(dq[q]);
+                    while (dm) {
+                        const int dl = __ffsll((long long)dm) - 1;
+                        dm &= dm - 1;
+                        const int64_t blk = b0 + q * WAVE + dl;
+                        float x = 0.0f;
+#pragma unroll
+                        for (int k = 0; k < BLK / WAVE; ++k) {
+                            const int64_t rr = blk * BLK + lane + k * WAVE;
+                            if (rr < m.num_rows[t]) x = fmaxf(x, rowmax[m.row_base[t] + rr]);
+                        }
+                        x = wave_max(x);
+                        if (lane == dl) nv[q] = x;
+                    }
+                    if (dq[q]) { blkmax[bb + b] = nv[q]; bdirty[bb + b] = 0; }
+                }
                 float v = 0.0f;
 #pragma unroll
                 for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
                     const int64_t b = b0 + lane + q * WAVE;
-                    if (b < b1) v = fmaxf(v, blkmax[bb + b]);
+                    if (b < b1) v = fmaxf(v, dq[q] ? nv[q] : blkmax[bb + b]);
                 }
                 v = wave_max(v);
                 if (lane == 0) { sblkmax[sbb + sb] = v; sdirty[sbb + sb] = 0; }
@@ -1250,10 +1281,11 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
 // "last workgroup finalizes" counter, writes back the XCD's L2 and measured 2x slower).
 __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
                                                          float* __restrict__ blkmax, float* __restrict__ sblkmax,
-                                                         uint8_t* __restrict__ sdirty, float* __restrict__ tmax,
+                                                         uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty,
+                                                         float* __restrict__ tmax,
                                                          const int64_t* __restrict__ meta, int T, int D) {
     const Meta m = make_meta(meta, T);
-    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, tmax, D);
+    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -1775,6 +1807,7 @@ struct ApplyArgs {
     float* blkmax;
     float* sblkmax;
     uint8_t* sdirty;
+    uint8_t* bdirty;
     const float* pscale;
     const int64_t* meta;
     uint32_t* err;
@@ -2000,6 +2033,121 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// K6 (flat): one lane group (LPR lanes x float4) per payload entry, thousands of
+// workgroups, no per-slot sort. Rank r's rows of a table arrive ascending and unique, so
+// the entry of row x in rank j is found by a binary search of rank j's row list (lane k of
+// the group searches ranks k, k+LPR, ...). The entry of the LOWEST rank holding x owns the
+// row: it sums the rank-ordered values (integers: exact in any order; FP32: ascending rank,
+// as the slot kernel and Gloo's sparse all_reduce), applies the SGD update, writes rowmax
+// and keeps the |W| hierarchy exact without a per-block pass: growth goes in with an
+// order-free atomicMax on the non-negative float bits; a row that held its block's max and
+// shrank flags the block (bdirty) and its superblock (sdirty) for finalize, which
+// re-reduces exactly those. Random 256-B row RMWs from the whole chip at once: the
+// translation / HBM latency of the 198 GB slab is overlapped across all CUs instead of
+// queueing behind 8 workgroups per table.
+// ------------------------------------------------------------------------------------
+DQRM_INLINE int table_entry_count(const unsigned char* payload, int t, int64_t cap) {
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(payload) + t * SPLIT;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < SPLIT; ++k) c += cnt[k] > 0 ? cnt[k] : 0;
+    return c < cap ? c : (int)cap;
+}
+
+// position of row x in an ascending row list of n entries, or -1
+DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rows[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return (lo < n && rows[lo] == x) ? lo : -1;
+}
+
+constexpr int FLAT_TPB = 256;
+
+template <int LPR>
+__global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
+    constexpr int D = LPR * 4;
+    constexpr int G = FLAT_TPB / LPR;               // entries per workgroup pass
+    __shared__ int s_pos[G][DQRM_MAX_RANKS];       // per entry: its row's position in each rank
+    const int t = blockIdx.y, r = blockIdx.z;
+    const int T = a.T, N = a.N;
+    const Meta m = make_meta(a.meta, T);
+    const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
+    const int64_t cb = a.cap_base[t];
+    const int64_t cap = a.cap_base[t + 1] - cb;
+    const unsigned char* pr = a.payloads + (int64_t)r * a.payload_bytes;
+    const int cnt_r = table_entry_count(pr, t, cap);
+    if ((int64_t)blockIdx.x * G >= cnt_r) return;
+    const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const ApplyUpdate update{a.mode, (float)(1.0 / (double)N), sc, (float)((double)sc / (double)N), a.nlr};
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    const PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, cb, 0};
+    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int gbase = (threadIdx.x % WAVE) - sub;   // first lane of this group in the wave
+    const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
+    int* pos = s_pos[grp];
+    const int32_t* rows_r = reinterpret_cast<const int32_t*>(pr + pl.rows_off) + cb;
+    for (int e = blockIdx.x * G + grp; e < cnt_r; e += gridDim.x * G) {
+        const int32_t x = rows_r[e];
+        if (x < 0 || x >= nrows) {  // cannot happen for payloads this library packed
+            if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+            continue;
+        }
+        float4 acc;
+        if (N == 1) {
+            acc = src.load((uint32_t)e, sub);
+        } else {  // where the other ranks hold row x (lane k searches ranks k, k+LPR, ...)
+            bool lower = false;
+            for (int j = sub; j < N; j += LPR) {
+                int p = e;
+                if (j != r) {
+                    const unsigned char* pj = a.payloads + (int64_t)j * a.payload_bytes;
+                    p = find_row(reinterpret_cast<const int32_t*>(pj + pl.rows_off) + cb, table_entry_count(pj, t, cap), x);
+                    lower |= (j < r) && p >= 0;
+                }
+                pos[j] = p;  // LDS, read back by the same wave below (in-order LDS within a wave)
+            }
+            if (__ballot(lower) & gmask) continue;  // a lower rank owns this row (group-uniform)
+            // owner: rank-ordered sum of the row's entries (ranks >= r)
+            bool first = true;
+            acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = r; j < N; ++j) {
+                const int p = pos[j];
+                if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
+            }
+        }
+        const int64_t grow = rb + x;
+        const int64_t blk = x >> 8;
+        const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+        const float old_blk = a.blkmax[bb + blk];
+        float4 w;
+        w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
+        w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
+        reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+        if (a.repack) pack4_row(w, a.packed + grow * (D / 2), sub, r_pack);
+        const float old_rm = group_max<LPR>(abs_max4(w0));
+        const float rm = group_max<LPR>(abs_max4(w));
+        if (sub == 0) {
+            a.rowmax[grow] = rm;
+            if (nrows > BLK) {  // narrow tables are rebuilt from W by finalize
+                const int64_t sb = sbb + (blk >> 8);
+                if (rm > old_blk) {
+                    atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
+                    if (rm > a.sblkmax[sb]) atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
+                }
+                if (old_rm == old_blk && rm < old_rm) {
+                    a.bdirty[bb + blk] = 1;
+                    a.sdirty[sb] = 1;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Row-wise PTQ formats of the reference's inference path:
 //   prepack   torch.ops.quantized.embedding_bag_{4bit,byte}_prepack
 //             (DLRM_Net.quantize_embedding, dlrm_s_pytorch_single_gpu_documentingp.py:689-704)
@@ -2150,7 +2298,7 @@ int check_set(const dqrm_table_set* s) {
     if (D < 4 || D > 256 || (D & 3) || ((D / 4) & (D / 4 - 1)))
         return set_error(DQRM_E_INVALID, "dqrm: dim must be 4*2^k <= 256 (got %d)", D);
     if (!s->W || !s->rowmax || !s->blkmax || !s->sblkmax || !s->tmax || !s->scale || !s->pscale ||
-        !s->meta || !s->err || !s->tflags || !s->sdirty)
+        !s->meta || !s->err || !s->tflags || !s->sdirty || !s->bdirty)
         return set_error(DQRM_E_INVALID, "dqrm: null state pointer");
     if (((uintptr_t)s->W) & 15)
         return set_error(DQRM_E_INVALID, "dqrm: W must be 16-byte aligned");
@@ -2160,7 +2308,7 @@ int check_set(const dqrm_table_set* s) {
 int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
     static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
     hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
-                       set->blkmax, set->sblkmax, set->sdirty, set->tmax, set->meta, set->num_tables,
+                       set->blkmax, set->sblkmax, set->sdirty, set->bdirty, set->tmax, set->meta, set->num_tables,
                        set->dim);
     LAUNCH_CHECK();
     return DQRM_OK;
@@ -2203,6 +2351,20 @@ int allow_lds(K kernel, size_t bytes) {
     return DQRM_OK;
 }
 
+// dqrm_apply_sparse_update's kernel choice: -1 = not yet read from DQRM_APPLY
+std::atomic<int> g_apply_kernel{-1};
+
+int apply_kernel_kind() {
+    int k = g_apply_kernel.load();
+    if (k < 0) {
+        const char* e = getenv("DQRM_APPLY");
+        k = (e && !strcmp(e, "flat")) ? DQRM_APPLY_FLAT : (e && !strcmp(e, "slot")) ? DQRM_APPLY_SLOT : DQRM_APPLY_AUTO;
+        int expect = -1;
+        g_apply_kernel.compare_exchange_strong(expect, k);
+        k = g_apply_kernel.load();
+    }
+    return k;
+}
 
 }  // namespace
 
@@ -2225,6 +2387,14 @@ const char* dqrm_last_error(void) { return g_last_error; }
 __attribute__((visibility("hidden"))) int dqrm_internal_set_error(int code, const char* msg) {
     return set_error(code, "%s", msg);
 }
+int dqrm_set_apply_kernel(int kind) {
+    if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_SLOT)
+        return set_error(DQRM_E_INVALID, "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat) or 2 (slot)");
+    const int prev = apply_kernel_kind();
+    g_apply_kernel.store(kind);
+    return prev;
+}
+
 int dqrm_abi_version(void) { return DQRM_ABI_VERSION; }
 
 int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream) {
@@ -2255,6 +2425,7 @@ int dqrm_refresh_absmax(const dqrm_table_set* set, void* stream) {
                        set->blkmax, set->sblkmax, set->meta, set->num_tables, 2, set->total_sblocks);
     LAUNCH_CHECK();
     HIP_TRY(hipMemsetAsync(set->sdirty, 0, (size_t)set->total_sblocks, st));
+    HIP_TRY(hipMemsetAsync(set->bdirty, 0, (size_t)set->total_blocks, st));
     hipLaunchKernelGGL(k_table_max, dim3(set->num_tables), dim3(256), 0, st, set->sblkmax, set->tmax,
                        set->meta, set->num_tables);
     LAUNCH_CHECK();
@@ -2503,7 +2674,7 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              const float* s_avg, float lr, int mode, int repack_bits, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
-    if (num_ranks <= 0 || num_ranks > 64 || !payloads || !cap_base)
+    if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS || !payloads || !cap_base)
         return set_error(DQRM_E_INVALID, "%s: bad ranks/payloads (%d)", "dqrm_apply_sparse_update", num_ranks);
     if (mode == DQRM_UPD_FP32 ? grad_bits != 32 : (grad_bits < 2 || grad_bits > 16 || !s_avg))
         return set_error(DQRM_E_INVALID, "%s: mode/grad_bits mismatch (%d)", "dqrm_apply_sparse_update", grad_bits);
@@ -2517,13 +2688,31 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
     a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
     a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)payload_bytes;
     a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
-    a.mode = mode; a.repack = repack_bits == 4;
+    a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty;
     hipStream_t st = (hipStream_t)stream;
     const int D = set->dim;
-    DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_apply<LPR>, SLOT_LDS))) return rc;
-        hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
-    });
+    const int kind = apply_kernel_kind();
+    // AUTO: flat while each lane of a row's group searches at most one other rank
+    // (num_ranks < D/4), slot beyond (tools/bench_apply_ranks.py)
+    if (kind == DQRM_APPLY_SLOT || (kind == DQRM_APPLY_AUTO && num_ranks > 1 && num_ranks >= D / 4)) {
+        DISPATCH_LPR(D, {
+            if ((rc = allow_lds(k_table_apply<LPR>, SLOT_LDS))) return rc;
+            hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
+        });
+    } else {
+        // grid (entry chunks, tables, ranks): twice the chunks of an average table (the
+        // per-table capacities live on the device); larger tables grid-stride, chunks past
+        // a table's count exit at once
+        DISPATCH_LPR(D, {
+            constexpr int G = FLAT_TPB / LPR;
+            int64_t gx = 2 * ((cap_total + (int64_t)a.T * G - 1) / ((int64_t)a.T * G));
+            const int64_t lim = (32768 + (int64_t)a.T * num_ranks - 1) / ((int64_t)a.T * num_ranks);
+            if (gx > lim) gx = lim;
+            if (gx < 1) gx = 1;
+            hipLaunchKernelGGL(k_apply_flat<LPR>, dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
+                               dim3(FLAT_TPB), 0, st, a);
+        });
+    }
     LAUNCH_CHECK();
     return launch_finalize(set, st);
 }

@@ -158,11 +158,12 @@ class EmbeddingTableSet:
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tflags = torch.zeros(T, dtype=torch.int32, device=dev)
         self.sdirty = torch.zeros(NS, dtype=torch.uint8, device=dev)
+        self.bdirty = torch.zeros(NB, dtype=torch.uint8, device=dev)
         self._c = L.TableSet(
             T, D, self.R, NB, NS,
             _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
             _ptr(self.tmax), _ptr(self.scale), _ptr(self.pscale), _ptr(self.meta), _ptr(self.err),
-            _ptr(self.tflags), _ptr(self.sdirty),
+            _ptr(self.tflags), _ptr(self.sdirty), _ptr(self.bdirty),
         )
         if weights is not None:
             if len(weights) != T:

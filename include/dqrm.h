@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 1
+#define DQRM_ABI_VERSION 2  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel */
 
 /* status codes */
 #define DQRM_OK            0
@@ -83,6 +83,7 @@ typedef struct dqrm_table_set {
     uint32_t* err;            /* 1 word, device-side error flags */
     uint32_t* tflags;         /* [T] scratch (repack decision), library-internal */
     uint8_t*  sdirty;         /* [NS] zero-initialised scratch (superblock rescan flags) */
+    uint8_t*  bdirty;         /* [NB] zero-initialised scratch (block rescan flags) */
 } dqrm_table_set;
 
 /* A batch of lookups for all T tables, in the reference's per-table
@@ -244,6 +245,18 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              int64_t cap_total, const void* payloads, size_t payload_bytes,
                              int num_ranks, int grad_bits, const float* s_avg, float lr,
                              int mode, int repack_bits, void* stream);
+
+/* Which kernel dqrm_apply_sparse_update launches (process-wide; returns the previous
+ * choice, or DQRM_E_INVALID). FLAT: one lane group per payload entry over the whole chip,
+ * rows located in the other ranks' sorted row lists by binary search; SLOT: one workgroup
+ * per (table, row-range slot), entries (row, rank) sorted in LDS. Both give bit-identical
+ * results. AUTO (default; the environment variable DQRM_APPLY=flat|slot overrides it)
+ * picks FLAT for num_ranks == 1 or num_ranks < dim/4 (one binary search per lane) and
+ * SLOT above, where the per-entry searches cost more than the slot sort. */
+#define DQRM_APPLY_AUTO 0
+#define DQRM_APPLY_FLAT 1
+#define DQRM_APPLY_SLOT 2
+int dqrm_set_apply_kernel(int kind);
 
 /* ---------------------------------------------------------------------------------
  * Dense (MLP) layer gradients, data-parallel:

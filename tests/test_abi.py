@@ -32,7 +32,7 @@ def test_header_declares_what_binding_expects():
 def test_library_exports_every_header_symbol(lib):
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.dqrm_abi_version() == 1
+    assert lib.dqrm_abi_version() == 2
 
 
 def test_payload_bytes_agree(lib):
@@ -41,8 +41,8 @@ def test_payload_bytes_agree(lib):
 
 
 def test_struct_layouts():
-    # dqrm_table_set: 2 x i32 + 3 x i64 + 12 pointers; dqrm_batch: 3 pointers + 2 x i64
-    assert C.sizeof(L.TableSet) == 8 + 24 + 12 * 8
+    # dqrm_table_set: 2 x i32 + 3 x i64 + 13 pointers; dqrm_batch: 3 pointers + 2 x i64
+    assert C.sizeof(L.TableSet) == 8 + 24 + 13 * 8
     assert C.sizeof(L.Batch) == 6 * 8
 
 
@@ -55,6 +55,17 @@ def test_invalid_arguments_rejected_without_device(lib):
     assert b"dim" in lib.dqrm_last_error()
     assert lib.dqrm_grad_quant_pack(0, 16, None, 0, None, None, None, None, 1, 8, None, 0, None, None, None) == L.DQRM_E_INVALID
     assert lib.dqrm_grad_quant_pack(2, 16, None, 0, None, None, None, None, 1, 37, None, 0, None, None, None) == L.DQRM_E_INVALID
+
+
+def test_apply_kernel_selector(lib):
+    prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_SLOT)
+    try:
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_SLOT
+        assert lib.dqrm_set_apply_kernel(3) == L.DQRM_E_INVALID
+        assert b"kind" in lib.dqrm_last_error()
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_AUTO) == L.DQRM_APPLY_FLAT
+    finally:
+        lib.dqrm_set_apply_kernel(prev)
 
 
 def test_slot_caps_partition():

@@ -29,6 +29,16 @@ def dq():
     return d
 
 
+@pytest.fixture(params=["flat", "slot"])
+def apply_kernel(request, dq):
+    """Run the test once per dqrm_apply_sparse_update kernel (the AUTO choice depends on N)."""
+    L = dq._lib
+    lib = L.load()
+    prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT if request.param == "flat" else L.DQRM_APPLY_SLOT)
+    yield request.param
+    lib.dqrm_set_apply_kernel(prev)
+
+
 def load(golden_dir, name):
     return dict(np.load(os.path.join(golden_dir, name)))
 
@@ -185,7 +195,7 @@ DP = ["dp_n2.npz", "dp_n4.npz", "dp_n4_zipf.npz", "dp_n2_fp32.npz", "dp_n2_b16.n
 
 
 @pytest.mark.parametrize("name", DP)
-def test_data_parallel_exchange_bitexact(dq, golden_dir, name):
+def test_data_parallel_exchange_bitexact(dq, golden_dir, name, apply_kernel):
     fx = load(golden_dir, name)
     num_rows = fx["num_rows"].tolist()
     D, seed, N, bits = int(fx["D"]), int(fx["seed"]), int(fx["N"]), int(fx["bits"])
@@ -214,7 +224,7 @@ def test_data_parallel_exchange_bitexact(dq, golden_dir, name):
         np.testing.assert_array_equal(ts.table_weight(t)[rows].cpu().numpy(), fx[f"w_t{t}"])
 
 
-def test_simulated_dp_bitexact(dq, golden_dir):
+def test_simulated_dp_bitexact(dq, golden_dir, apply_kernel):
     from deep_quantized_recommendation_model_dqrm_amd import _lib as L
 
     fx = load(golden_dir, "sim_dp.npz")
@@ -371,7 +381,7 @@ def test_slot_sort_and_segment_paths_bitexact(dq, D, dist):
 
 
 @pytest.mark.parametrize("grad_bits", [8, 32])
-def test_exchange_many_ranks_long_segments(dq, grad_bits):
+def test_exchange_many_ranks_long_segments(dq, grad_bits, apply_kernel):
     """N=12 emulated ranks: a row present in every rank's payload is a 12-entry segment in
     the apply kernel (the block-cooperative long-segment path); against oracle.dp_step."""
     rows, D, B, N = [3, 50, 2000], 32, 256, 12
@@ -389,6 +399,28 @@ def test_exchange_many_ranks_long_segments(dq, grad_bits):
     assert ts.read_errors() == 0
     for t in range(len(rows)):
         np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Ws[t])
+
+
+@pytest.mark.parametrize("N", [1, 3, 6])
+def test_apply_keeps_absmax_hierarchy_exact(dq, N, apply_kernel):
+    """After the DP apply (large steps, so block-max holders shrink and other rows grow), the
+    incrementally kept rowmax / block / superblock / table maxima equal a full rebuild from W
+    (the flat kernel's atomicMax growth + bdirty/sdirty rescans, the slot kernel's block pass)."""
+    rows, D, B = [7, 300, 70000, 400000], 16, 2048
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 41)
+    ts = make_set(dq, Ws)
+    Ps = [G.pooling_one(rows, B, 300 + r, dist="zipf" if r % 2 else "uniform") for r in range(N)]
+    dys = [G.upstream_grad(T, B, D, 400 + r) * 20 for r in range(N)]
+    rank_batches = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+    for it in range(3):
+        ts.forward(rank_batches[0])
+        _emulate_ranks(dq, ts, rank_batches, [torch.from_numpy(d).cuda() for d in dys], 8, 2.0 + it)
+        assert ts.read_errors() == 0
+        inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+        ts.refresh_absmax()
+        for a, b in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
 def test_pooling_one_flag_matches_offsets_path(dq):

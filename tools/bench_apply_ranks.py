@@ -1,0 +1,55 @@
+"""Time the DP update kernel (dqrm_apply_sparse_update: k_apply_flat and the per-slot
+k_table_apply, each + k_table_finalize) for N emulated ranks on
+one GPU: N different ranks' payloads (coalesce + quant-pack of N different batch slices)
+gathered into one buffer, exactly what the RCCL all-gather delivers at N GPUs.
+usage: python tools/bench_apply_ranks.py [terabyte|kaggle]   -> one JSON line per N"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden")]
+import deep_quantized_recommendation_model_dqrm_amd as dq  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd import _lib as L  # noqa: E402
+import gen_inputs as G  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "terabyte"
+D = 64 if cfg == "terabyte" else 16
+rows = [n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS] if cfg == "terabyte" else G.KAGGLE_ROWS
+B = 2048
+T = len(rows)
+ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
+ex = dq.SparseGradExchange(ts, B, grad_bits=8)
+lib = L.load()
+for mode, N in [(m, n) for m in ("flat", "slot") for n in (1, 2, 4, 8)]:
+    lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT if mode == "flat" else L.DQRM_APPLY_SLOT)
+    gathered = torch.zeros(N, ex.payload_bytes, dtype=torch.uint8, device="cuda")
+    for r in range(N):
+        P = torch.stack([torch.randint(0, n, (B,), device="cuda") for n in rows])
+        b = dq.LookupBatch.pooling_one(P)
+        dy = torch.randn(T, B, D, device="cuda") * 0.05
+        ts.forward(b)
+        ex.kernels.coalesce(b, dy, ex.ws, True, "tbd")
+        ex.kernels.quant_pack(ex.ws, ex.ws.absmax.view(1, -1), 1, 8, ex.cap_base, ex.cap_total, ex.s_avg, ex.payload)
+        gathered[r].copy_(ex.payload)
+
+    def run():
+        ex.kernels.apply(ex.cap_base, ex.cap_total, gathered, ex.payload_bytes, N, 8, ex.s_avg, 1e-3,
+                         L.DQRM_UPD_DP, False)
+
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
+    for a, c in ev:
+        a.record()
+        run()
+        c.record()
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    assert ts.read_errors() == 0
+    print(json.dumps({"kernel": f"apply_sparse_update ({mode}) + finalize", "config": cfg, "emulated_ranks": N,
+                      "ms": round(ms, 4)}), flush=True)
