@@ -7,6 +7,9 @@ A step = one pass of the hot path over one synthetic batch per rank:
   comm      RCCL all-gather of the [T] scales, quantize-pack to INT8       (K5)
             RCCL all-gather of the fixed-capacity {rows, int8} payloads
   update    decode all ranks' payloads, integer union-sum, dequant, SGD    (K6)
+At N=1 there is nothing to exchange: K5 + K6 run as one fused kernel (dqrm_apply_local:
+the same quantize, dequantize and SGD arithmetic, bit-identical W; --unfused-local runs the
+payload round trip instead).
 The MLP/interaction layers are outside the north-star path (SURVEY.md §8) and are not run;
 the upstream gradient dL/dy is a fixed synthetic tensor.
 
@@ -74,6 +77,8 @@ def parse():
     p.add_argument("--seed", type=int, default=123)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for measurements; gloo only to rehearse N>1 on one GPU")
+    p.add_argument("--unfused-local", action="store_true",
+                   help="N=1: run quant-pack + payload apply instead of the fused dqrm_apply_local")
     p.add_argument("--sample-every", type=int, default=8,
                    help="bracket the dominant kernel with HIP events on every k-th timed step")
     p.add_argument("--traffic-profile", default=None,
@@ -87,7 +92,8 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "emb_fwd": "k_emb_fwd<{lpr},",
     "bwd_coalesce": "k_table_bwd<{lpr}, 1>",
     "grad_quant_pack": "k_quant_pack<{lpr}>",
-    "apply_sparse_update": "k_table_apply<{lpr}>",
+    "apply_sparse_update": "k_apply_flat<{lpr}>",
+    "apply_local": "k_apply_local<{lpr}>",
 }
 
 
@@ -161,7 +167,11 @@ def main():
     torch.cuda.synchronize()
     setup_s = time.time() - t0
 
-    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
+    # N=1: quantize-pack + apply fused (dqrm_apply_local; same quantize/dequantize/SGD
+    # arithmetic, bit-identical W, no payload since nothing is exchanged)
+    fused = world == 1 and not a.unfused_local
+    names = (["emb_fwd", "bwd_coalesce", "apply_local"] if fused
+             else ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"])
 
     def step(i, ev=None, only=None):
         """One QAT step. ev: per-phase (start, end) events; only: bracket just that phase."""
@@ -177,6 +187,11 @@ def main():
         mark(1, 0)
         kern.coalesce(b, dy, ex.ws, True, "tbd")
         mark(1, 1)
+        if fused:
+            mark(2, 0)
+            kern.apply_local(ex.ws, a.grad_bits, ex.s_avg, a.lr, False)
+            mark(2, 1)
+            return
         if ex.world == 1:
             absmax_all = ex.ws.absmax.view(1, -1)
         else:
@@ -199,7 +214,7 @@ def main():
         step(i)
     # per-phase breakdown (untimed): every kernel bracketed by events; picks the dominant one
     nb = max(10, min(50, a.steps))
-    bev = [timed_events(4) for _ in range(nb)]
+    bev = [timed_events(len(names)) for _ in range(nb)]
     for i in range(nb):
         step(i, bev[i])
     torch.cuda.synchronize()
@@ -211,7 +226,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [timed_events(4) for _ in range(a.steps)]
+    evs = [timed_events(len(names)) for _ in range(a.steps)]
     sampled = [i for i in range(a.steps) if i % a.sample_every == 0]
     t_start = time.perf_counter()
     for i in range(a.steps):
@@ -234,6 +249,7 @@ def main():
         "bwd_coalesce": L_tot * 8 + T * B * 8 + L_tot * D * 4 + U * (D * 4 + 4),
         "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
         "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4,
+        "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4,
     }
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     err = ts.read_errors()

@@ -60,6 +60,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_grad_quant_pack_ranked",
     "dqrm_emb_local_update",
     "dqrm_apply_sparse_update",
+    "dqrm_apply_local",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
     "dqrm_dense_grad_quant",
@@ -182,6 +183,10 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_apply_sparse_update": (
             C.c_int,
             [TS, P, C.c_int64, P, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
+        ),
+        "dqrm_apply_local": (
+            C.c_int,
+            [TS, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P],
         ),
         "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
         "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),

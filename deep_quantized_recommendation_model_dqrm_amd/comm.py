@@ -77,6 +77,16 @@ class HipExchangeKernels:
             "dqrm_apply_sparse_update",
         )
 
+    def apply_local(self, ws, grad_bits, s_avg, lr, repack):
+        """world size 1: quant_pack + apply fused, straight from the workspace (no payload)."""
+        t = self.tables
+        L.check(
+            self.lib.dqrm_apply_local(
+                C.byref(t.c), _ptr(ws.slot_cap_base), ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount),
+                _ptr(ws.absmax), grad_bits, _ptr(s_avg), float(lr), 4 if repack else 0, _stream_handle()),
+            "dqrm_apply_local",
+        )
+
     def quant_pack_ranked(self, ws, table_bits, table_scale, cap_base, cap_total, payload):
         t = self.tables
         L.check(
@@ -178,7 +188,17 @@ class SparseGradExchange:
 
     def step(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
              mode: int | None = None, repack: bool = False, layout: str = "tbd") -> None:
-        """grad_update_parallel_comm + weight_update_parallel_comm for all tables."""
+        """grad_update_parallel_comm + weight_update_parallel_comm for all tables.
+
+        At world size 1 with quantized DP gradients the quantize-pack and the apply run as
+        one fused kernel (dqrm_apply_local, bit-identical; no payload is produced)."""
+        gb = self.grad_bits
+        fused = getattr(self.kernels, "apply_local", None)
+        if (fused is not None and self.world == 1 and 2 <= gb <= 16
+                and (mode is None or mode == L.DQRM_UPD_DP)):
+            self.kernels.coalesce(batch, dy, self.ws, ste, layout)
+            fused(self.ws, gb, self.s_avg, lr, repack)
+            return
         self.exchange(batch, dy, ste=ste, layout=layout)
         self.apply(lr, mode=mode, repack=repack)
 

@@ -1174,8 +1174,9 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
-                               int D) {
+                               int D, bool tracked) {
     __shared__ float red[16];
+    __shared__ int s_rescan;
     if (m.num_rows[t] <= BLK) {
         const int64_t grow = m.row_base[t] + threadIdx.x;
         float v = 0.0f;
@@ -1203,6 +1204,11 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
     constexpr int U4 = 4;  // loads in flight per thread
+    // tracked (flat apply kernels): tmax already holds every grown row max (atomicMax), so
+    // the table-wide rescan is needed only if a rescanned superblock held the table max
+    const float tmax0 = tracked ? tmax[t] : 0.0f;
+    if (threadIdx.x == 0) s_rescan = tracked ? 0 : 1;
+    __syncthreads();
     for (int64_t k0 = (int64_t)w * WAVE * U4; k0 < ns; k0 += (int64_t)nw * WAVE * U4) {
         bool d[U4];
 #pragma unroll
@@ -1220,13 +1226,18 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
                 const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
                 // blocks the flat apply flagged (a max holder shrank): re-reduce their 256 rowmax
                 // (wave-cooperative; the owning lane keeps the new value in a register)
+                // the superblock's dirty flags, block maxima and old max in one round trip
                 float nv[SBLK_BLOCKS / WAVE];
                 bool dq[SBLK_BLOCKS / WAVE];
+                const float old_sb = sblkmax[sbb + sb];
 #pragma unroll
                 for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
                     const int64_t b = b0 + lane + q * WAVE;
                     dq[q] = b < b1 && bdirty[bb + b];
-                    nv[q] = 0.0f;
+                    nv[q] = b < b1 ? blkmax[bb + b] : 0.0f;
+                }
+#pragma unroll
+                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
                     uint64_t dm = __ballot(dq[q]);
                     while (dm) {
                         const int dl = __ffsll((long long)dm) - 1;
@@ -1241,20 +1252,22 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
                         x = wave_max(x);
                         if (lane == dl) nv[q] = x;
                     }
-                    if (dq[q]) { blkmax[bb + b] = nv[q]; bdirty[bb + b] = 0; }
+                    if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; bdirty[b0 + lane + q * WAVE + bb] = 0; }
                 }
                 float v = 0.0f;
 #pragma unroll
-                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-                    const int64_t b = b0 + lane + q * WAVE;
-                    if (b < b1) v = fmaxf(v, dq[q] ? nv[q] : blkmax[bb + b]);
-                }
+                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
                 v = wave_max(v);
-                if (lane == 0) { sblkmax[sbb + sb] = v; sdirty[sbb + sb] = 0; }
+                if (lane == 0) {
+                    sblkmax[sbb + sb] = v;
+                    sdirty[sbb + sb] = 0;
+                    if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
+                }
             }
         }
     }
     __syncthreads();
+    if (!s_rescan) return;  // uniform: tmax is exact already
     float v = 0.0f;
     for (int64_t k0 = threadIdx.x; k0 < ns; k0 += (int64_t)blockDim.x * U4) {
         float x[U4];
@@ -1283,9 +1296,10 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
                                                          float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                                          uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty,
                                                          float* __restrict__ tmax,
-                                                         const int64_t* __restrict__ meta, int T, int D) {
+                                                         const int64_t* __restrict__ meta, int T, int D,
+                                                         int tracked) {
     const Meta m = make_meta(meta, T);
-    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D);
+    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -1808,6 +1822,7 @@ struct ApplyArgs {
     float* sblkmax;
     uint8_t* sdirty;
     uint8_t* bdirty;
+    float* tmax;
     const float* pscale;
     const int64_t* meta;
     uint32_t* err;
@@ -2066,6 +2081,93 @@ DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
 
 constexpr int FLAT_TPB = 256;
 
+// SGD of row x (global row grow) by one LPR-lane group with the summed value acc, rowmax,
+// and the exact |W| hierarchy without a per-block pass: growth goes in with an order-free
+// atomicMax on the non-negative float bits; a row that held its block's max and shrank
+// flags the block (bdirty) and its superblock (sdirty) for finalize's re-reduction. Rows
+// of one call are distinct, so a concurrent grower either raised old_blk before this row
+// read it (then the block max is that grower's current value) or the holder is flagged.
+template <int LPR>
+DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
+                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub) {
+    constexpr int D = LPR * 4;
+    const int64_t blk = x >> 8;
+    const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+    const float old_blk = a.blkmax[bb + blk];
+    float4 w;
+    w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
+    w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
+    reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+    if (a.repack) pack4_row(w, a.packed + grow * (D / 2), sub, r_pack);
+    const float old_rm = group_max<LPR>(abs_max4(w0));
+    const float rm = group_max<LPR>(abs_max4(w));
+    if (sub == 0) {
+        a.rowmax[grow] = rm;
+        if (nrows > BLK) {  // narrow tables are rebuilt from W by finalize
+            const int64_t sb = sbb + (blk >> 8);
+            if (rm > old_blk) {
+                atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
+                if (rm > a.sblkmax[sb]) {
+                    atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
+                    if (rm > a.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
+                }
+            }
+            if (old_rm == old_blk && rm < old_rm) {
+                a.bdirty[bb + blk] = 1;
+                a.sdirty[sb] = 1;
+            }
+        }
+    }
+}
+
+// Single-rank DP step, quantize-pack and apply fused (dqrm_apply_local): grid (entry
+// chunks, T * SPLIT workspace slots). Every workgroup derives table t's scale from the
+// slots' max|grad| exactly as k_quant_pack does for N = 1 (s = sym_scale(max) * 1.0f),
+// quantizes its coalesced entries with k_quant_pack's rounding and applies them with
+// k_apply_flat's update: the same values the payload round trip produces, without
+// writing and re-reading the payload.
+template <int LPR>
+__global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int64_t* __restrict__ ws_cap_base,
+                                                          const int32_t* __restrict__ ws_rows,
+                                                          const float* __restrict__ ws_vals,
+                                                          const int32_t* __restrict__ ws_ucount,
+                                                          const float* __restrict__ ws_absmax,
+                                                          float* __restrict__ s_avg) {
+    constexpr int D = LPR * 4;
+    constexpr int G = FLAT_TPB / LPR;
+    const int k = blockIdx.y, t = k / SPLIT;
+    const int64_t cap = ws_cap_base[k + 1] - ws_cap_base[k];
+    int cnt = ws_ucount[k];
+    cnt = cnt < 0 ? 0 : (cnt > cap ? (int)cap : cnt);
+    const bool writer = blockIdx.x == 0 && k % SPLIT == 0;  // s_avg[t], even for an empty slot
+    if ((int64_t)blockIdx.x * G >= cnt && !writer) return;
+    float am = 0.0f;
+    for (int ss = 0; ss < SPLIT; ++ss) am = fmaxf(am, ws_absmax[t * SPLIT + ss]);
+    const float sv = sym_scale(am, a.bits) * (float)(1.0 / 1.0);
+    if (writer && threadIdx.x == 0) s_avg[t] = sv;
+    if ((int64_t)blockIdx.x * G >= cnt) return;
+    const Meta m = make_meta(a.meta, a.T);
+    const float rr = 1.0f / sv;
+    const float qlo = -(float)(1 << (a.bits - 1)), qhi = (float)((1 << (a.bits - 1)) - 1);
+    const ApplyUpdate update{DQRM_UPD_DP, 1.0f, sv, sv, a.nlr};
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    const int64_t src0 = ws_cap_base[k];
+    const int sub = threadIdx.x % LPR;
+    for (int e = blockIdx.x * G + threadIdx.x / LPR; e < cnt; e += gridDim.x * G) {
+        const int32_t x = ws_rows[src0 + e];
+        const float4 v = reinterpret_cast<const float4*>(ws_vals + (src0 + e) * D)[sub];
+        if (x < 0 || x >= nrows) {  // cannot happen for a workspace this library coalesced
+            if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+            continue;
+        }
+        float4 acc;  // + 0.0f: the payload's integer round trip turns -0 into +0
+        acc.x = fake_quant(v.x, rr, qlo, qhi) + 0.0f; acc.y = fake_quant(v.y, rr, qlo, qhi) + 0.0f;
+        acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
+    }
+}
+
 template <int LPR>
 __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     constexpr int D = LPR * 4;
@@ -2119,31 +2221,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
                 if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
             }
         }
-        const int64_t grow = rb + x;
-        const int64_t blk = x >> 8;
-        const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
-        const float old_blk = a.blkmax[bb + blk];
-        float4 w;
-        w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
-        w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
-        reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
-        if (a.repack) pack4_row(w, a.packed + grow * (D / 2), sub, r_pack);
-        const float old_rm = group_max<LPR>(abs_max4(w0));
-        const float rm = group_max<LPR>(abs_max4(w));
-        if (sub == 0) {
-            a.rowmax[grow] = rm;
-            if (nrows > BLK) {  // narrow tables are rebuilt from W by finalize
-                const int64_t sb = sbb + (blk >> 8);
-                if (rm > old_blk) {
-                    atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
-                    if (rm > a.sblkmax[sb]) atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
-                }
-                if (old_rm == old_blk && rm < old_rm) {
-                    a.bdirty[bb + blk] = 1;
-                    a.sdirty[sb] = 1;
-                }
-            }
-        }
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
     }
 }
 
@@ -2305,11 +2383,12 @@ int check_set(const dqrm_table_set* s) {
     return DQRM_OK;
 }
 
-int launch_finalize(const dqrm_table_set* set, hipStream_t st) {
+// tracked: the preceding kernel raised tmax for every grown row (the flat apply kernels)
+int launch_finalize(const dqrm_table_set* set, hipStream_t st, bool tracked = false) {
     static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
     hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
                        set->blkmax, set->sblkmax, set->sdirty, set->bdirty, set->tmax, set->meta, set->num_tables,
-                       set->dim);
+                       set->dim, tracked ? 1 : 0);
     LAUNCH_CHECK();
     return DQRM_OK;
 }
@@ -2688,10 +2767,11 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
     a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
     a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)payload_bytes;
     a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
-    a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty;
+    a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty; a.tmax = set->tmax;
     hipStream_t st = (hipStream_t)stream;
     const int D = set->dim;
     const int kind = apply_kernel_kind();
+    bool flat = false;
     // AUTO: flat while each lane of a row's group searches at most one other rank
     // (num_ranks < D/4), slot beyond (tools/bench_apply_ranks.py)
     if (kind == DQRM_APPLY_SLOT || (kind == DQRM_APPLY_AUTO && num_ranks > 1 && num_ranks >= D / 4)) {
@@ -2700,6 +2780,7 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
             hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
         });
     } else {
+        flat = true;
         // grid (entry chunks, tables, ranks): twice the chunks of an average table (the
         // per-table capacities live on the device); larger tables grid-stride, chunks past
         // a table's count exit at once
@@ -2714,7 +2795,42 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
         });
     }
     LAUNCH_CHECK();
-    return launch_finalize(set, st);
+    return launch_finalize(set, st, flat);
+}
+
+int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                     const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                     const float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                     void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if (grad_bits < 2 || grad_bits > 16)
+        return set_error(DQRM_E_INVALID, "%s: grad_bits must be 2..16 (got %d)", "dqrm_apply_local", grad_bits);
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !ws_absmax || !s_avg || ws_cap_total < 0)
+        return set_error(DQRM_E_INVALID, "%s: null workspace pointer", "dqrm_apply_local");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_apply_local", repack_bits);
+    ApplyArgs a{};
+    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
+    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.bdirty = set->bdirty; a.tmax = set->tmax; a.pscale = set->pscale;
+    a.meta = set->meta; a.err = set->err; a.N = 1; a.T = set->num_tables; a.bits = grad_bits;
+    a.s_avg = s_avg; a.nlr = -lr; a.mode = DQRM_UPD_DP; a.repack = repack_bits == 4;
+    hipStream_t st = (hipStream_t)stream;
+    const int D = set->dim;
+    const int64_t slots = (int64_t)a.T * SPLIT;
+    DISPATCH_LPR(D, {
+        // grid (entry chunks, slots): enough chunks for a slot at its mean capacity, slots
+        // with fewer entries exit at once, fuller ones grid-stride
+        constexpr int G = FLAT_TPB / LPR;
+        int64_t gx = (ws_cap_total / (slots > 0 ? slots : 1) + G - 1) / G;
+        const int64_t lim = (32768 + slots - 1) / (slots > 0 ? slots : 1);
+        if (gx > lim) gx = lim;
+        if (gx < 1) gx = 1;
+        hipLaunchKernelGGL(k_apply_local<LPR>, dim3((unsigned)gx, (unsigned)slots), dim3(FLAT_TPB), 0, st, a,
+                           ws_cap_base, ws_rows, ws_vals, ws_ucount, ws_absmax, s_avg);
+    });
+    LAUNCH_CHECK();
+    return launch_finalize(set, st, true);
 }
 
 int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {

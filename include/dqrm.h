@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 2  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel */
+#define DQRM_ABI_VERSION 2  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local */
 
 /* status codes */
 #define DQRM_OK            0
@@ -245,6 +245,18 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              int64_t cap_total, const void* payloads, size_t payload_bytes,
                              int num_ranks, int grad_bits, const float* s_avg, float lr,
                              int mode, int repack_bits, void* stream);
+
+/* Single-rank DP step (num_ranks == 1, mode DQRM_UPD_DP), dqrm_grad_quant_pack and
+ * dqrm_apply_sparse_update fused: the table scale s = clamp(max_s ws_absmax[t*S+s], 1e-8)
+ * / (2^(bits-1)-1) (-> s_avg[t]), q = quantize(v, s) per coalesced entry, and
+ * W += -lr * ((q * 1) * s) straight from the coalesce workspace, with the same rounding
+ * as the payload round trip (bit-identical W, rowmax/blkmax/sblkmax/tmax, s_avg and,
+ * with repack_bits == 4, packed rows). No payload is written. Replaces, at world size 1,
+ * quantize_emb_grad (s_q_g_p_c.py:861-869) + weight_update_parallel_comm (:601-628). */
+int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                     const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                     const float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                     void* stream);
 
 /* Which kernel dqrm_apply_sparse_update launches (process-wide; returns the previous
  * choice, or DQRM_E_INVALID). FLAT: one lane group per payload entry over the whole chip,

@@ -423,6 +423,58 @@ def test_apply_keeps_absmax_hierarchy_exact(dq, N, apply_kernel):
             torch.testing.assert_close(a, b, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("D,bits,repack", [(16, 8, False), (64, 8, True), (32, 4, False), (64, 16, False)])
+def test_fused_local_apply_matches_payload_path_and_oracle(dq, D, bits, repack):
+    """dqrm_apply_local (world size 1: quant-pack + apply fused) against the payload round
+    trip (coalesce -> quant_pack -> apply) on a copy of the same tables, bit for bit (W,
+    packed rows, s_avg and the |W| hierarchy), and against oracle.dp_step with N = 1."""
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels, payload_bytes
+
+    rows, B = [3, 200, 5000, 300000], 1024
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 51)
+    P = G.pooling_one(rows, B, 52, dist="zipf")
+    dy = G.upstream_grad(T, B, D, 53) * 10
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+    sets = [make_set(dq, Ws, packed=repack) for _ in range(2)]
+    s_avg = [torch.zeros(T, dtype=torch.float32, device="cuda") for _ in range(2)]
+    caps = dq.default_caps(rows, B)
+    cap_base = torch.tensor(np.concatenate([[0], np.cumsum(caps)]), dtype=torch.int64, device="cuda")
+    cap_total = int(sum(caps))
+    Pb = payload_bytes(T, cap_total, D, bits)
+    payload = torch.zeros(1, Pb, dtype=torch.uint8, device="cuda")
+    for it in range(3):
+        for j, ts in enumerate(sets):
+            if repack:
+                ts.refresh_scale_and_pack(4)
+            ts.forward(b)
+            k = HipExchangeKernels(ts)
+            ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+            k.coalesce(b, torch.from_numpy(dy).cuda(), ws, True, "tbd")
+            if j == 0:
+                k.apply_local(ws, bits, s_avg[0], 0.5, repack)
+            else:
+                k.quant_pack(ws, ws.absmax.view(1, -1), 1, bits, cap_base, cap_total, s_avg[1], payload[0])
+                k.apply(cap_base, cap_total, payload, Pb, 1, bits, s_avg[1], 0.5, L.DQRM_UPD_DP, repack)
+        assert torch.equal(s_avg[0], s_avg[1])
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax") + (("packed",) if repack else ()):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), name
+    assert sets[0].read_errors() == 0
+    # one more fused step against the oracle's DP update with N = 1
+    ts = make_set(dq, Ws)
+    ts.forward(b)
+    s_fwd = ts.scale.cpu().numpy()
+    ex = dq.SparseGradExchange(ts, B, grad_bits=bits)
+    ex.step(b, torch.from_numpy(dy).cuda(), lr=0.5)
+    ar = np.arange(B, dtype=np.int64)
+    Wo = [w.copy() for w in Ws]
+    O.dp_step(Wo, [[(P[t], ar) for t in range(T)]], [[dy[t] for t in range(T)]], s_fwd, 0.5, grad_bits=bits)
+    assert ts.read_errors() == 0
+    for t in range(T):
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Wo[t])
+
+
 def test_pooling_one_flag_matches_offsets_path(dq):
     """DQRM_BATCH_POOLING_ONE (offsets not read) gives the same forward, SGD and coalesce as
     the general offsets path on the same Criteo-form batch."""
