@@ -1239,18 +1239,32 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
 #pragma unroll
                 for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
                     uint64_t dm = __ballot(dq[q]);
-                    while (dm) {
-                        const int dl = __ffsll((long long)dm) - 1;
-                        dm &= dm - 1;
-                        const int64_t blk = b0 + q * WAVE + dl;
-                        float x = 0.0f;
+                    while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
+                        constexpr int DB = 8;
+                        int dl[DB];
+                        float x[DB];
 #pragma unroll
-                        for (int k = 0; k < BLK / WAVE; ++k) {
-                            const int64_t rr = blk * BLK + lane + k * WAVE;
-                            if (rr < m.num_rows[t]) x = fmaxf(x, rowmax[m.row_base[t] + rr]);
+                        for (int i = 0; i < DB; ++i) {
+                            dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
+                            dm &= dm ? dm - 1 : 0;
                         }
-                        x = wave_max(x);
-                        if (lane == dl) nv[q] = x;
+#pragma unroll
+                        for (int i = 0; i < DB; ++i) {
+                            x[i] = 0.0f;
+                            if (dl[i] < 0) continue;
+                            const int64_t blk = b0 + q * WAVE + dl[i];
+#pragma unroll
+                            for (int k = 0; k < BLK / WAVE; ++k) {
+                                const int64_t rr = blk * BLK + lane + k * WAVE;
+                                if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], rowmax[m.row_base[t] + rr]);
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < DB; ++i) {
+                            if (dl[i] < 0) continue;
+                            const float y = wave_max(x[i]);
+                            if (lane == dl[i]) nv[q] = y;
+                        }
                     }
                     if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; bdirty[b0 + lane + q * WAVE + bb] = 0; }
                 }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 run of bench.py (tools/prof_r1.sh) into profiles/:
+"""Summarise a rocprofv3 run of bench.py (tools/prof_cfg.sh) into profiles/:
 
   <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim copy)
   <tag>_summary.json       per libdqrm kernel: calls, average duration (us), and the
@@ -8,7 +8,7 @@
                            reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, in bytes.
 bench.py reads <tag>_summary.json (if present) to fill roofline.traffic.
 
-usage: python tools/prof_summary.py gpurun_out/prof_r1 profiles/r1_tb
+usage: python tools/prof_summary.py gpurun_out/prof_tb profiles/r1_tb
 """
 import collections
 import csv
