@@ -279,8 +279,8 @@ def main():
 
     mlp = dense_phase(a, dev, world, rank) if a.mlp_iters > 0 else None
 
-    cpu = None
-    if rank == 0 and a.cpu_baseline:
+    cpu = None  # the CPU baseline is an N=1 figure: rank 0 of a single-rank run only
+    if world == 1 and a.cpu_baseline:
         cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
 
     # replicas must stay bit-identical (deterministic kernels, same exchanged data): compare a
