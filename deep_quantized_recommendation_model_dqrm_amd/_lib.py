@@ -47,11 +47,14 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
+DQRM_ABI_VERSION = 3  # include/dqrm.h
+
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
     "dqrm_refresh_absmax",
     "dqrm_refresh_scale_and_pack",
     "dqrm_emb_fwd",
+    "dqrm_bwd_workspace_bytes",
     "dqrm_emb_bwd_sgd",
     "dqrm_coalesce_slot_caps",
     "dqrm_emb_bwd_coalesce",
@@ -161,11 +164,14 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_refresh_absmax": (C.c_int, [TS, P]),
         "dqrm_refresh_scale_and_pack": (C.c_int, [TS, C.c_int, P]),
         "dqrm_emb_fwd": (C.c_int, [TS, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P]),
-        "dqrm_emb_bwd_sgd": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P]),
+        "dqrm_bwd_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int64]),
+        "dqrm_emb_bwd_sgd": (
+            C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P, C.c_size_t, P]
+        ),
         "dqrm_coalesce_slot_caps": (C.c_int64, [P, C.c_int, C.c_int64, P]),
         "dqrm_emb_bwd_coalesce": (
             C.c_int,
-            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, P],
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, P, C.c_size_t, P],
         ),
         "dqrm_payload_bytes": (C.c_size_t, [C.c_int, C.c_int64, C.c_int, C.c_int]),
         "dqrm_grad_quant_pack": (
@@ -178,7 +184,7 @@ def load(path: str | None = None) -> C.CDLL:
         ),
         "dqrm_emb_local_update": (
             C.c_int,
-            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, P, C.c_int, P],
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, P, C.c_int, P, C.c_size_t, P],
         ),
         "dqrm_apply_sparse_update": (
             C.c_int,
@@ -210,6 +216,12 @@ def load(path: str | None = None) -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    got = lib.dqrm_abi_version()
+    if got != DQRM_ABI_VERSION:  # a stale build would be called with the wrong argument lists
+        raise DQRMError(
+            f"{path} has ABI version {got}, this package needs {DQRM_ABI_VERSION}: rebuild it with "
+            "`python -m deep_quantized_recommendation_model_dqrm_amd._build`"
+        )
     _lib = lib
     return lib
 

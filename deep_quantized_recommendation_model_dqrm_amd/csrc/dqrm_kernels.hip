@@ -39,6 +39,12 @@ __device__ unsigned long long g_diag_clk[8192 * 16];
 #else
 #define DIAG_T(k) do { } while (0)
 #endif
+// diagnostic stamp after every outstanding memory operation of the thread has landed
+#ifdef DQRM_DIAG_CLOCK
+#define DIAG_W(k) do { __builtin_amdgcn_s_waitcnt(0); DIAG_T(k); } while (0)
+#else
+#define DIAG_W(k) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------------------------
 // error reporting (host)
@@ -1977,6 +1983,64 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
     if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, s_wsum + TWG / WAVE + 2);
 }
 
+DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x);
+template <int LPR>
+DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
+                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub);
+
+// A slot whose merged entries exceed SLOT_KEYS (LDS sort capacity): k_apply_flat's method
+// restricted to the slot. Every rank's slot rows are ascending, so the entry of row x in
+// rank j is a binary search of rank j's slot range; the lowest rank holding x owns the row
+// and sums the ranks' values in ascending rank order (= the sorted path's order).
+template <int LPR>
+DQRM_INLINE void apply_slot_flat(const ApplyArgs& a, const Meta& m, int t, const PayloadLayout& pl, const int* s_e0,
+                                 const int* s_start, int* pos_lds) {
+    constexpr int NG = TWG / LPR;
+    const int N = a.N;
+    const int64_t cb = a.cap_base[t];
+    const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const ApplyUpdate update{a.mode, (float)(1.0 / (double)N), sc, (float)((double)sc / (double)N), a.nlr};
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    const PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, cb, 0};
+    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int gbase = (threadIdx.x % WAVE) - sub;
+    const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
+    int* pos = pos_lds + grp * DQRM_MAX_RANKS;  // LDS, written and read back by the same wave
+    auto rows_of = [&](int j) {
+        return reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes + pl.rows_off) + cb;
+    };
+    const int M = s_start[N];
+    for (int i = grp; i < M; i += NG) {
+        int r = 0;
+        while (i >= s_start[r + 1]) ++r;
+        const int e = s_e0[r] + (i - s_start[r]);
+        const int32_t x = rows_of(r)[e];
+        if (x < 0 || x >= nrows) {  // cannot happen for payloads this library packed
+            if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+            continue;
+        }
+        bool lower = false;
+        for (int j = sub; j < N; j += LPR) {
+            int p = e;
+            if (j != r) {
+                const int q = find_row(rows_of(j) + s_e0[j], s_start[j + 1] - s_start[j], x);
+                p = q >= 0 ? s_e0[j] + q : -1;
+                lower |= (j < r) && p >= 0;
+            }
+            pos[j] = p;
+        }
+        if (__ballot(lower) & gmask) continue;  // a lower rank owns this row (group-uniform)
+        bool first = true;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = r; j < N; ++j) {
+            const int p = pos[j];
+            if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
+        }
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
+    }
+}
+
 template <int LPR>
 __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -2032,8 +2096,8 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     }
     __syncthreads();
     const int M = s_start[a.N];
-    if (M > SLOT_KEYS) {  // uniform: whole workgroup leaves
-        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+    if (M > SLOT_KEYS) {  // crowded slot (uniform): the flat method over its entries, full rows
+        if (off4 == 0) apply_slot_flat<LPR>(a, m, t, pl, s_e0, s_start, reinterpret_cast<int*>(lds));
         return;
     }
     for (int i = threadIdx.x; i < M; i += blockDim.x) {
@@ -2237,6 +2301,1008 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
         }
         flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
     }
+}
+
+// ------------------------------------------------------------------------------------
+// K4: backward = STE (quant_utils.py:349-363) + EmbeddingBag sparse backward, then one of
+//   MODE 0  torch.optim.SGD on the uncoalesced grad        (dlrm_s_pytorch_single_gpu.py:1736-1750)
+//   MODE 1  grad.coalesce() + per-slot max|grad|           (s_q_g_p_c.py:859-861)
+//   MODE 2  W.add_(-lr * grad), product rounded            (s_q_g_p_c.py:615-616, ranking range)
+// in two launches, with no per-batch capacity:
+//   K4a k_sort_slots   one 512-thread workgroup per (table, row-range slot): the slot's valid
+//       lookups as keys (row << 32 | bag) in lookup order (a stable ballot compaction of the
+//       table's lookups), a stable LSD radix sort by row (8-bit digits, wave-ballot ranks;
+//       in LDS up to SORT_LDS_KEYS keys, in the caller's workspace beyond), then one 32-byte
+//       record per distinct row {row, bags 1..4, slot, length, coalesced-workspace entry}
+//       APPENDED to a chip-wide record list (the slot reserves its run with one atomicAdd),
+//       and the slot's long segments with one work item per long-stream chunk and dimension
+//       slice. The last workgroup to finish publishes the list lengths and re-arms the
+//       counters (the workspace's counters are zero between calls).
+//   K4b k_bwd_segments  one float4 lane group per short record (<= LONG_SEG lookups: nearly
+//       every row of a wide table), SEG_SB records in flight, straight from the record list
+//       (record -> dy rows: two round trips); long items (hot rows of narrow / power-law
+//       tables) stream their lookups through an LDS stage, each segment combined strictly
+//       in lookup order by one dim-lane group that carries its running row across stage
+//       chunks, the D dimensions split over DS work items (independent chains, so a 3-row
+//       table's 700-lookup chains run on 3 x DS CUs).
+// Every row's lookups are combined in ascending lookup order, as the reference's torch
+// ops accumulate duplicates (sparse SGD axpy / coalesce); the list order (atomic) never
+// reaches a result. Wide-table SGD keeps the |W| hierarchy with the flat protocol (atomicMax
+// growth, dirty flags for shrunk holders, tracked finalize); narrow tables are rebuilt by
+// finalize.
+// ------------------------------------------------------------------------------------
+constexpr int SORT_TPB = 512;
+constexpr int SORT_WAVES = SORT_TPB / WAVE;
+constexpr int SORT_LDS_KEYS = 4096;                 // keys a slot sorts in LDS (32 KiB + 32 KiB)
+constexpr int SORT_KC = SORT_LDS_KEYS / SORT_TPB;   // key batches per lane cached in registers
+constexpr int RADIX = 256;
+constexpr int HP = SORT_WAVES + 1;                  // [digit][wave] counter pitch (odd: no bank conflicts)
+constexpr int SORT_LDS = SORT_LDS_KEYS * 16 + RADIX * HP * 4;
+static_assert(SORT_LDS + 2048 <= 160 * 1024, "sort LDS budget");
+constexpr int LONG_RANGE = 512;   // long-stream lookups whose segments one long item owns
+constexpr int SEG_TPB = 256;
+constexpr int SEG_SB = 4;         // short records in flight per lane group
+constexpr int LSTAGE = 4096;      // floats of the long-segment LDS stage (16 KiB, + pad)
+constexpr int LMAXK = LONG_RANGE / (LONG_SEG + 1) + 2;
+constexpr int DS_MAX = 8;
+constexpr int LONG_WGS = 256;     // K4b workgroups looping over the long items
+constexpr uint32_t REC_LEN_MAX = (1u << 21) - 1;
+
+template <int LPR>
+struct SegGeom {
+    static constexpr int D = LPR * 4;
+    static constexpr int DS = LPR < DS_MAX ? LPR : DS_MAX;  // dim slices of a long segment (>= 4 dims)
+    static constexpr int NG = SEG_TPB / LPR;                 // float4 lane groups
+    static constexpr int US = NG * SEG_SB;                   // records per short workgroup
+};
+
+struct SortWs {
+    uint64_t* skey;   // [T*S][Lc] every slot's sorted keys (row << 32 | bag)
+    uint64_t* skey2;  // [T*S][Lc] radix ping-pong (only when Lc > SORT_LDS_KEYS)
+    uint4* rec;       // [T*Lc] record list: {row, bag0, slot | min(len, REC_LEN_MAX) << 11, ws entry}
+    uint4* rbag;      // [T*Lc] {bag1, bag2, bag3, first key} (length > 1)
+    uint4* lrec;      // [T*S][Lc] every slot's long segments in order: {row, first key, record or
+                      //            ws entry (MODE 1), long-stream start}
+    uint4* litem;     // [NLI] long items {slot | slice << 16, first, end, stream end}
+    uint32_t* ctr;    // [8] {records, long items, slots done, records (final), long items (final)}
+    int64_t nli;      // long-item capacity
+};
+
+__host__ __device__ inline int64_t long_item_cap(int T, int64_t Lc) {
+    return ((int64_t)T * SPLIT + (int64_t)T * ((Lc + LONG_RANGE - 1) / LONG_RANGE)) * DS_MAX;
+}
+
+// byte layout of the backward workspace (base == nullptr: sizes only); returns its bytes
+__host__ __device__ inline int64_t sort_ws_layout(unsigned char* base, int T, int64_t Lc, SortWs* ws) {
+    int64_t o = 0;
+    auto take = [&](int64_t bytes) {
+        const int64_t p = o;
+        o += align16(bytes);
+        return base ? base + p : nullptr;
+    };
+    const int64_t TL = (int64_t)T * Lc, TSL = TL * SPLIT;
+    SortWs w;
+    w.ctr = reinterpret_cast<uint32_t*>(take(64));
+    w.skey = reinterpret_cast<uint64_t*>(take(TSL * 8));
+    w.skey2 = reinterpret_cast<uint64_t*>(take(Lc > SORT_LDS_KEYS ? TSL * 8 : 0));
+    w.rec = reinterpret_cast<uint4*>(take(TL * 16));
+    w.rbag = reinterpret_cast<uint4*>(take(TL * 16));
+    w.lrec = reinterpret_cast<uint4*>(take(TSL * 16));
+    w.nli = long_item_cap(T, Lc);
+    w.litem = reinterpret_cast<uint4*>(take(w.nli * 16));
+    if (ws) *ws = w;
+    return o;
+}
+
+// exclusive prefix of one int per thread over NT threads; *total = the sum.
+// s_w: NT/WAVE + 1 ints. Two barriers.
+template <int NT>
+DQRM_INLINE int block_scan_excl(int cnt, int* s_w, int* total) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    int v = cnt;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int y = __shfl_up(v, o, WAVE);
+        if (lane >= o) v += y;
+    }
+    if (lane == WAVE - 1) s_w[w] = v;
+    __syncthreads();
+    if (w == 0) {  // wave 0 scans the NT/WAVE wave totals
+        constexpr int NW = NT / WAVE;
+        const int x = lane < NW ? s_w[lane] : 0;
+        int y = x;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            const int z = __shfl_up(y, o, WAVE);
+            if (lane >= o) y += z;
+        }
+        if (lane < NW) s_w[lane] = y - x;
+        if (lane == NW - 1) s_w[NW] = y;
+    }
+    __syncthreads();
+    *total = s_w[NT / WAVE];
+    return s_w[w] + v - cnt;
+}
+
+// lanes of the wave whose 8-bit digit equals v, from the eight bit-slice ballots
+DQRM_INLINE uint64_t digit_lanes8(uint32_t v, const uint64_t (&b)[8]) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m &= ((v >> k) & 1u) ? b[k] : ~b[k];
+    return m;
+}
+
+// one wave-batch of 64 keys: the key, its digit, and the lanes sharing it (incl. itself)
+DQRM_INLINE void radix_batch(const uint64_t* src, int i, int n, uint32_t r0, int sh, uint64_t& x, uint32_t& d,
+                             uint64_t& mine) {
+    const bool v = i < n;
+    x = v ? src[i] : 0ull;
+    d = ((key_row(x) - r0) >> sh) & 255u;
+    uint64_t b[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) b[q] = __ballot((d >> q) & 1u);
+    mine = digit_lanes8(d, b) & __ballot(v);
+}
+
+// Stable LSD radix sort of keys[0, n) by row - r0 (bits [0, nbits)), 8-bit digits. Wave w
+// owns keys [w*64*kpl, (w+1)*64*kpl), 64 at a time. Per pass: each batch's same-digit lanes
+// come from eight bit-slice ballots; the last lane of a digit adds the batch's count to the
+// wave's [digit][wave] counter (its own LDS column: no barrier); one block scan turns the
+// counters into bases, and every lane places its key at its base plus the earlier same-digit
+// lanes, the last one advancing the base. Up to SORT_KC batches per lane stay in registers
+// between the count and the scatter. keys / tmp: LDS or global.
+DQRM_INLINE void radix_sort_rows(uint64_t* keys, uint64_t* tmp, int n, uint32_t r0, int nbits, int* hist,
+                                 int* s_scan) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const int kpl = (n + SORT_TPB - 1) / SORT_TPB;
+    const int i0 = w * WAVE * kpl + lane;
+    const uint64_t lt = lanemask_lt();
+    const bool cached = kpl <= SORT_KC;
+    uint64_t* src = keys;
+    uint64_t* dst = tmp;
+    for (int sh = 0; sh < nbits; sh += 8) {
+        for (int j = threadIdx.x; j < RADIX * HP; j += SORT_TPB) hist[j] = 0;
+        __syncthreads();
+        uint64_t cx[SORT_KC], cm[SORT_KC];
+        uint32_t cd[SORT_KC];
+        auto count = [&](int i, uint32_t d, uint64_t mine) {
+            if (i < n && (mine >> lane) == 1ull) hist[d * HP + w] += (int)__popcll(mine);
+        };
+        if (cached) {
+#pragma unroll
+            for (int k = 0; k < SORT_KC; ++k)
+                if (k < kpl) {
+                    radix_batch(src, i0 + k * WAVE, n, r0, sh, cx[k], cd[k], cm[k]);
+                    count(i0 + k * WAVE, cd[k], cm[k]);
+                }
+        } else {
+            for (int k = 0; k < kpl; ++k) {
+                uint64_t x, mine;
+                uint32_t d;
+                radix_batch(src, i0 + k * WAVE, n, r0, sh, x, d, mine);
+                count(i0 + k * WAVE, d, mine);
+            }
+        }
+        __syncthreads();
+        {  // exclusive scan of the (digit-major, wave-minor) counters, 4 per thread
+            static_assert(SORT_TPB * 4 == RADIX * SORT_WAVES, "4 counters per thread");
+            int* h = hist + (threadIdx.x / 2) * HP + (threadIdx.x % 2) * 4;
+            const int h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3];
+            int tot;
+            const int ex = block_scan_excl<SORT_TPB>(h0 + h1 + h2 + h3, s_scan, &tot);
+            h[0] = ex; h[1] = ex + h0; h[2] = ex + h0 + h1; h[3] = ex + h0 + h1 + h2;
+        }
+        __syncthreads();
+        auto place = [&](int i, uint64_t x, uint32_t d, uint64_t mine) {
+            if (i < n) {
+                int* hp = hist + d * HP + w;
+                const int pos = *hp + (int)__popcll(mine & lt);
+                dst[pos] = x;
+                if ((mine >> lane) == 1ull) *hp = pos + 1;
+            }
+        };
+        if (cached) {
+#pragma unroll
+            for (int k = 0; k < SORT_KC; ++k)
+                if (k < kpl) place(i0 + k * WAVE, cx[k], cd[k], cm[k]);
+        } else {
+            for (int k = 0; k < kpl; ++k) {
+                uint64_t x, mine;
+                uint32_t d;
+                radix_batch(src, i0 + k * WAVE, n, r0, sh, x, d, mine);
+                place(i0 + k * WAVE, x, d, mine);
+            }
+        }
+        __syncthreads();
+        uint64_t* tt = src;
+        src = dst;
+        dst = tt;
+    }
+    if (src != keys) {
+        for (int i = threadIdx.x; i < n; i += SORT_TPB) keys[i] = src[i];
+        __syncthreads();
+    }
+}
+
+// Bitonic sort of n <= SORT_TPB keys, one per thread (padding ~0), ascending: exchanges
+// within a wave by shuffles, across waves through LDS. Keys equal in (row, bag) stand for
+// the same dy row, so the result equals the stable sort by row.
+DQRM_INLINE void bitonic_sort_keys(uint64_t* keys, int n, uint64_t* xch) {
+    const int tid = threadIdx.x;
+    uint64_t x = tid < n ? keys[tid] : ~0ull;
+    int n2 = 2;
+    while (n2 < n) n2 <<= 1;
+    for (int k = 2; k <= n2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            uint64_t y;
+            if (j >= WAVE) {
+                xch[tid] = x;
+                __syncthreads();
+                y = xch[tid ^ j];
+                __syncthreads();
+            } else {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, j, WAVE);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j, WAVE);
+                y = ((uint64_t)hi << 32) | lo;
+            }
+            const bool keep_min = ((tid & j) == 0) == ((tid & k) == 0);
+            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+        }
+    }
+    if (tid < n) keys[tid] = x;
+    __syncthreads();
+}
+
+struct SortArgs {
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    int64_t B;
+    int pool1;
+    const int64_t* meta;
+    int T;
+    uint32_t* err;
+    SortWs ws;
+    int64_t Lc;
+    int ds;                      // dimension slices of a long item (K4b's SegGeom<LPR>::DS)
+    const int32_t* tmask;        // MODE 2: tables to update (nullable = all)
+    const int64_t* ws_cap_base;  // MODE 1: coalesced workspace slots
+    int32_t* ws_ucount;
+    float* ws_absmax;
+};
+
+// the slot's keys (row in [r0, r1)) in lookup order into LDS (n <= SORT_LDS_KEYS) or the
+// workspace: each thread owns a contiguous run of bags (count, block scan, write; RC keys
+// per thread kept in registers). Returns n; *in_lds tells where they went.
+DQRM_INLINE int gather_slot_keys(uint64_t* lds_keys, uint64_t* ws_keys, bool* in_lds, int* s_scan,
+                                 const int64_t* off, const int64_t* idx, int64_t B, int64_t L, int64_t nrows,
+                                 int64_t r0, int64_t r1, bool report, uint32_t* err, bool pool1) {
+    const int64_t per = (B + SORT_TPB - 1) / SORT_TPB;
+    int64_t b0 = (int64_t)threadIdx.x * per;
+    b0 = b0 < B ? b0 : B;
+    const int64_t b1 = b0 + per < B ? b0 + per : B;
+    constexpr int RC = 8;
+    uint64_t cache[RC];
+    int cnt = 0;
+    visit_slot_lookups(off, idx, B, L, nrows, b0, b1, report, err, pool1, [&](int64_t r, int64_t b) {
+        if (r >= r0 && r < r1) {
+            const uint64_t key = ((uint64_t)r << 32) | (uint64_t)b;
+#pragma unroll
+            for (int c = 0; c < RC; ++c)
+                if (c == cnt) cache[c] = key;
+            ++cnt;
+        }
+    });
+    int total;
+    int pos = block_scan_excl<SORT_TPB>(cnt, s_scan, &total);
+    *in_lds = total <= SORT_LDS_KEYS;
+    uint64_t* keys = *in_lds ? lds_keys : ws_keys;
+    if (cnt <= RC) {
+#pragma unroll
+        for (int c = 0; c < RC; ++c)
+            if (c < cnt) keys[pos + c] = cache[c];
+    } else {
+        visit_slot_lookups(off, idx, B, L, nrows, b0, b1, false, err, pool1, [&](int64_t r, int64_t b) {
+            if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
+        });
+    }
+    __syncthreads();
+    return total;
+}
+
+// sort one slot's keys, append its records and long items; returns the slot's distinct rows
+// s_base[0] / s_base[3]: the slot's record run (reserved by the caller) and its length
+template <int MODE>
+DQRM_INLINE int sort_slot(const SortArgs& a, int k, int t, int64_t r0, int64_t r1, int n, uint64_t* keys,
+                          uint64_t* tmp, int* hist, int* s_scan, int* s_wl, uint32_t* s_base, int64_t ws_e0,
+                          int64_t ws_cap, bool wide) {
+    const int64_t Lc = a.Lc;
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const uint32_t span = (uint32_t)(r1 - r0);
+    const int nbits = span <= 1 ? 0 : 32 - __builtin_clz(span - 1);
+    if (n <= SORT_TPB && nbits > 8)  // small slot of a wide table: one bitonic network
+        bitonic_sort_keys(keys, n, tmp);
+    else
+        radix_sort_rows(keys, tmp, n, (uint32_t)r0, nbits, hist, s_scan);
+    DIAG_T(2);
+
+    // segment heads (first key of every distinct row) -> hpos, in order
+    uint32_t* hpos = reinterpret_cast<uint32_t*>(tmp);
+    uint32_t* lst = hpos + n;  // long segments' stream starts (tmp holds 2n words)
+    const uint64_t lt = lanemask_lt();
+    int U;
+    {
+        const int kpl = (n + SORT_TPB - 1) / SORT_TPB;
+        const int i0 = w * WAVE * kpl + lane;
+        auto is_head = [&](int i) { return i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1])); };
+        int hc = 0;
+        for (int q = 0; q < kpl; ++q) hc += (int)__popcll(__ballot(is_head(i0 + q * WAVE)));
+        if (lane == 0) s_wl[w] = hc;
+        __syncthreads();
+        int run = 0;
+        U = 0;
+        for (int q = 0; q < SORT_WAVES; ++q) { const int c = s_wl[q]; run += q < w ? c : 0; U += c; }
+        for (int q = 0; q < kpl; ++q) {
+            const int i = i0 + q * WAVE;
+            const bool h = is_head(i);
+            const uint64_t hm = __ballot(h);
+            if (h) hpos[run + __popcll(hm & lt)] = (uint32_t)i;
+            run += (int)__popcll(hm);
+        }
+        __syncthreads();
+    }
+    DIAG_T(3);
+    const uint32_t rbase = s_base[0];  // the run reserved before the sort: rcap >= U records
+    const int rcap = (int)s_base[3];
+    if ((int64_t)rbase + rcap > (int64_t)a.T * Lc) {  // only with a workspace not zero-filled
+        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        return 0;
+    }
+    for (int u = U + threadIdx.x; u < rcap; u += SORT_TPB) a.ws.rec[rbase + u] = make_uint4(0u, 0u, 0u, 0u);
+    // records (+ the 2nd..4th bags); long segments by ordered compaction with their stream start
+    uint4* lrec = a.ws.lrec + (int64_t)k * Lc;
+    const int kpu = (U + SORT_TPB - 1) / SORT_TPB;
+    const int u0 = w * WAVE * kpu + lane;
+    auto seg_len = [&](int u) { return (int)((u + 1 < U ? hpos[u + 1] : (uint32_t)n) - hpos[u]); };
+    int nl = 0, el = 0;
+    for (int q = 0; q < kpu; ++q) {
+        const int u = u0 + q * WAVE;
+        const bool v = u < U;
+        int len = 0;
+        if (v) {
+            const uint32_t i = hpos[u];
+            len = seg_len(u);
+            const uint64_t x = keys[i];
+            const uint32_t e = MODE == 1 ? (u < ws_cap ? (uint32_t)(ws_e0 + u) : 0xFFFFFFFFu) : 0u;
+            const uint32_t ln = (uint32_t)len < REC_LEN_MAX ? (uint32_t)len : REC_LEN_MAX;
+            a.ws.rec[rbase + u] = make_uint4(key_row(x), key_lo(x), (uint32_t)k | (ln << 11), e);
+            if (len > 1)
+                a.ws.rbag[rbase + u] = make_uint4(key_lo(keys[i + 1]), len > 2 ? key_lo(keys[i + 2]) : 0u,
+                                                  len > 3 ? key_lo(keys[i + 3]) : 0u, i);
+        }
+        const bool lg = v && len > LONG_SEG;
+        nl += (int)__popcll(__ballot(lg));
+        el += lg ? len : 0;
+    }
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) el += __shfl_xor(el, o, WAVE);
+    if (lane == 0) { s_wl[w] = nl; s_wl[SORT_WAVES + w] = el; }
+    __syncthreads();
+    DIAG_T(4);
+    int kb = 0, eb = 0, nlong = 0, elong = 0;
+    for (int q = 0; q < SORT_WAVES; ++q) {
+        const int c = s_wl[q], e = s_wl[SORT_WAVES + q];
+        kb += q < w ? c : 0;
+        eb += q < w ? e : 0;
+        nlong += c;
+        elong += e;
+    }
+    if (nlong > 0) {  // uniform
+        for (int q = 0; q < kpu; ++q) {
+            const int u = u0 + q * WAVE;
+            const int len = u < U ? seg_len(u) : 0;
+            const bool lg = len > LONG_SEG;
+            const uint64_t lm = __ballot(lg);
+            int inc = lg ? len : 0;  // inclusive scan of the long lengths over the batch
+#pragma unroll
+            for (int o = 1; o < WAVE; o <<= 1) {
+                const int y = __shfl_up(inc, o, WAVE);
+                if (lane >= o) inc += y;
+            }
+            if (lg) {
+                const int j = kb + (int)__popcll(lm & lt);
+                const uint32_t i = hpos[u], st = (uint32_t)(eb + inc - len);
+                const uint32_t e = MODE == 1 ? (u < ws_cap ? (uint32_t)(ws_e0 + u) : 0xFFFFFFFFu) : (uint32_t)u;
+                lrec[j] = make_uint4(key_row(keys[i]), i, e, st);
+                lst[j] = st;
+            }
+            kb += (int)__popcll(lm);
+            eb += __shfl(inc, WAVE - 1, WAVE);
+        }
+        __syncthreads();
+        // one item per long-stream chunk holding a segment start, per dimension slice
+        const int dsx = (MODE != 1 && wide) ? 1 : a.ds;  // wide-table SGD: full rows (rowmax)
+        auto chunk_head = [&](int j) { return j < nlong && (j == 0 || lst[j - 1] / LONG_RANGE != lst[j] / LONG_RANGE); };
+        int hc = 0;
+        for (int j = threadIdx.x; j < nlong; j += SORT_TPB) hc += chunk_head(j) ? 1 : 0;
+        int tot;
+        block_scan_excl<SORT_TPB>(hc, s_scan, &tot);
+        if (threadIdx.x == 0) s_base[1] = atomicAdd(&a.ws.ctr[1], (uint32_t)(tot * dsx));
+        if (threadIdx.x == 0) s_base[2] = 0u;
+        __syncthreads();
+        const uint32_t ibase = s_base[1];
+        for (int j = threadIdx.x; j < nlong; j += SORT_TPB) {
+            if (!chunk_head(j)) continue;
+            int je = j + 1;
+            while (je < nlong && !chunk_head(je)) ++je;
+            const uint32_t send = je < nlong ? lst[je] : (uint32_t)elong;
+            const uint32_t slot_i = atomicAdd(&s_base[2], (uint32_t)dsx);  // item order is immaterial
+            for (int z = 0; z < dsx; ++z) {
+                const int64_t it = (int64_t)ibase + slot_i + z;
+                if (it < a.ws.nli)
+                    a.ws.litem[it] = make_uint4((uint32_t)k | ((uint32_t)z << 16), (uint32_t)j, (uint32_t)je, send);
+                else
+                    flag_error(a.err, DQRM_ERRF_OVERFLOW);
+            }
+        }
+    }
+    return U;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(SORT_TPB) k_sort_slots(SortArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int s_scan[SORT_WAVES + 1];
+    __shared__ int s_wl[2 * SORT_WAVES];
+    __shared__ uint32_t s_base[4];
+    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
+    DIAG_T(0);
+    const Meta m = make_meta(a.meta, a.T);
+    const int64_t nrows = m.num_rows[t];
+    int64_t r0, r1;
+    slot_rows(nrows, s, r0, r1);
+    // Criteo form: L_t == B for every table, so the table's lookups start at t * B (no
+    // dependent idx_base round trip before the index loads)
+    const int64_t ib = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
+    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ib;
+    const bool skip = (MODE == 2 && a.tmask != nullptr && a.tmask[t] == 0) || r0 >= r1;
+    int64_t ws_e0 = 0, ws_cap = 0;
+    if (MODE == 1) {
+        ws_e0 = a.ws_cap_base[k];
+        ws_cap = a.ws_cap_base[k + 1] - ws_e0;
+    }
+    int U = 0;
+    if (!skip) {  // uniform
+        if (L > a.Lc) {  // more lookups than the caller planned for: skipped, flagged
+            if (threadIdx.x == 0 && s == SPLIT - 1) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        } else {
+            uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds);
+            int* hist = reinterpret_cast<int*>(lds + SORT_LDS_KEYS * 16);
+            bool in_lds;
+            const int n = gather_slot_keys(lkeys, a.ws.skey + (int64_t)k * a.Lc, &in_lds, s_scan,
+                                           a.off + (int64_t)t * a.B, a.idx + ib, a.B, L, nrows, r0, r1,
+                                           s == SPLIT - 1, a.err, a.pool1 != 0);
+            DIAG_T(1);
+            if (n > 0) {
+                // reserve the record run now (distinct rows <= min(n, slot rows)): the atomic's
+                // round trip overlaps the sort; records past the actual count are left empty
+                const int rcap = (int)(n < r1 - r0 ? n : r1 - r0);
+                if (threadIdx.x == 0) {
+                    s_base[0] = atomicAdd(&a.ws.ctr[0], (uint32_t)rcap);
+                    s_base[3] = (uint32_t)rcap;
+                }
+                const bool wide = nrows > BLK;
+                if (in_lds) {
+                    U = sort_slot<MODE>(a, k, t, r0, r1, n, lkeys, lkeys + SORT_LDS_KEYS, hist, s_scan, s_wl,
+                                        s_base, ws_e0, ws_cap, wide);
+                    uint64_t* sk = a.ws.skey + (int64_t)k * a.Lc;  // publish the sorted keys
+                    for (int i = threadIdx.x; i < n; i += SORT_TPB) sk[i] = lkeys[i];
+                } else {
+                    U = sort_slot<MODE>(a, k, t, r0, r1, n, a.ws.skey + (int64_t)k * a.Lc,
+                                        a.ws.skey2 + (int64_t)k * a.Lc, hist, s_scan, s_wl, s_base, ws_e0, ws_cap,
+                                        wide);
+                }
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        if (MODE == 1) {
+            if (U > ws_cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);  // undersized coalesced workspace
+            a.ws_ucount[k] = U < ws_cap ? U : (int32_t)ws_cap;
+            a.ws_absmax[k] = 0.0f;
+        }
+        DIAG_T(5);
+        // every slot's list runs are reserved (the atomics above returned before this one):
+        // the last slot publishes the list lengths and re-arms the counters for the next call
+        const uint32_t done = atomicAdd(&a.ws.ctr[2], 1u);
+        if (done == gridDim.x - 1) {
+            a.ws.ctr[3] = atomicExch(&a.ws.ctr[0], 0u);
+            a.ws.ctr[4] = atomicExch(&a.ws.ctr[1], 0u);
+            atomicExch(&a.ws.ctr[2], 0u);
+        }
+    }
+}
+
+// K4b --------------------------------------------------------------------------------
+struct SegArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    float* tmax;
+    uint8_t* sdirty;
+    uint8_t* bdirty;
+    const float* scale;
+    const float* pscale;
+    const int64_t* meta;
+    uint32_t* err;
+    const float* dy;
+    int64_t dst_t, dst_b;
+    int T;
+    int ste;
+    float nlr;                   // -lr
+    int repack;                  // MODE 0/2: repack touched INT4 rows with pscale
+    int32_t* ws_rows;            // MODE 1 outputs
+    float* ws_vals;
+    float* ws_absmax;
+    SortWs ws;
+    int64_t Lc;
+};
+
+// per-table constants staged in LDS by every K4b workgroup
+struct TabLds {
+    int64_t rb[MAX_TABLES];
+    uint32_t bb[MAX_TABLES];     // blocks / superblocks / rows < 2^32 (checked on the host)
+    uint32_t sbb[MAX_TABLES];
+    uint32_t nrows[MAX_TABLES];
+    float s[MAX_TABLES];
+    float rp[MAX_TABLES];
+};
+
+DQRM_INLINE void stage_tables(const SegArgs& a, TabLds* tl, int mode) {
+    const Meta m = make_meta(a.meta, a.T);
+    for (int t = threadIdx.x; t < a.T; t += SEG_TPB) {
+        tl->rb[t] = m.row_base[t];
+        tl->nrows[t] = (uint32_t)m.num_rows[t];
+        tl->bb[t] = (uint32_t)m.blk_base[t];
+        tl->sbb[t] = (uint32_t)m.sblk_base[t];
+        tl->s[t] = a.scale[t];
+        tl->rp[t] = (mode != 1 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+    }
+}
+
+// |W| hierarchy upkeep of one updated row of a wide table (the flat protocol, see
+// flat_row_update): growth by atomicMax on the non-negative float bits, a shrunk block-max
+// holder flags its block and superblock for the tracked finalize.
+DQRM_INLINE void row_upkeep(const SegArgs& a, int t, int64_t grow, uint32_t x, int64_t bb, int64_t sbb, float old_rm,
+                            float rm, float old_blk) {
+    a.rowmax[grow] = rm;
+    const int64_t blk = x >> 8;
+    const int64_t sb = sbb + (blk >> 8);
+    if (rm > old_blk) {
+        atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
+        if (rm > a.sblkmax[sb]) {
+            atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
+            if (rm > a.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
+        }
+    }
+    if (old_rm == old_blk && rm < old_rm) {
+        a.bdirty[bb + blk] = 1;
+        a.sdirty[sb] = 1;
+    }
+}
+
+template <int OP>
+DQRM_INLINE float seg_op(float acc, float v, float nlr) {
+    if (OP == OP_FMA) return fmaf(v, nlr, acc);
+    if (OP == OP_AXPY) return acc + v * nlr;
+    return acc + v;
+}
+
+// MODE 1: max|grad| into the slot's ws_absmax (order-free atomicMax on the non-negative
+// float bits)
+DQRM_INLINE void absmax_to_slot(const SegArgs& a, int k, float am) {
+    atomicMax(reinterpret_cast<unsigned int*>(a.ws_absmax) + k, __float_as_uint(am));
+}
+
+// the same for the wave's (slot, value) pairs of the lanes with `valid`: one atomic per
+// distinct slot per wave (a slot's records are one contiguous run of the list, so a wave's
+// records come from one or two slots). Wave-uniform call.
+DQRM_INLINE void wave_slot_max(const SegArgs& a, int k, float am, bool valid) {
+    uint64_t pend = __ballot(valid);
+    while (pend) {
+        const int l = __ffsll((long long)pend) - 1;
+        const int k0 = __shfl(k, l, WAVE);
+        const bool mine = valid && k == k0;
+        const uint64_t mm = __ballot(mine);
+        const float v = wave_max(mine ? am : 0.0f);
+        if ((int)(threadIdx.x % WAVE) == l) absmax_to_slot(a, k0, v);
+        pend &= ~mm;
+    }
+}
+
+// one short-record chunk; the list length, the table constants and the records are
+// loaded in one round trip (records past the list are read from the workspace's capacity
+// and masked), then every record's W row and dy rows in a second
+template <int LPR, int MODE>
+DQRM_INLINE void short_records(const SegArgs& a, TabLds* tl, int r_begin, unsigned int (*s_am)[SEG_SB * 2]) {
+    constexpr int D = LPR * 4;
+    using G = SegGeom<LPR>;
+    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
+    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int nrec = (int)a.ws.ctr[3];
+    uint4 rec[SEG_SB], bg[SEG_SB];
+    bool act[SEG_SB];
+    const int64_t rlim = (int64_t)a.T * a.Lc;  // the list's capacity
+#pragma unroll
+    for (int b = 0; b < SEG_SB; ++b) {
+        const int r = r_begin + grp + b * G::NG;
+        rec[b] = r < rlim ? a.ws.rec[r] : make_uint4(0u, 0u, 0u, 0u);
+        bg[b] = r < rlim ? a.ws.rbag[r] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    stage_tables(a, tl, MODE);
+    if (r_begin >= nrec) return;  // uniform
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < SEG_SB; ++b) {
+        const int r = r_begin + grp + b * G::NG;
+        act[b] = r < nrec && (rec[b].z >> 11) - 1u < (uint32_t)LONG_SEG;  // 1..LONG_SEG (0: empty)
+    }
+    DIAG_W(3);
+    float4 wold[SEG_SB], v[SEG_SB][4];
+    float oblk[SEG_SB], am[SEG_SB];
+#pragma unroll
+    for (int b = 0; b < SEG_SB; ++b) {  // every segment's W row and lookups (<= 4) in flight
+        if (!act[b]) continue;
+        const int t = (int)(rec[b].z & 2047u) / SPLIT;
+        const int len = (int)(rec[b].z >> 11);
+        const float* dyt = a.dy + (int64_t)t * a.dst_t;
+        const int64_t grow = tl->rb[t] + rec[b].x;
+        if (MODE != 1) {
+            wold[b] = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+            oblk[b] = tl->nrows[t] > BLK ? a.blkmax[tl->bb[t] + (rec[b].x >> 8)] : 0.0f;
+        }
+        v[b][0] = reinterpret_cast<const float4*>(dyt + (int64_t)rec[b].y * a.dst_b)[sub];
+        if (len > 1) v[b][1] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].x * a.dst_b)[sub];
+        if (len > 2) v[b][2] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].y * a.dst_b)[sub];
+        if (len > 3) v[b][3] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].z * a.dst_b)[sub];
+    }
+    DIAG_W(4);
+#pragma unroll
+    for (int b = 0; b < SEG_SB; ++b) {
+        am[b] = 0.0f;
+        if (!act[b]) continue;
+        const int k = (int)(rec[b].z & 2047u), t = k / SPLIT;
+        const int len = (int)(rec[b].z >> 11);
+        const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, tl->s[t], a.ste, 0};
+        bool first = true;
+        float4 acc = MODE != 1 ? wold[b] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (c < len) acc = combine<OP>(acc, src.finish(v[b][c]), first, a.nlr);
+        if (len > 4) {  // 5..LONG_SEG (rare): the slot's sorted keys from the record's first key on
+            const uint64_t* sk = a.ws.skey + (int64_t)k * a.Lc + bg[b].w;
+            float4 q[4];
+            for (int j = 4; j < len; j += 4) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (j + c < len) q[c] = src.fetch(key_lo(sk[j + c]), sub);
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (j + c < len) acc = combine<OP>(acc, src.finish(q[c]), first, a.nlr);
+            }
+        }
+        const uint32_t x = rec[b].x;
+        const int64_t grow = tl->rb[t] + x;
+        if (MODE == 1) {
+            const uint32_t e = rec[b].w;
+            am[b] = group_max<LPR>(abs_max4(acc));
+            if (e != 0xFFFFFFFFu) {
+                reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * D)[sub] = acc;
+                if (sub == 0) a.ws_rows[e] = (int32_t)x;
+            }
+        } else {
+            reinterpret_cast<float4*>(a.W + grow * D)[sub] = acc;
+            if (a.repack) pack4_row(acc, a.packed + grow * (D / 2), sub, tl->rp[t]);
+            if (tl->nrows[t] > BLK) {
+                const float old_rm = group_max<LPR>(abs_max4(wold[b]));
+                const float rm = group_max<LPR>(abs_max4(acc));
+                if (sub == 0) row_upkeep(a, t, grow, x, tl->bb[t], tl->sbb[t], old_rm, rm, oblk[b]);
+            }
+        }
+    }
+    DIAG_W(5);
+    if (MODE == 1) {  // slot maxima: per wave then per workgroup, one atomic per distinct slot
+        const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+        int nk = 0;
+#pragma unroll
+        for (int b = 0; b < SEG_SB; ++b) {  // the wave's distinct (slot, max) pairs -> s_am[w]
+            const bool valid = act[b] && sub == 0;
+            const int kk = (int)(rec[b].z & 2047u);
+            uint64_t pend = __ballot(valid);
+            while (pend) {
+                const int l = __ffsll((long long)pend) - 1;
+                const int k0 = __shfl(kk, l, WAVE);
+                const bool mine = valid && kk == k0;
+                const float v = wave_max(mine ? am[b] : 0.0f);
+                pend &= ~__ballot(mine);
+                int q = 0;  // merge into the wave's list (at most 2*SEG_SB distinct slots)
+                while (q < nk && (int)s_am[w][q] != k0) ++q;
+                if (lane == 0) {
+                    if (q < nk) {
+                        s_am[w][SEG_SB + q] = max(s_am[w][SEG_SB + q], __float_as_uint(v));
+                    } else if (nk < SEG_SB) {
+                        s_am[w][nk] = (unsigned)k0;
+                        s_am[w][SEG_SB + nk] = __float_as_uint(v);
+                    } else {
+                        absmax_to_slot(a, k0, v);  // list full (never for ordered runs)
+                    }
+                }
+                if (q >= nk && nk < SEG_SB) ++nk;
+            }
+        }
+        __shared__ int s_nk[SEG_TPB / WAVE];
+        if (lane == 0) s_nk[w] = nk;
+        __syncthreads();
+        if (threadIdx.x == 0) {  // merge the waves' lists, one atomic per distinct slot
+            unsigned int ks[SEG_TPB / WAVE * SEG_SB], vs[SEG_TPB / WAVE * SEG_SB];
+            int m = 0;
+            for (int ww = 0; ww < SEG_TPB / WAVE; ++ww)
+                for (int q = 0; q < s_nk[ww]; ++q) {
+                    const unsigned int k0 = s_am[ww][q], v = s_am[ww][SEG_SB + q];
+                    int p = 0;
+                    while (p < m && ks[p] != k0) ++p;
+                    if (p < m) vs[p] = max(vs[p], v); else { ks[m] = k0; vs[m] = v; ++m; }
+                }
+            for (int p = 0; p < m; ++p) atomicMax(reinterpret_cast<unsigned int*>(a.ws_absmax) + ks[p], vs[p]);
+        }
+    }
+}
+
+// largest k in [0, nk) with p[k] <= e (p ascending, p[0] <= e)
+DQRM_INLINE int seg_search(const int* p, int nk, int e) {
+    int lo = 0, hi = nk - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (p[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+struct LongLds {
+    int lp[LMAXK + 1];  // long-stream position of each owned segment (relative), + end
+    int st[LMAXK];      // first key
+    uint32_t row[LMAXK];
+    uint32_t e[LMAXK];  // MODE 1: ws entry
+};
+
+// A long item: the long segments of slot k whose long-stream start falls in one
+// LONG_RANGE chunk, dimension slice z. Their lookups (this slice of each dy row) stream
+// through the LDS stage CE at a time, dim-major; dim-lane group g combines segments
+// j = g (mod NGL) strictly in lookup order, carrying its running row in registers into the
+// next chunk (only the chunk's last segment can continue, and the same group owns it there).
+template <int LPR, int MODE, bool FULL>
+DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float* stage, LongLds* ll) {
+    constexpr int D = LPR * 4;
+    using G = SegGeom<LPR>;
+    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
+    constexpr int SW = FULL ? D : D / G::DS;  // floats of each row this item owns
+    constexpr int GL = SW < WAVE ? SW : WAVE;
+    constexpr int NDL = SW / GL;
+    constexpr int NGL = SEG_TPB / GL;
+    constexpr int F4 = SW / 4;
+    constexpr int CE = LSTAGE / SW;           // lookups per stage chunk
+    constexpr int SP = CE + 4;                // stage pitch of one dim
+    constexpr int FM = LSTAGE / 4 / SEG_TPB;  // float4 fetched per thread per chunk
+    const int k = (int)(item.x & 0xFFFFu), z = (int)(item.x >> 16), t = k / SPLIT;
+    const int dim0 = FULL ? 0 : z * SW;
+    const int kf = (int)item.y, nk = (int)item.z - kf;
+    const int64_t Lc = a.Lc;
+    const uint4* __restrict__ lrec = a.ws.lrec + (int64_t)k * Lc;
+    __syncthreads();  // the previous item is done with the LDS
+    const int E0 = (int)lrec[kf].w;
+    for (int i = threadIdx.x; i <= nk; i += SEG_TPB) {
+        if (i < nk) {
+            const uint4 r = lrec[kf + i];
+            ll->lp[i] = (int)r.w - E0;
+            ll->row[i] = r.x;
+            ll->st[i] = (int)r.y;
+            ll->e[i] = r.z;
+        } else {
+            ll->lp[i] = (int)item.w - E0;
+        }
+    }
+    __syncthreads();
+    const int64_t rb = tl->rb[t], bb = tl->bb[t], sbb = tl->sbb[t];
+    const uint64_t* __restrict__ skey = a.ws.skey + (int64_t)k * Lc;
+    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, tl->s[t], a.ste, dim0 / 4};
+    const float r_pack = tl->rp[t];
+    const int E = ll->lp[nk];
+    const int lig = threadIdx.x % GL, g = threadIdx.x / GL;
+    float acc[NDL];
+    float orm = 0.0f, oblk = 0.0f;
+#pragma unroll
+    for (int d = 0; d < NDL; ++d) acc[d] = 0.0f;
+    for (int c0 = 0; c0 < E; c0 += CE) {
+        const int ce = min(CE, E - c0);
+        {  // fetch the chunk: thread-contiguous (lookup, float4) items, one segment search per
+           // thread then a forward walk; keys first, then this slice of every dy row
+            const int q0 = threadIdx.x * FM;
+            uint32_t bag[FM];
+            if (q0 / F4 < ce) {
+                int j = seg_search(ll->lp, nk, c0 + q0 / F4);
+                uint32_t bb0 = 0;
+#pragma unroll
+                for (int f = 0; f < FM; ++f) {
+                    const int q = q0 + f, el = q / F4;
+                    if (el < ce && (f == 0 || q % F4 == 0)) {
+                        const int e = c0 + el;
+                        while (e >= ll->lp[j + 1]) ++j;
+                        bb0 = key_lo(skey[ll->st[j] + (e - ll->lp[j])]);
+                    }
+                    bag[f] = bb0;
+                }
+            }
+            float4 v[FM];
+#pragma unroll
+            for (int f = 0; f < FM; ++f) {
+                const int q = q0 + f;
+                if (q / F4 < ce) v[f] = src.fetch(bag[f], q % F4);
+            }
+#pragma unroll
+            for (int f = 0; f < FM; ++f) {
+                const int q = q0 + f, el = q / F4;
+                if (el < ce) {
+                    const float4 x = src.finish(v[f]);
+                    float* col = stage + (4 * (q % F4)) * SP + el;
+                    col[0] = x.x; col[SP] = x.y; col[2 * SP] = x.z; col[3 * SP] = x.w;
+                }
+            }
+        }
+        __syncthreads();
+        const int jfc = seg_search(ll->lp, nk, c0), jlc = seg_search(ll->lp, nk, c0 + ce - 1);
+        for (int j = jfc + ((g - jfc % NGL) + NGL) % NGL; j <= jlc; j += NGL) {
+            const int sb = ll->lp[j], se = ll->lp[j + 1];
+            const bool begin = sb >= c0;
+            const uint32_t x = ll->row[j];
+            const int64_t grow = rb + x;
+            int e = (begin ? sb : c0) - c0;
+            const int e1 = (se < c0 + ce ? se : c0 + ce) - c0;
+            const float* col[NDL];
+#pragma unroll
+            for (int d = 0; d < NDL; ++d) col[d] = stage + (lig + GL * d) * SP;
+            if (begin) {
+                if (MODE == 1) {
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) acc[d] = col[d][e];
+                    ++e;
+                } else {
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) acc[d] = a.W[grow * D + dim0 + lig + GL * d];
+                    if (FULL) {
+                        float mx = 0.0f;
+#pragma unroll
+                        for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
+                        orm = group_max<GL>(mx);
+                        oblk = a.blkmax[bb + (x >> 8)];
+                    }
+                }
+            }
+            // strictly ordered chain: peel to a 16-B boundary, then 16-B LDS reads, the next
+            // VB float4 per dim in flight while the current ones are combined (ping-pong)
+            for (; e < e1 && (e & 3); ++e)
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) acc[d] = seg_op<OP>(acc[d], col[d][e], a.nlr);
+            constexpr int VB = NDL >= 4 ? 1 : 4 / NDL;
+            constexpr int BE = 4 * VB;
+            float4 xa[VB][NDL], xb[VB][NDL];
+            auto loadb = [&](float4 (&xx)[VB][NDL], int jj) {
+#pragma unroll
+                for (int vv = 0; vv < VB; ++vv)
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) xx[vv][d] = *reinterpret_cast<const float4*>(col[d] + jj + 4 * vv);
+            };
+            auto addb = [&](const float4 (&xx)[VB][NDL]) {
+#pragma unroll
+                for (int vv = 0; vv < VB; ++vv)
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d)
+                        acc[d] = seg_op<OP>(seg_op<OP>(seg_op<OP>(seg_op<OP>(acc[d], xx[vv][d].x, a.nlr), xx[vv][d].y,
+                                                                  a.nlr), xx[vv][d].z, a.nlr), xx[vv][d].w, a.nlr);
+            };
+            if (e + BE <= e1) {
+                loadb(xa, e);
+                while (true) {
+                    const bool m1 = e + 2 * BE <= e1;
+                    if (m1) loadb(xb, e + BE);
+                    addb(xa);
+                    e += BE;
+                    if (!m1) break;
+                    const bool m2 = e + 2 * BE <= e1;
+                    if (m2) loadb(xa, e + BE);
+                    addb(xb);
+                    e += BE;
+                    if (!m2) break;
+                }
+            }
+            for (; e + 4 <= e1; e += 4)
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) {
+                    const float4 xx = *reinterpret_cast<const float4*>(col[d] + e);
+                    acc[d] = seg_op<OP>(seg_op<OP>(seg_op<OP>(seg_op<OP>(acc[d], xx.x, a.nlr), xx.y, a.nlr), xx.z, a.nlr),
+                                        xx.w, a.nlr);
+                }
+            for (; e < e1; ++e)
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) acc[d] = seg_op<OP>(acc[d], col[d][e], a.nlr);
+            if (se > c0 + ce) continue;  // continues in the next chunk (same group, acc carried)
+            if (MODE == 1) {
+                const uint32_t ew = ll->e[j];
+                float mx = 0.0f;
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
+                mx = group_max<GL>(mx);
+                if (ew != 0xFFFFFFFFu) {
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) a.ws_vals[(int64_t)ew * D + dim0 + lig + GL * d] = acc[d];
+                    if (dim0 == 0 && lig == 0) a.ws_rows[ew] = (int32_t)x;
+                }
+                if (lig == 0) absmax_to_slot(a, k, mx);
+            } else {
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) a.W[grow * D + dim0 + lig + GL * d] = acc[d];
+                if (a.repack) {  // even lanes pack their nibble with the odd neighbour's
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) {
+                        const int q = (int)fake_quant(acc[d], r_pack, -8.0f, 7.0f) + 8;
+                        const int qn = __shfl_xor(q, 1, WAVE);
+                        const int dim = dim0 + lig + GL * d;
+                        if ((dim & 1) == 0) a.packed[grow * (D / 2) + dim / 2] = (uint8_t)(q | (qn << 4));
+                    }
+                }
+                if (FULL) {
+                    float mx = 0.0f;
+#pragma unroll
+                    for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
+                    const float rm = group_max<GL>(mx);
+                    if (lig == 0) row_upkeep(a, t, grow, x, bb, sbb, orm, rm, oblk);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int LPR, int MODE>
+__global__ void __launch_bounds__(SEG_TPB) k_bwd_segments(SegArgs a) {
+    using G = SegGeom<LPR>;
+    __shared__ __attribute__((aligned(16))) float s_stage[LSTAGE + 4 * 256];
+    __shared__ unsigned int s_am[SEG_TPB / WAVE][SEG_SB * 2];   // MODE 1: per wave (slot, max) pairs
+    __shared__ LongLds s_ll;
+    __shared__ TabLds s_tl;
+    // grid.x: LONG_WGS workgroups looping over the long items first (the long chains are
+    // the critical path, so they are dispatched first), then one per US-record chunk
+    const bool is_long = (int)blockIdx.x < LONG_WGS;
+    if (is_long) {
+        const int nli = (int)a.ws.ctr[4];
+        if ((int)blockIdx.x >= nli) return;
+        stage_tables(a, &s_tl, MODE);
+        for (int w = blockIdx.x; w < nli; w += LONG_WGS) {
+            const uint4 item = a.ws.litem[w];
+            const int t = (int)(item.x & 0xFFFFu) / SPLIT;
+            __syncthreads();  // s_tl staged
+            if (MODE != 1 && s_tl.nrows[t] > BLK)
+                long_item<LPR, MODE, true>(a, &s_tl, item, s_stage, &s_ll);
+            else
+                long_item<LPR, MODE, false>(a, &s_tl, item, s_stage, &s_ll);
+        }
+        return;
+    }
+    DIAG_T(0);
+    const int r_begin = ((int)blockIdx.x - LONG_WGS) * G::US;
+    short_records<LPR, MODE>(a, &s_tl, r_begin, s_am);
+    DIAG_W(6);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2459,6 +3525,68 @@ int apply_kernel_kind() {
     return k;
 }
 
+// one backward call (K4a + K4b [+ finalize]) on the caller's workspace
+struct BwdCall {
+    const dqrm_table_set* set;
+    const dqrm_batch* batch;
+    const float* dy;
+    int64_t dst_t, dst_b;
+    int ste;
+    float lr;
+    int repack;
+    const int32_t* tmask;
+    const int64_t* ws_cap_base;
+    int32_t* ws_rows;
+    float* ws_vals;
+    int32_t* ws_ucount;
+    float* ws_absmax;
+    void* ws;
+    size_t ws_bytes;
+};
+
+int64_t bwd_lookup_cap(const dqrm_batch* batch) { return batch->max_lookups > 0 ? batch->max_lookups : 1; }
+
+template <int MODE>
+int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
+    const dqrm_table_set* set = c.set;
+    const int T = set->num_tables, D = set->dim;
+    const int64_t Lc = bwd_lookup_cap(c.batch);
+    if (Lc > 0x3fffffffll || (int64_t)T * Lc > 0xffffffffll)
+        return set_error(DQRM_E_CAPACITY, "%s: max_lookups %lld too large", who, (long long)Lc);
+    if (set->total_rows > 0xffffffffll)
+        return set_error(DQRM_E_CAPACITY, "%s: more than 2^32 rows", who);
+    const int64_t need = sort_ws_layout(nullptr, T, Lc, nullptr);
+    if (!c.ws || (int64_t)c.ws_bytes < need || (((uintptr_t)c.ws) & 15))
+        return set_error(DQRM_E_WORKSPACE, "%s: workspace needs %lld bytes, 16-B aligned (got %zu)", who,
+                         (long long)need, c.ws_bytes);
+    SortWs ws;
+    sort_ws_layout(reinterpret_cast<unsigned char*>(c.ws), T, Lc, &ws);
+    SortArgs sa{};
+    sa.idx = c.batch->idx; sa.off = c.batch->off; sa.idx_base = c.batch->idx_base; sa.B = c.batch->num_bags;
+    sa.pool1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    sa.meta = set->meta; sa.T = T; sa.err = set->err; sa.ws = ws; sa.Lc = Lc; sa.tmask = c.tmask;
+    sa.ws_cap_base = c.ws_cap_base; sa.ws_ucount = c.ws_ucount; sa.ws_absmax = c.ws_absmax;
+    SegArgs ga{};
+    ga.W = set->W; ga.packed = set->packed; ga.rowmax = set->rowmax; ga.blkmax = set->blkmax;
+    ga.sblkmax = set->sblkmax; ga.tmax = set->tmax; ga.sdirty = set->sdirty; ga.bdirty = set->bdirty;
+    ga.scale = set->scale; ga.pscale = set->pscale; ga.meta = set->meta; ga.err = set->err;
+    ga.dy = c.dy; ga.dst_t = c.dst_t; ga.dst_b = c.dst_b; ga.T = T; ga.ste = c.ste; ga.nlr = -c.lr;
+    ga.repack = c.repack; ga.ws_rows = c.ws_rows; ga.ws_vals = c.ws_vals; ga.ws_absmax = c.ws_absmax;
+    ga.ws = ws; ga.Lc = Lc;
+    int rc = allow_lds(k_sort_slots<MODE>, SORT_LDS);
+    if (rc) return rc;
+    DISPATCH_LPR(D, {
+        using G = SegGeom<LPR>;
+        sa.ds = G::DS;
+        hipLaunchKernelGGL(k_sort_slots<MODE>, dim3(T * SPLIT), dim3(SORT_TPB), SORT_LDS, st, sa);
+        const int64_t nxs = ((int64_t)T * Lc + G::US - 1) / G::US;  // record chunks (records <= lookups)
+        hipLaunchKernelGGL((k_bwd_segments<LPR, MODE>), dim3((unsigned)(LONG_WGS + nxs)), dim3(SEG_TPB), 0, st, ga);
+    });
+    LAUNCH_CHECK();
+    if (MODE != 1) return launch_finalize(set, st, true);
+    return DQRM_OK;
+}
+
 }  // namespace
 
 // ======================================================================================
@@ -2607,9 +3735,14 @@ static int check_batch(const dqrm_batch* batch, const char* who) {
     return DQRM_OK;
 }
 
+size_t dqrm_bwd_workspace_bytes(int num_tables, int64_t max_lookups) {
+    if (num_tables <= 0 || num_tables > MAX_TABLES || max_lookups < 0) return 0;
+    return (size_t)sort_ws_layout(nullptr, num_tables, max_lookups > 0 ? max_lookups : 1, nullptr);
+}
+
 int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                      int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, int repack_bits,
-                     void* stream) {
+                     void* workspace, size_t workspace_bytes, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if ((rc = check_batch(batch, "dqrm_emb_bwd_sgd"))) return rc;
@@ -2618,23 +3751,10 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     if (repack_bits && (repack_bits != 4 || !set->packed))
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_emb_bwd_sgd", repack_bits);
     if (batch->num_bags <= 0) return DQRM_OK;
-    BwdArgs a;
-    memset(&a, 0, sizeof(a));
-    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
-    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.scale = set->scale; a.pscale = set->pscale;
-    a.meta = set->meta; a.err = set->err;
-    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
-    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
-    a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4;
-    hipStream_t st = (hipStream_t)stream;
-    const int D = set->dim;
-    DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_bwd<LPR, 0>, SLOT_LDS))) return rc;
-        hipLaunchKernelGGL((k_table_bwd<LPR, 0>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
-    });
-    LAUNCH_CHECK();
-    return launch_finalize(set, st);
+    BwdCall c{};
+    c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
+    c.lr = lr; c.repack = repack_bits == 4; c.ws = workspace; c.ws_bytes = workspace_bytes;
+    return launch_bwd<0>(c, (hipStream_t)stream, "dqrm_emb_bwd_sgd");
 }
 
 int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, int64_t max_lookups,
@@ -2649,7 +3769,7 @@ int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, in
             const int64_t r1 = b1 * BLK < num_rows_host[t] ? b1 * BLK : num_rows_host[t];
             int64_t rows = r1 - b0 * BLK;
             if (rows < 0) rows = 0;
-            const int64_t lim = max_lookups < SLOT_KEYS ? max_lookups : SLOT_KEYS;
+            const int64_t lim = max_lookups;  // distinct rows <= lookups: never exceeded
             ws_cap_base_host[t * SPLIT + s] = run;
             run += rows < lim ? rows : lim;
         }
@@ -2661,7 +3781,7 @@ int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, in
 int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                           int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
                           int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount, float* ws_absmax,
-                          void* stream) {
+                          void* workspace, size_t workspace_bytes, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if ((rc = check_batch(batch, "dqrm_emb_bwd_coalesce"))) return rc;
@@ -2669,22 +3789,11 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
         return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_coalesce");
     if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !ws_absmax || (((uintptr_t)ws_vals) & 15))
         return set_error(DQRM_E_INVALID, "%s: null/unaligned workspace", "dqrm_emb_bwd_coalesce");
-    BwdArgs a;
-    memset(&a, 0, sizeof(a));
-    a.W = set->W; a.scale = set->scale; a.meta = set->meta; a.err = set->err;
-    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
-    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables; a.ste = ste;
-    a.ws_cap_base = ws_cap_base; a.ws_rows = ws_rows; a.ws_vals = ws_vals; a.ws_ucount = ws_ucount;
-    a.ws_absmax = ws_absmax;
-    hipStream_t st = (hipStream_t)stream;
-    const int D = set->dim;
-    DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_bwd<LPR, 1>, SLOT_LDS))) return rc;
-        hipLaunchKernelGGL((k_table_bwd<LPR, 1>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
-    });
-    LAUNCH_CHECK();
-    return DQRM_OK;
+    BwdCall c{};
+    c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
+    c.ws_cap_base = ws_cap_base; c.ws_rows = ws_rows; c.ws_vals = ws_vals; c.ws_ucount = ws_ucount;
+    c.ws_absmax = ws_absmax; c.ws = workspace; c.ws_bytes = workspace_bytes;
+    return launch_bwd<1>(c, (hipStream_t)stream, "dqrm_emb_bwd_coalesce");
 }
 
 size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits) {
@@ -2734,7 +3843,7 @@ int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_b
 
 int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                           int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, const int32_t* table_mask,
-                          int repack_bits, void* stream) {
+                          int repack_bits, void* workspace, size_t workspace_bytes, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if ((rc = check_batch(batch, "dqrm_emb_local_update"))) return rc;
@@ -2743,23 +3852,10 @@ int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, co
     if (repack_bits && (repack_bits != 4 || !set->packed))
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_emb_local_update", repack_bits);
     if (batch->num_bags <= 0) return DQRM_OK;
-    BwdArgs a;
-    memset(&a, 0, sizeof(a));
-    a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
-    a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.scale = set->scale; a.pscale = set->pscale;
-    a.meta = set->meta; a.err = set->err;
-    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base; a.B = batch->num_bags;
-    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-    a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.T = set->num_tables;
-    a.ste = ste; a.nlr = -lr; a.repack = repack_bits == 4; a.tmask = table_mask;
-    hipStream_t st = (hipStream_t)stream;
-    const int D = set->dim;
-    DISPATCH_LPR(D, {
-        if ((rc = allow_lds(k_table_bwd<LPR, 2>, SLOT_LDS))) return rc;
-        hipLaunchKernelGGL((k_table_bwd<LPR, 2>), dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
-    });
-    LAUNCH_CHECK();
-    return launch_finalize(set, st);
+    BwdCall c{};
+    c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
+    c.lr = lr; c.repack = repack_bits == 4; c.tmask = table_mask; c.ws = workspace; c.ws_bytes = workspace_bytes;
+    return launch_bwd<2>(c, (hipStream_t)stream, "dqrm_emb_local_update");
 }
 
 int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,

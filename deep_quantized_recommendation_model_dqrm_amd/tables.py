@@ -159,6 +159,7 @@ class EmbeddingTableSet:
         self.tflags = torch.zeros(T, dtype=torch.int32, device=dev)
         self.sdirty = torch.zeros(NS, dtype=torch.uint8, device=dev)
         self.bdirty = torch.zeros(NB, dtype=torch.uint8, device=dev)
+        self._bws: torch.Tensor | None = None  # backward workspace, grown to the largest batch seen
         self._c = L.TableSet(
             T, D, self.R, NB, NS,
             _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
@@ -251,6 +252,16 @@ class EmbeddingTableSet:
         return out
 
     # ------------------------------------------------------------------ backward
+    def bwd_workspace(self, max_lookups: int) -> torch.Tensor:
+        """Device scratch of the backward's per-table lookup sort (dqrm_bwd_workspace_bytes);
+        allocated once per batch-size high-water mark, never on a steady-state step."""
+        need = int(self.lib.dqrm_bwd_workspace_bytes(self.T, int(max_lookups)))
+        if need <= 0:
+            raise ValueError("bad workspace request (%d tables, max_lookups %d)" % (self.T, max_lookups))
+        if self._bws is None or self._bws.numel() < need:  # zero-filled: the library's list counters
+            self._bws = torch.zeros(need, dtype=torch.uint8, device=self.device)
+        return self._bws
+
     @staticmethod
     def _dy_strides(dy: torch.Tensor, layout: str, T: int, B: int, D: int) -> tuple[int, int]:
         if dy.stride(-1) != 1:
@@ -263,13 +274,17 @@ class EmbeddingTableSet:
             raise ValueError("dy must be [B, T, D]")
         return dy.stride(1), dy.stride(0)
 
+    def _ws_args(self, batch: LookupBatch) -> tuple[int, int]:
+        w = self.bwd_workspace(batch.max_lookups)
+        return w.data_ptr(), w.numel()
+
     def backward_sgd(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
                      repack: bool = False, layout: str = "tbd") -> None:
         """Fused STE + sparse backward + SGD (torch.optim.SGD semantics, in lookup order)."""
         st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
         L.check(
             self.lib.dqrm_emb_bwd_sgd(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
-                                      float(lr), 4 if repack else 0, _stream_handle()),
+                                      float(lr), 4 if repack else 0, *self._ws_args(batch), _stream_handle()),
             "dqrm_emb_bwd_sgd",
         )
 
@@ -280,7 +295,8 @@ class EmbeddingTableSet:
         st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
         L.check(
             self.lib.dqrm_emb_local_update(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
-                                           float(lr), _ptr(table_mask), 4 if repack else 0, _stream_handle()),
+                                           float(lr), _ptr(table_mask), 4 if repack else 0,
+                                           *self._ws_args(batch), _stream_handle()),
             "dqrm_emb_local_update",
         )
 
@@ -291,7 +307,8 @@ class EmbeddingTableSet:
         L.check(
             self.lib.dqrm_emb_bwd_coalesce(
                 C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.slot_cap_base),
-                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), _stream_handle()),
+                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), *self._ws_args(batch),
+                _stream_handle()),
             "dqrm_emb_bwd_coalesce",
         )
 

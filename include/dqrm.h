@@ -45,24 +45,27 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 2  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local */
+#define DQRM_ABI_VERSION 3  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+                               3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap */
 
 /* status codes */
 #define DQRM_OK            0
 #define DQRM_E_INVALID    -1   /* bad argument (shape, null pointer, unsupported bits) */
 #define DQRM_E_HIP        -2   /* HIP runtime error */
-#define DQRM_E_CAPACITY   -3   /* per-table work exceeds this build's on-chip capacity */
+#define DQRM_E_CAPACITY   -3   /* a size exceeds this build's index range (e.g. max_lookups >= 2^30) */
 #define DQRM_E_WORKSPACE  -4   /* workspace too small */
 
 /* device-side error flags accumulated in dqrm_table_set.err (read with dqrm_read_errors) */
 #define DQRM_ERRF_INDEX    1u  /* an index was outside [0, num_rows[t]) (reference: IndexError) */
 #define DQRM_ERRF_OFFSET   2u  /* offsets not non-decreasing / outside [0, L_t] */
-#define DQRM_ERRF_OVERFLOW 4u  /* a coalesced/merged per-table count exceeded its capacity */
+#define DQRM_ERRF_OVERFLOW 4u  /* a table had more lookups than dqrm_batch.max_lookups promised, or a
+                                      caller-sized workspace / payload was too small */
 
 #define DQRM_BLOCK_ROWS   256     /* rows per blkmax entry */
 #define DQRM_SBLOCK_ROWS  65536   /* rows per sblkmax entry */
 #define DQRM_TABLE_SPLIT  8       /* workgroups (row-range slots) per table in the backward */
-#define DQRM_SLOT_KEYS    8192    /* max lookups / merged entries one slot sorts on chip */
+#define DQRM_SLOT_KEYS    8192    /* merged payload entries the slot apply kernel sorts on chip
+                                     (a fuller slot is applied by the flat method instead) */
 
 /* Resident state of T tables. All pointers are device pointers. */
 typedef struct dqrm_table_set {
@@ -92,9 +95,8 @@ typedef struct dqrm_table_set {
  *   off      i64 [T][B]       bag b of table t = idx_base[t] + [off[t][b], off[t][b+1])
  *                             (last bag ends at L_t), exactly nn.EmbeddingBag offsets
  *   idx_base i64 [T+1]        device copy
- * Backward capacity: the lookups of one table that fall in one row-range slot (1/8 of
- * the table's 256-row blocks) must not exceed DQRM_SLOT_KEYS (DQRM_E_CAPACITY / the
- * DQRM_ERRF_OVERFLOW flag otherwise). */
+ * max_lookups must bound every L_t: it sizes the backward workspace (a table with more
+ * lookups is skipped and flags DQRM_ERRF_OVERFLOW). There is no other per-batch limit. */
 typedef struct dqrm_batch {
     const int64_t* idx;
     const int64_t* off;
@@ -148,6 +150,17 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits,
                  void* stream);
 
 /* ---------------------------------------------------------------------------------
+ * Backward workspace. The three backward calls below (SGD, coalesce, local update) sort
+ * the lookups of every (table, row-range slot) by row on the device (in LDS up to 4096
+ * lookups, in this workspace beyond) and process the distinct rows from a device-built
+ * work list. Its size depends only on the table count and dqrm_batch.max_lookups.
+ * Returns the bytes needed (0 on bad arguments). The workspace must be 16-B aligned and
+ * ZERO-FILLED before its first use; every call leaves its counters at zero again, so the
+ * same buffer is reused without clearing (one call at a time per workspace).
+ * ------------------------------------------------------------------------------ */
+size_t dqrm_bwd_workspace_bytes(int num_tables, int64_t max_lookups);
+
+/* ---------------------------------------------------------------------------------
  * Single-GPU backward + SGD, fused (no sparse gradient materialised).
  * Replaces: SymmetricQuantFunction.backward (quant_utils.py:349-363) + autograd of q*s,
  * EmbeddingBag sparse backward, and torch.optim.SGD.step on the sparse grad
@@ -159,7 +172,8 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits,
  * ------------------------------------------------------------------------------ */
 int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
                      const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
-                     int ste, float lr, int repack_bits, void* stream);
+                     int ste, float lr, int repack_bits, void* workspace, size_t workspace_bytes,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Data-parallel gradient path (sgd_quantized_gradients_parallel_comm.py)
@@ -174,7 +188,8 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
  * dqrm_coalesce_slot_caps() gives the slot capacities (host).
  * ------------------------------------------------------------------------------ */
 
-/* Host helper: slot capacities cap[t*S+s] = min(max_lookups, rows in slot s of table t);
+/* Host helper: slot capacities cap[t*S+s] = min(max_lookups, rows in slot s of table t)
+ * (a slot can never hold more distinct rows than that);
  * writes the exclusive prefix into ws_cap_base_host[T*S+1]; returns WCAP (>= 0). */
 int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, int64_t max_lookups,
                                 int64_t* ws_cap_base_host);
@@ -185,7 +200,8 @@ int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, in
 int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
                           const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
                           int ste, const int64_t* ws_cap_base, int32_t* ws_rows, float* ws_vals,
-                          int32_t* ws_ucount, float* ws_absmax, void* stream);
+                          int32_t* ws_ucount, float* ws_absmax, void* workspace, size_t workspace_bytes,
+                          void* stream);
 
 /* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
  *   [counts i32 T*S | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
@@ -229,7 +245,7 @@ int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_b
  * are maintained as in dqrm_emb_bwd_sgd. */
 int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                           int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, const int32_t* table_mask,
-                          int repack_bits, void* stream);
+                          int repack_bits, void* workspace, size_t workspace_bytes, void* stream);
 
 /* update modes for dqrm_apply_sparse_update */
 #define DQRM_UPD_DP        0  /* v = ((Q * (1/N)) * s) ; W += -lr * v   (s_q_g_p_c.py:885,618-622) */

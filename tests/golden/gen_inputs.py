@@ -15,11 +15,14 @@ import hashlib
 
 import numpy as np
 
-KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194, 27,
-               14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572]
-# reference TB profile at --max-ind-range=10M (python_profiling_script/finding_kaggle_compression_ratio.py:5)
-TERABYTE_ROWS = [9980200, 26095, 17224, 7383, 20152, 3, 7112, 1435, 62, 9756762, 1332128, 314263, 10, 2208,
-                 11168, 122, 4, 971, 14, 9994101, 7267918, 9946670, 415284, 12422, 102, 36]
+# table-size profiles live in the package (bench.py uses them too)
+import os as _os  # noqa: E402
+import sys as _sys  # noqa: E402
+
+_ROOT = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+if _ROOT not in _sys.path:
+    _sys.path.insert(0, _ROOT)
+from deep_quantized_recommendation_model_dqrm_amd.workloads import KAGGLE_ROWS, TERABYTE_ROWS  # noqa: E402,F401
 
 
 def table_weights(num_rows, dim, seed):

@@ -276,14 +276,84 @@ def test_invalid_indices_flag_not_fault(dq):
     assert ts.read_errors() & L.DQRM_ERRF_INDEX
 
 
-def test_capacity_overflow_is_flagged(dq):
-    """One row-range slot receiving more than DQRM_SLOT_KEYS lookups is flagged, not faulted."""
+@pytest.mark.parametrize("D", [16, 64])
+def test_large_batch_no_capacity_cliff(dq, D):
+    """B = 65,536 Criteo-form lookups per table (8x the in-LDS sort, so the tables sort in
+    the workspace) on 3-row and 971-row tables plus a wide one: coalesce, SGD and the local
+    update are bit-exact against the oracle -- the reference has no per-batch limit."""
+    rows, B = [3, 971, 200000], 65536
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 81)
+    P = G.pooling_one(rows, B, 82, dist="zipf")
+    P[0, : B // 2] = 1  # one 3-row table row holding half the batch: a 33k-lookup chain
+    dy = G.upstream_grad(T, B, D, 83)
+    ar = np.arange(B, dtype=np.int64)
+    ts = make_set(dq, Ws)
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+    ts.forward(b)
+    s = ts.scale.cpu().numpy()
+    ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+    ts.backward_coalesce(b, torch.from_numpy(dy).cuda(), ws)
+    for t in range(T):
+        r_o, v_o, err = O.emb_bwd_coalesce(rows[t], P[t], ar, dy[t], s[t])
+        r_g, v_g = _table_slots(ws, t)
+        np.testing.assert_array_equal(r_g, r_o)
+        np.testing.assert_array_equal(v_g, v_o)
+        am = ws.absmax.view(T, -1)[t].max().item()
+        assert am == np.abs(v_o).max()
+    ts.backward_sgd(b, torch.from_numpy(dy).cuda(), lr=0.1)
+    mask = torch.tensor([1, 0, 1], dtype=torch.int32, device="cuda")
+    ts.local_update(b, torch.from_numpy(dy).cuda(), 0.05, table_mask=mask)
+    assert ts.read_errors() == 0
+    for t in range(T):
+        Wo = Ws[t].copy()
+        O.emb_bwd_sgd(Wo, P[t], ar, dy[t], s[t], 0.1)
+        if t != 1:
+            O.emb_local_update(Wo, P[t], ar, dy[t], s[t], 0.05)
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Wo)
+    inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+    ts.refresh_absmax()
+    for x, y in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
+        assert torch.equal(x, y)
+
+
+def test_apply_crowded_slot_bitexact(dq, apply_kernel):
+    """Two ranks x 65,536 lookups: a 200k-row table's row-range slot merges > DQRM_SLOT_KEYS
+    payload entries (the slot kernel then applies it by the flat method) -- W equals
+    oracle.dp_step, and the |W| hierarchy equals a rebuild."""
+    rows, D, B, N = [971, 200000], 16, 65536, 2
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 91)
+    ts = make_set(dq, Ws)
+    Ps = [G.pooling_one(rows, B, 92 + r) for r in range(N)]
+    dys = [G.upstream_grad(T, B, D, 94 + r) for r in range(N)]
+    rank_batches = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+    ts.forward(rank_batches[0])
+    s_fwd = ts.scale.cpu().numpy()
+    wss, _, _, _ = _emulate_ranks(dq, ts, rank_batches, [torch.from_numpy(d).cuda() for d in dys], 8, 0.1)
+    assert max(int(ws.ucount.cpu().max()) for ws in wss) * N > dq._lib.DQRM_SLOT_KEYS
+    ar = np.arange(B, dtype=np.int64)
+    O.dp_step(Ws, [[(Ps[r][t], ar) for t in range(T)] for r in range(N)],
+              [[dys[r][t] for t in range(T)] for r in range(N)], s_fwd, 0.1, grad_bits=8)
+    assert ts.read_errors() == 0
+    for t in range(T):
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Ws[t])
+    inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+    ts.refresh_absmax()
+    for x, y in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
+        assert torch.equal(x, y)
+
+
+def test_max_lookups_understated_is_flagged(dq):
+    """A batch whose tables hold more lookups than dqrm_batch.max_lookups promised (the
+    workspace's size) is skipped and flagged, never written out of bounds."""
     ts = make_set(dq, G.table_weights([100], 16, 3))
     W0 = ts.W.clone()
     b = dq.LookupBatch.pooling_one(torch.zeros(1, 9000, dtype=torch.int64, device="cuda"))
+    b.c.max_lookups = 100
     ts.backward_sgd(b, torch.ones(1, 9000, 16, device="cuda"), lr=0.1)
     assert ts.read_errors() & dq._lib.DQRM_ERRF_OVERFLOW
-    assert torch.equal(ts.W, W0)  # the overflowing slot did not touch its rows
+    assert torch.equal(ts.W, W0)
 
 
 def test_kaggle_full_size_forward_and_step(dq):
