@@ -1385,92 +1385,6 @@ DQRM_INLINE void visit_slot_lookups(const int64_t* off, const int64_t* idx, int6
     }
 }
 
-DQRM_INLINE int gather_lookup_keys(uint64_t* keys, int* s_wsum, const int64_t* idx, const int64_t* off,
-                                   const int64_t* idx_base, int64_t B, int t, int64_t nrows,
-                                   int64_t r0, int64_t r1, bool report, uint32_t* err, bool pool1) {
-    const int64_t ib = idx_base[t];
-    const int64_t L = idx_base[t + 1] - ib;
-    const int64_t* __restrict__ toff = off + (int64_t)t * B;
-    const int64_t* __restrict__ tidx = idx + ib;
-    const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
-    const int64_t per = (B + blockDim.x - 1) / blockDim.x;
-    const int64_t b0 = (int64_t)tid * per, b1 = b0 + per < B ? b0 + per : B;
-    constexpr int RC = 8;  // matches kept in registers (pass 2 re-reads only past RC)
-    uint64_t cache[RC];
-    int cnt = 0;
-    visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, report, err, pool1, [&](int64_t r, int64_t b) {
-        if (r >= r0 && r < r1) {
-            const uint64_t key = ((uint64_t)r << 32) | (uint64_t)b;
-#pragma unroll
-            for (int c = 0; c < RC; ++c)
-                if (c == cnt) cache[c] = key;
-            ++cnt;
-        }
-    });
-    int v = cnt;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        int y = __shfl_up(v, o, WAVE);
-        if (lane >= o) v += y;
-    }
-    if (lane == WAVE - 1) s_wsum[w] = v;
-    __syncthreads();
-    if (tid == 0) {
-        int run = 0;
-        for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) { int x = s_wsum[k]; s_wsum[k] = run; run += x; }
-        s_wsum[blockDim.x / WAVE] = run;
-    }
-    __syncthreads();
-    const int n = s_wsum[blockDim.x / WAVE];
-    if (n > SLOT_KEYS) {
-        if (tid == 0) flag_error(err, DQRM_ERRF_OVERFLOW);
-        return -1;
-    }
-    int pos = s_wsum[w] + v - cnt;
-    if (cnt <= RC) {
-#pragma unroll
-        for (int c = 0; c < RC; ++c)
-            if (c < cnt) keys[pos + c] = cache[c];
-    } else {
-        visit_slot_lookups(toff, tidx, B, L, nrows, b0, b1, false, err, pool1, [&](int64_t r, int64_t b) {
-            if (r >= r0 && r < r1) keys[pos++] = ((uint64_t)r << 32) | (uint64_t)b;
-        });
-    }
-    __syncthreads();
-    return n;
-}
-
-struct BwdArgs {
-    int pool1;  // DQRM_BATCH_POOLING_ONE
-    float* W;
-    uint8_t* packed;
-    float* rowmax;
-    float* blkmax;
-    float* sblkmax;
-    uint8_t* sdirty;
-    const float* scale;
-    const float* pscale;
-    const int64_t* meta;
-    uint32_t* err;
-    const int64_t* idx;
-    const int64_t* off;
-    const int64_t* idx_base;
-    const float* dy;
-    int64_t B;
-    int64_t dst_t, dst_b;
-    int T;
-    int ste;
-    float nlr;          // -lr (f32)
-    int repack;         // repack touched INT4 rows with pscale
-    // coalesce mode outputs (slot workspace)
-    const int64_t* ws_cap_base;
-    int32_t* ws_rows;
-    float* ws_vals;
-    int32_t* ws_ucount;
-    float* ws_absmax;
-    const int32_t* tmask;  // MODE 2: tables to update (nullable = all)
-};
-
 // dy row of bag `lo` for the STE backward: g' = (g * s) / s  (quant_utils.py:349-363);
 // off4 = first float4 of the row this slot owns (dimension-split tables)
 struct DySource {
@@ -1506,182 +1420,6 @@ struct DimSplit {
 };
 
 DQRM_INLINE bool narrow_table(int64_t nrows) { return nrows <= BLK; }
-
-// MODE 0: fused SGD (single GPU);  MODE 1: coalesce + per-slot max |grad| (DP)
-template <int LPR, int LPRS, int MODE>
-DQRM_INLINE void bwd_segments(const BwdArgs& a, const SlotLds& sl, uint16_t* s_long, int* s_wsum,
-                              unsigned int* s_misc, const Meta& m, int t, int slot, int U, int n, int off4,
-                              bool dsplit, int64_t ws_e0, int64_t cap) {
-    constexpr int D = LPR * 4;
-    uint64_t* keys = sl.keys;
-    const uint16_t* heads = sl.heads;
-    const int64_t rb = m.row_base[t];
-    DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, off4};
-    const float r_pack = (MODE != 1 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
-    float local_absmax = 0.0f;
-
-    auto finit = [&](int, int i, int sub, SegState& st) {
-        const int64_t grow = rb + key_row(keys[i]);
-        if (MODE != 1) {
-            st.acc = reinterpret_cast<const float4*>(a.W + grow * D)[off4 + sub];
-            st.w = st.acc;  // old row (its max is taken in ffin, after every load is in flight)
-            if (!dsplit) st.blk = a.blkmax[m.blk_base[t] + (key_row(keys[i]) >> 8)];
-        } else {
-            st.acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    auto ffin = [&](int u, int i, int sub, SegState& st) {
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        if (MODE != 1) {
-            reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = st.acc;
-            if (a.repack) pack4_row(st.acc, a.packed + grow * (D / 2), off4 + sub, r_pack);
-            if (!dsplit) {
-                const float old_rm = group_max<LPRS>(abs_max4(st.w));
-                const float rm = group_max<LPRS>(abs_max4(st.acc));
-                if (sub == 0) {
-                    a.rowmax[grow] = rm;
-                    keys[i] = with_lo(keys[i], row_record(rm, old_rm, st.blk));
-                }
-            }
-        } else {
-            if (u < cap) {
-                const int64_t e = ws_e0 + u;
-                reinterpret_cast<float4*>(a.ws_vals + e * D)[off4 + sub] = st.acc;
-                if (sub == 0 && off4 == 0) a.ws_rows[e] = (int32_t)row;
-            }
-            local_absmax = fmaxf(local_absmax, abs_max4(st.acc));
-        }
-    };
-    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
-    short_segments<LPRS, OP, 8>(keys, heads, U, n, src, a.nlr, finit, ffin);
-
-    using DL = DimLane<LPRS>;
-    auto fbegin = [&](int i, int lig, float (&v)[DL::NDL]) {
-        const int64_t grow = rb + key_row(keys[i]);
-#pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) v[d] = MODE != 1 ? a.W[grow * D + off4 * 4 + lig + DL::GD * d] : 0.0f;
-    };
-    auto fend = [&](int u, int i, int lig, float (&v)[DL::NDL]) {
-        const uint32_t row = key_row(keys[i]);
-        const int64_t grow = rb + row;
-        if (MODE != 1) {
-            float old_rm = 0.0f, old_blk = 0.0f;
-            if (!dsplit) {  // the row is still unwritten (and cached since fbegin): its old max
-                float w0[DL::NDL];
-#pragma unroll
-                for (int d = 0; d < DL::NDL; ++d) w0[d] = a.W[grow * D + lig + DL::GD * d];
-                old_rm = dl_absmax<LPRS>(w0);
-                old_blk = a.blkmax[m.blk_base[t] + (row >> 8)];
-            }
-#pragma unroll
-            for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = v[d];
-            if (a.repack) dl_pack_int4<LPRS>(v, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
-            if (!dsplit) {
-                const float rm = dl_absmax<LPRS>(v);
-                if (lig == 0) {
-                    a.rowmax[grow] = rm;
-                    keys[i] = with_lo(keys[i], row_record(rm, old_rm, old_blk));
-                }
-            }
-        } else {
-            if (u < cap) {
-                const int64_t e = ws_e0 + u;
-#pragma unroll
-                for (int d = 0; d < DL::NDL; ++d) a.ws_vals[e * D + off4 * 4 + lig + DL::GD * d] = v[d];
-                if (lig == 0 && off4 == 0) a.ws_rows[e] = (int32_t)row;
-            }
-            local_absmax = fmaxf(local_absmax, dl_absmax<LPRS>(v));
-        }
-    };
-    const int nlong = compact_long(heads, U, n, s_long, s_wsum);
-    DIAG_T(3);
-    staged_long_segments<LPRS, OP>(sl, U, n, s_long, nlong, s_wsum, src, a.nlr, fbegin, fend);
-    DIAG_T(4);
-    if (MODE == 1) {
-        local_absmax = wave_max(local_absmax);
-        if ((threadIdx.x % WAVE) == 0) atomicMax(&s_misc[1], __float_as_uint(local_absmax));
-    }
-    __syncthreads();
-    if (MODE != 1) {
-        if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty,
-                                     reinterpret_cast<int*>(&s_misc[2]));
-    } else if (threadIdx.x == 0) {
-        if (U > cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        const int32_t used = U < cap ? U : (int32_t)cap;
-        if (!dsplit) {
-            a.ws_ucount[slot] = used;
-        } else {
-            if (off4 == 0) a.ws_ucount[t * SPLIT + SPLIT - 1] = used;
-            if (slot % SPLIT != SPLIT - 1) a.ws_ucount[slot] = 0;
-        }
-        a.ws_absmax[slot] = __uint_as_float(s_misc[1]);
-    }
-}
-
-template <int LPR, int MODE>
-__global__ void __launch_bounds__(TWG) k_table_bwd(BwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const SlotLds sl(lds);
-    __shared__ int s_wsum[TWG / WAVE + 8];   // 64 B: static LDS stays a multiple of 16
-    __shared__ unsigned int s_misc[4];
-    __shared__ uint16_t s_long[(LONG_SEGS_MAX + 7) / 8 * 8];
-
-    const int t = blockIdx.x / SPLIT, s = blockIdx.x % SPLIT;
-    if (MODE == 2 && a.tmask != nullptr && a.tmask[t] == 0) return;  // table not selected
-    const int T = a.T;
-    Meta m = make_meta(a.meta, T);
-    const int64_t nrows = m.num_rows[t];
-    const int slot = t * SPLIT + s;
-    const bool dsplit = narrow_table(nrows);
-    using DS = DimSplit<LPR>;
-    int64_t r0, r1;
-    int off4 = 0;
-    if (dsplit) {
-        r0 = 0;
-        r1 = nrows;
-        off4 = s * DS::LPRS;
-        if (s >= DS::ACTIVE) {  // no slice for this slot (D < 4 * SPLIT)
-            if (MODE == 1 && threadIdx.x == 0) {
-                if (s != SPLIT - 1) a.ws_ucount[slot] = 0;
-                a.ws_absmax[slot] = 0.0f;
-            }
-            return;
-        }
-    } else {
-        slot_rows(nrows, s, r0, r1);
-    }
-    const int own = dsplit ? t * SPLIT + SPLIT - 1 : slot;  // workspace slot of these rows
-    if (threadIdx.x == 1) s_misc[1] = 0u;
-    DIAG_T(0);
-
-    const int n = gather_lookup_keys(sl.keys, s_wsum, a.idx, a.off, a.idx_base, a.B, t, nrows, r0, r1, s == 0,
-                                     a.err, a.pool1 != 0);
-    if (n < 0) {
-        if (MODE == 1 && threadIdx.x == 0) {
-            if (off4 == 0) a.ws_ucount[own] = 0;
-            if (!dsplit || s != SPLIT - 1) a.ws_ucount[slot] = 0;
-            a.ws_absmax[slot] = 0.0f;
-        }
-        return;
-    }
-#if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 1
-    if (n >= 0) return;  // diagnostic build: gather only
-#endif
-    DIAG_T(1);
-    const int U = sort_and_heads(sl, n, (uint32_t)r0, (uint32_t)(r1 - r0), s_wsum);
-    DIAG_T(2);
-#if defined(DQRM_DIAG_STOP) && DQRM_DIAG_STOP == 2
-    if (U >= 0) return;  // diagnostic build: gather + sort + heads
-#endif
-    const int64_t ws_e0 = MODE == 1 ? a.ws_cap_base[own] : 0;
-    const int64_t cap = MODE == 1 ? a.ws_cap_base[own + 1] - ws_e0 : 0;
-    if (dsplit)
-        bwd_segments<LPR, DS::LPRS, MODE>(a, sl, s_long, s_wsum, s_misc, m, t, slot, U, n, off4, true, ws_e0, cap);
-    else
-        bwd_segments<LPR, LPR, MODE>(a, sl, s_long, s_wsum, s_misc, m, t, slot, U, n, 0, false, ws_e0, cap);
-    DIAG_T(5);
-}
 
 // ------------------------------------------------------------------------------------
 // K5: scale average + quantize-pack (slot workspace -> dense wire payload)
@@ -2304,32 +2042,8 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// K4: backward = STE (quant_utils.py:349-363) + EmbeddingBag sparse backward, then one of
-//   MODE 0  torch.optim.SGD on the uncoalesced grad        (dlrm_s_pytorch_single_gpu.py:1736-1750)
-//   MODE 1  grad.coalesce() + per-slot max|grad|           (s_q_g_p_c.py:859-861)
-//   MODE 2  W.add_(-lr * grad), product rounded            (s_q_g_p_c.py:615-616, ranking range)
-// in two launches, with no per-batch capacity:
-//   K4a k_sort_slots   one 512-thread workgroup per (table, row-range slot): the slot's valid
-//       lookups as keys (row << 32 | bag) in lookup order (a stable ballot compaction of the
-//       table's lookups), a stable LSD radix sort by row (8-bit digits, wave-ballot ranks;
-//       in LDS up to SORT_LDS_KEYS keys, in the caller's workspace beyond), then one 32-byte
-//       record per distinct row {row, bags 1..4, slot, length, coalesced-workspace entry}
-//       APPENDED to a chip-wide record list (the slot reserves its run with one atomicAdd),
-//       and the slot's long segments with one work item per long-stream chunk and dimension
-//       slice. The last workgroup to finish publishes the list lengths and re-arms the
-//       counters (the workspace's counters are zero between calls).
-//   K4b k_bwd_segments  one float4 lane group per short record (<= LONG_SEG lookups: nearly
-//       every row of a wide table), SEG_SB records in flight, straight from the record list
-//       (record -> dy rows: two round trips); long items (hot rows of narrow / power-law
-//       tables) stream their lookups through an LDS stage, each segment combined strictly
-//       in lookup order by one dim-lane group that carries its running row across stage
-//       chunks, the D dimensions split over DS work items (independent chains, so a 3-row
-//       table's 700-lookup chains run on 3 x DS CUs).
-// Every row's lookups are combined in ascending lookup order, as the reference's torch
-// ops accumulate duplicates (sparse SGD axpy / coalesce); the list order (atomic) never
-// reaches a result. Wide-table SGD keeps the |W| hierarchy with the flat protocol (atomicMax
-// growth, dirty flags for shrunk holders, tracked finalize); narrow tables are rebuilt by
-// finalize.
+// Sort and gather helpers of the fused backward (K4, below): a workgroup of SORT_TPB threads
+// sorts one slot's (row << 32 | position) keys in LDS or in the caller's workspace.
 // ------------------------------------------------------------------------------------
 constexpr int SORT_TPB = 512;
 constexpr int SORT_WAVES = SORT_TPB / WAVE;
@@ -2337,63 +2051,6 @@ constexpr int SORT_LDS_KEYS = 4096;                 // keys a slot sorts in LDS 
 constexpr int SORT_KC = SORT_LDS_KEYS / SORT_TPB;   // key batches per lane cached in registers
 constexpr int RADIX = 256;
 constexpr int HP = SORT_WAVES + 1;                  // [digit][wave] counter pitch (odd: no bank conflicts)
-constexpr int SORT_LDS = SORT_LDS_KEYS * 16 + RADIX * HP * 4;
-static_assert(SORT_LDS + 2048 <= 160 * 1024, "sort LDS budget");
-constexpr int LONG_RANGE = 512;   // long-stream lookups whose segments one long item owns
-constexpr int SEG_TPB = 256;
-constexpr int SEG_SB = 4;         // short records in flight per lane group
-constexpr int LSTAGE = 4096;      // floats of the long-segment LDS stage (16 KiB, + pad)
-constexpr int LMAXK = LONG_RANGE / (LONG_SEG + 1) + 2;
-constexpr int DS_MAX = 8;
-constexpr int LONG_WGS = 256;     // K4b workgroups looping over the long items
-constexpr uint32_t REC_LEN_MAX = (1u << 21) - 1;
-
-template <int LPR>
-struct SegGeom {
-    static constexpr int D = LPR * 4;
-    static constexpr int DS = LPR < DS_MAX ? LPR : DS_MAX;  // dim slices of a long segment (>= 4 dims)
-    static constexpr int NG = SEG_TPB / LPR;                 // float4 lane groups
-    static constexpr int US = NG * SEG_SB;                   // records per short workgroup
-};
-
-struct SortWs {
-    uint64_t* skey;   // [T*S][Lc] every slot's sorted keys (row << 32 | bag)
-    uint64_t* skey2;  // [T*S][Lc] radix ping-pong (only when Lc > SORT_LDS_KEYS)
-    uint4* rec;       // [T*Lc] record list: {row, bag0, slot | min(len, REC_LEN_MAX) << 11, ws entry}
-    uint4* rbag;      // [T*Lc] {bag1, bag2, bag3, first key} (length > 1)
-    uint4* lrec;      // [T*S][Lc] every slot's long segments in order: {row, first key, record or
-                      //            ws entry (MODE 1), long-stream start}
-    uint4* litem;     // [NLI] long items {slot | slice << 16, first, end, stream end}
-    uint32_t* ctr;    // [8] {records, long items, slots done, records (final), long items (final)}
-    int64_t nli;      // long-item capacity
-};
-
-__host__ __device__ inline int64_t long_item_cap(int T, int64_t Lc) {
-    return ((int64_t)T * SPLIT + (int64_t)T * ((Lc + LONG_RANGE - 1) / LONG_RANGE)) * DS_MAX;
-}
-
-// byte layout of the backward workspace (base == nullptr: sizes only); returns its bytes
-__host__ __device__ inline int64_t sort_ws_layout(unsigned char* base, int T, int64_t Lc, SortWs* ws) {
-    int64_t o = 0;
-    auto take = [&](int64_t bytes) {
-        const int64_t p = o;
-        o += align16(bytes);
-        return base ? base + p : nullptr;
-    };
-    const int64_t TL = (int64_t)T * Lc, TSL = TL * SPLIT;
-    SortWs w;
-    w.ctr = reinterpret_cast<uint32_t*>(take(64));
-    w.skey = reinterpret_cast<uint64_t*>(take(TSL * 8));
-    w.skey2 = reinterpret_cast<uint64_t*>(take(Lc > SORT_LDS_KEYS ? TSL * 8 : 0));
-    w.rec = reinterpret_cast<uint4*>(take(TL * 16));
-    w.rbag = reinterpret_cast<uint4*>(take(TL * 16));
-    w.lrec = reinterpret_cast<uint4*>(take(TSL * 16));
-    w.nli = long_item_cap(T, Lc);
-    w.litem = reinterpret_cast<uint4*>(take(w.nli * 16));
-    if (ws) *ws = w;
-    return o;
-}
-
 // exclusive prefix of one int per thread over NT threads; *total = the sum.
 // s_w: NT/WAVE + 1 ints. Two barriers.
 template <int NT>
@@ -2524,52 +2181,99 @@ DQRM_INLINE void radix_sort_rows(uint64_t* keys, uint64_t* tmp, int n, uint32_t 
     }
 }
 
-// Bitonic sort of n <= SORT_TPB keys, one per thread (padding ~0), ascending: exchanges
-// within a wave by shuffles, across waves through LDS. Keys equal in (row, bag) stand for
-// the same dy row, so the result equals the stable sort by row.
-DQRM_INLINE void bitonic_sort_keys(uint64_t* keys, int n, uint64_t* xch) {
-    const int tid = threadIdx.x;
-    uint64_t x = tid < n ? keys[tid] : ~0ull;
-    int n2 = 2;
-    while (n2 < n) n2 <<= 1;
-    for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            uint64_t y;
-            if (j >= WAVE) {
-                xch[tid] = x;
-                __syncthreads();
-                y = xch[tid ^ j];
-                __syncthreads();
-            } else {
-                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, j, WAVE);
-                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j, WAVE);
-                y = ((uint64_t)hi << 32) | lo;
-            }
-            const bool keep_min = ((tid & j) == 0) == ((tid & k) == 0);
-            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+// Sort of a slot whose keys are few for their row span (a wide table's slot): ONE stable
+// 8-bit radix pass on the TOP digit of (row - r0) puts the keys into 256 row-ordered buckets
+// of ~n/256 keys, and one thread per bucket finishes it by insertion sort on the full
+// (unique) key. A bucket above FIX_MAX keys (power-law rows) falls back to the full LSD radix
+// from the untouched input. keys -> keys; tmp, hist as for radix_sort_rows.
+constexpr int FIX_MAX = 32;
+DQRM_INLINE void msd_sort_rows(uint64_t* keys, uint64_t* tmp, int n, uint32_t r0, int nbits, int* hist, int* s_scan,
+                               int* s_flag) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const int kpl = (n + SORT_TPB - 1) / SORT_TPB;
+    const int i0 = w * WAVE * kpl + lane;
+    const uint64_t lt = lanemask_lt();
+    const int sh = nbits - 8;
+    int* start = hist + RADIX * HP;  // bucket starts [RADIX + 1]
+    for (int j = threadIdx.x; j < RADIX * HP; j += SORT_TPB) hist[j] = 0;
+    if (threadIdx.x == 0) *s_flag = 0;
+    __syncthreads();
+    uint64_t cx[SORT_KC], cm[SORT_KC];
+    uint32_t cd[SORT_KC];
+#pragma unroll
+    for (int k = 0; k < SORT_KC; ++k)
+        if (k < kpl) {
+            radix_batch(keys, i0 + k * WAVE, n, r0, sh, cx[k], cd[k], cm[k]);
+            if (i0 + k * WAVE < n && (cm[k] >> lane) == 1ull) hist[cd[k] * HP + w] += (int)__popcll(cm[k]);
+        }
+    __syncthreads();
+    {
+        int* h = hist + (threadIdx.x / 2) * HP + (threadIdx.x % 2) * 4;
+        const int h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3];
+        int tot;
+        const int ex = block_scan_excl<SORT_TPB>(h0 + h1 + h2 + h3, s_scan, &tot);
+        h[0] = ex; h[1] = ex + h0; h[2] = ex + h0 + h1; h[3] = ex + h0 + h1 + h2;
+        if (threadIdx.x % 2 == 0) start[threadIdx.x / 2] = ex;
+        if (threadIdx.x == 0) start[RADIX] = tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SORT_KC; ++k)
+        if (k < kpl && i0 + k * WAVE < n) {
+            int* hp = hist + cd[k] * HP + w;
+            const int pos = *hp + (int)__popcll(cm[k] & lt);
+            tmp[pos] = cx[k];
+            if ((cm[k] >> lane) == 1ull) *hp = pos + 1;
+        }
+    if (threadIdx.x < RADIX && start[threadIdx.x + 1] - start[threadIdx.x] > FIX_MAX) *s_flag = 1;
+    __syncthreads();
+    if (*s_flag) {  // crowded bucket: the full LSD sort of the original keys
+        radix_sort_rows(keys, tmp, n, r0, nbits, hist, s_scan);
+        return;
+    }
+    if (threadIdx.x < RADIX) {  // insertion sort of bucket d, written back to keys
+        const int b0 = start[threadIdx.x], b1 = start[threadIdx.x + 1];
+        for (int i = b0; i < b1; ++i) {
+            const uint64_t x = tmp[i];
+            int j = i;
+            while (j > b0 && keys[j - 1] > x) { keys[j] = keys[j - 1]; --j; }
+            keys[j] = x;
         }
     }
-    if (tid < n) keys[tid] = x;
     __syncthreads();
 }
 
-struct SortArgs {
-    const int64_t* idx;
-    const int64_t* off;
-    const int64_t* idx_base;
-    int64_t B;
-    int pool1;
-    const int64_t* meta;
-    int T;
-    uint32_t* err;
-    SortWs ws;
-    int64_t Lc;
-    int ds;                      // dimension slices of a long item (K4b's SegGeom<LPR>::DS)
-    const int32_t* tmask;        // MODE 2: tables to update (nullable = all)
-    const int64_t* ws_cap_base;  // MODE 1: coalesced workspace slots
-    int32_t* ws_ucount;
-    float* ws_absmax;
-};
+// gather_slot_keys for a Criteo-form batch whose indices the caller already loaded: the
+// thread's bags [tid*per, +per) (per <= 8) are pre[0..per)
+DQRM_INLINE int gather_slot_keys_pre(uint64_t* lds_keys, uint64_t* ws_keys, bool* in_lds, int* s_scan,
+                                     const int64_t (&pre)[8], int per, int64_t B, int64_t nrows, int64_t r0,
+                                     int64_t r1, bool report, uint32_t* err) {
+    const int64_t b0 = (int64_t)threadIdx.x * per;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t r = pre[j];
+        if (j < per && b0 + j < B) {
+            if (r < 0 || r >= nrows) {
+                if (report) flag_error(err, DQRM_ERRF_INDEX);
+            } else if (r >= r0 && r < r1) {
+                ++cnt;
+            }
+        }
+    }
+    int total;
+    int pos = block_scan_excl<SORT_TPB>(cnt, s_scan, &total);
+    *in_lds = total <= SORT_LDS_KEYS;
+    uint64_t* keys = *in_lds ? lds_keys : ws_keys;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t r = pre[j];
+        if (j < per && b0 + j < B && r >= r0 && r < r1 && r < nrows)
+            keys[pos++] = ((uint64_t)r << 32) | (uint64_t)(b0 + j);
+    }
+    __syncthreads();
+    return total;
+}
 
 // the slot's keys (row in [r0, r1)) in lookup order into LDS (n <= SORT_LDS_KEYS) or the
 // workspace: each thread owns a contiguous run of bags (count, block scan, write; RC keys
@@ -2610,221 +2314,52 @@ DQRM_INLINE int gather_slot_keys(uint64_t* lds_keys, uint64_t* ws_keys, bool* in
     return total;
 }
 
-// sort one slot's keys, append its records and long items; returns the slot's distinct rows
-// s_base[0] / s_base[3]: the slot's record run (reserved by the caller) and its length
-template <int MODE>
-DQRM_INLINE int sort_slot(const SortArgs& a, int k, int t, int64_t r0, int64_t r1, int n, uint64_t* keys,
-                          uint64_t* tmp, int* hist, int* s_scan, int* s_wl, uint32_t* s_base, int64_t ws_e0,
-                          int64_t ws_cap, bool wide) {
-    const int64_t Lc = a.Lc;
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
-    const uint32_t span = (uint32_t)(r1 - r0);
-    const int nbits = span <= 1 ? 0 : 32 - __builtin_clz(span - 1);
-    if (n <= SORT_TPB && nbits > 8)  // small slot of a wide table: one bitonic network
-        bitonic_sort_keys(keys, n, tmp);
-    else
-        radix_sort_rows(keys, tmp, n, (uint32_t)r0, nbits, hist, s_scan);
-    DIAG_T(2);
-
-    // segment heads (first key of every distinct row) -> hpos, in order
-    uint32_t* hpos = reinterpret_cast<uint32_t*>(tmp);
-    uint32_t* lst = hpos + n;  // long segments' stream starts (tmp holds 2n words)
-    const uint64_t lt = lanemask_lt();
-    int U;
-    {
-        const int kpl = (n + SORT_TPB - 1) / SORT_TPB;
-        const int i0 = w * WAVE * kpl + lane;
-        auto is_head = [&](int i) { return i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1])); };
-        int hc = 0;
-        for (int q = 0; q < kpl; ++q) hc += (int)__popcll(__ballot(is_head(i0 + q * WAVE)));
-        if (lane == 0) s_wl[w] = hc;
-        __syncthreads();
-        int run = 0;
-        U = 0;
-        for (int q = 0; q < SORT_WAVES; ++q) { const int c = s_wl[q]; run += q < w ? c : 0; U += c; }
-        for (int q = 0; q < kpl; ++q) {
-            const int i = i0 + q * WAVE;
-            const bool h = is_head(i);
-            const uint64_t hm = __ballot(h);
-            if (h) hpos[run + __popcll(hm & lt)] = (uint32_t)i;
-            run += (int)__popcll(hm);
-        }
-        __syncthreads();
-    }
-    DIAG_T(3);
-    const uint32_t rbase = s_base[0];  // the run reserved before the sort: rcap >= U records
-    const int rcap = (int)s_base[3];
-    if ((int64_t)rbase + rcap > (int64_t)a.T * Lc) {  // only with a workspace not zero-filled
-        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        return 0;
-    }
-    for (int u = U + threadIdx.x; u < rcap; u += SORT_TPB) a.ws.rec[rbase + u] = make_uint4(0u, 0u, 0u, 0u);
-    // records (+ the 2nd..4th bags); long segments by ordered compaction with their stream start
-    uint4* lrec = a.ws.lrec + (int64_t)k * Lc;
-    const int kpu = (U + SORT_TPB - 1) / SORT_TPB;
-    const int u0 = w * WAVE * kpu + lane;
-    auto seg_len = [&](int u) { return (int)((u + 1 < U ? hpos[u + 1] : (uint32_t)n) - hpos[u]); };
-    int nl = 0, el = 0;
-    for (int q = 0; q < kpu; ++q) {
-        const int u = u0 + q * WAVE;
-        const bool v = u < U;
-        int len = 0;
-        if (v) {
-            const uint32_t i = hpos[u];
-            len = seg_len(u);
-            const uint64_t x = keys[i];
-            const uint32_t e = MODE == 1 ? (u < ws_cap ? (uint32_t)(ws_e0 + u) : 0xFFFFFFFFu) : 0u;
-            const uint32_t ln = (uint32_t)len < REC_LEN_MAX ? (uint32_t)len : REC_LEN_MAX;
-            a.ws.rec[rbase + u] = make_uint4(key_row(x), key_lo(x), (uint32_t)k | (ln << 11), e);
-            if (len > 1)
-                a.ws.rbag[rbase + u] = make_uint4(key_lo(keys[i + 1]), len > 2 ? key_lo(keys[i + 2]) : 0u,
-                                                  len > 3 ? key_lo(keys[i + 3]) : 0u, i);
-        }
-        const bool lg = v && len > LONG_SEG;
-        nl += (int)__popcll(__ballot(lg));
-        el += lg ? len : 0;
-    }
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) el += __shfl_xor(el, o, WAVE);
-    if (lane == 0) { s_wl[w] = nl; s_wl[SORT_WAVES + w] = el; }
-    __syncthreads();
-    DIAG_T(4);
-    int kb = 0, eb = 0, nlong = 0, elong = 0;
-    for (int q = 0; q < SORT_WAVES; ++q) {
-        const int c = s_wl[q], e = s_wl[SORT_WAVES + q];
-        kb += q < w ? c : 0;
-        eb += q < w ? e : 0;
-        nlong += c;
-        elong += e;
-    }
-    if (nlong > 0) {  // uniform
-        for (int q = 0; q < kpu; ++q) {
-            const int u = u0 + q * WAVE;
-            const int len = u < U ? seg_len(u) : 0;
-            const bool lg = len > LONG_SEG;
-            const uint64_t lm = __ballot(lg);
-            int inc = lg ? len : 0;  // inclusive scan of the long lengths over the batch
-#pragma unroll
-            for (int o = 1; o < WAVE; o <<= 1) {
-                const int y = __shfl_up(inc, o, WAVE);
-                if (lane >= o) inc += y;
-            }
-            if (lg) {
-                const int j = kb + (int)__popcll(lm & lt);
-                const uint32_t i = hpos[u], st = (uint32_t)(eb + inc - len);
-                const uint32_t e = MODE == 1 ? (u < ws_cap ? (uint32_t)(ws_e0 + u) : 0xFFFFFFFFu) : (uint32_t)u;
-                lrec[j] = make_uint4(key_row(keys[i]), i, e, st);
-                lst[j] = st;
-            }
-            kb += (int)__popcll(lm);
-            eb += __shfl(inc, WAVE - 1, WAVE);
-        }
-        __syncthreads();
-        // one item per long-stream chunk holding a segment start, per dimension slice
-        const int dsx = (MODE != 1 && wide) ? 1 : a.ds;  // wide-table SGD: full rows (rowmax)
-        auto chunk_head = [&](int j) { return j < nlong && (j == 0 || lst[j - 1] / LONG_RANGE != lst[j] / LONG_RANGE); };
-        int hc = 0;
-        for (int j = threadIdx.x; j < nlong; j += SORT_TPB) hc += chunk_head(j) ? 1 : 0;
-        int tot;
-        block_scan_excl<SORT_TPB>(hc, s_scan, &tot);
-        if (threadIdx.x == 0) s_base[1] = atomicAdd(&a.ws.ctr[1], (uint32_t)(tot * dsx));
-        if (threadIdx.x == 0) s_base[2] = 0u;
-        __syncthreads();
-        const uint32_t ibase = s_base[1];
-        for (int j = threadIdx.x; j < nlong; j += SORT_TPB) {
-            if (!chunk_head(j)) continue;
-            int je = j + 1;
-            while (je < nlong && !chunk_head(je)) ++je;
-            const uint32_t send = je < nlong ? lst[je] : (uint32_t)elong;
-            const uint32_t slot_i = atomicAdd(&s_base[2], (uint32_t)dsx);  // item order is immaterial
-            for (int z = 0; z < dsx; ++z) {
-                const int64_t it = (int64_t)ibase + slot_i + z;
-                if (it < a.ws.nli)
-                    a.ws.litem[it] = make_uint4((uint32_t)k | ((uint32_t)z << 16), (uint32_t)j, (uint32_t)je, send);
-                else
-                    flag_error(a.err, DQRM_ERRF_OVERFLOW);
-            }
-        }
-    }
-    return U;
+template <int OP>
+DQRM_INLINE float seg_op(float acc, float v, float nlr) {
+    if (OP == OP_FMA) return fmaf(v, nlr, acc);
+    if (OP == OP_AXPY) return acc + v * nlr;
+    return acc + v;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(SORT_TPB) k_sort_slots(SortArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ int s_scan[SORT_WAVES + 1];
-    __shared__ int s_wl[2 * SORT_WAVES];
-    __shared__ uint32_t s_base[4];
-    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
-    DIAG_T(0);
-    const Meta m = make_meta(a.meta, a.T);
-    const int64_t nrows = m.num_rows[t];
-    int64_t r0, r1;
-    slot_rows(nrows, s, r0, r1);
-    // Criteo form: L_t == B for every table, so the table's lookups start at t * B (no
-    // dependent idx_base round trip before the index loads)
-    const int64_t ib = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
-    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ib;
-    const bool skip = (MODE == 2 && a.tmask != nullptr && a.tmask[t] == 0) || r0 >= r1;
-    int64_t ws_e0 = 0, ws_cap = 0;
-    if (MODE == 1) {
-        ws_e0 = a.ws_cap_base[k];
-        ws_cap = a.ws_cap_base[k + 1] - ws_e0;
-    }
-    int U = 0;
-    if (!skip) {  // uniform
-        if (L > a.Lc) {  // more lookups than the caller planned for: skipped, flagged
-            if (threadIdx.x == 0 && s == SPLIT - 1) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        } else {
-            uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds);
-            int* hist = reinterpret_cast<int*>(lds + SORT_LDS_KEYS * 16);
-            bool in_lds;
-            const int n = gather_slot_keys(lkeys, a.ws.skey + (int64_t)k * a.Lc, &in_lds, s_scan,
-                                           a.off + (int64_t)t * a.B, a.idx + ib, a.B, L, nrows, r0, r1,
-                                           s == SPLIT - 1, a.err, a.pool1 != 0);
-            DIAG_T(1);
-            if (n > 0) {
-                // reserve the record run now (distinct rows <= min(n, slot rows)): the atomic's
-                // round trip overlaps the sort; records past the actual count are left empty
-                const int rcap = (int)(n < r1 - r0 ? n : r1 - r0);
-                if (threadIdx.x == 0) {
-                    s_base[0] = atomicAdd(&a.ws.ctr[0], (uint32_t)rcap);
-                    s_base[3] = (uint32_t)rcap;
-                }
-                const bool wide = nrows > BLK;
-                if (in_lds) {
-                    U = sort_slot<MODE>(a, k, t, r0, r1, n, lkeys, lkeys + SORT_LDS_KEYS, hist, s_scan, s_wl,
-                                        s_base, ws_e0, ws_cap, wide);
-                    uint64_t* sk = a.ws.skey + (int64_t)k * a.Lc;  // publish the sorted keys
-                    for (int i = threadIdx.x; i < n; i += SORT_TPB) sk[i] = lkeys[i];
-                } else {
-                    U = sort_slot<MODE>(a, k, t, r0, r1, n, a.ws.skey + (int64_t)k * a.Lc,
-                                        a.ws.skey2 + (int64_t)k * a.Lc, hist, s_scan, s_wl, s_base, ws_e0, ws_cap,
-                                        wide);
-                }
-            }
-        }
-    }
-    if (threadIdx.x == 0) {
-        if (MODE == 1) {
-            if (U > ws_cap) flag_error(a.err, DQRM_ERRF_OVERFLOW);  // undersized coalesced workspace
-            a.ws_ucount[k] = U < ws_cap ? U : (int32_t)ws_cap;
-            a.ws_absmax[k] = 0.0f;
-        }
-        DIAG_T(5);
-        // every slot's list runs are reserved (the atomics above returned before this one):
-        // the last slot publishes the list lengths and re-arms the counters for the next call
-        const uint32_t done = atomicAdd(&a.ws.ctr[2], 1u);
-        if (done == gridDim.x - 1) {
-            a.ws.ctr[3] = atomicExch(&a.ws.ctr[0], 0u);
-            a.ws.ctr[4] = atomicExch(&a.ws.ctr[1], 0u);
-            atomicExch(&a.ws.ctr[2], 0u);
-        }
-    }
-}
+// ------------------------------------------------------------------------------------
+// K4 (fused): the backward of one (table, row-range slot) per 512-thread workgroup.
+//   STE (quant_utils.py:349-363) + EmbeddingBag sparse backward, then one of
+//     MODE 0  torch.optim.SGD on the uncoalesced grad        (dlrm_s_pytorch_single_gpu.py:1736-1750)
+//     MODE 1  grad.coalesce() + per-slot max|grad|           (s_q_g_p_c.py:859-861)
+//     MODE 2  W.add_(-lr * grad), product rounded            (s_q_g_p_c.py:615-616, ranking range)
+//  1. gather: the slot's valid lookups in lookup order (a stable count / scan / write over
+//     the table's lookups; keys become (row << 32 | gather position), bags kept aside);
+//  2. prefetch: every gathered lookup's dy row (this workgroup's dimensions, STE applied)
+//     is loaded into registers BEFORE the sort, so the HBM round trip overlaps it;
+//  3. sort by row: a sparse wide slot takes one MSD 8-bit pass + per-bucket insertion sort,
+//     everything else a stable 8-bit LSD radix (narrow spans: one pass); the keys are
+//     unique, so both give the reference's order (rows ascending, duplicates in lookup order);
+//  4. every distinct row (segment) by one float4 lane group, its lookups combined strictly
+//     in lookup order from LDS, FB_SB segments per group in flight; outputs written once,
+//     the slot's max|grad| reduced in LDS and stored (no atomics).
+// Tables with fewer than 8 row blocks (coalesce) or <= 256 rows (SGD: finalize rebuilds
+// their maxima) are split by DIMENSION instead: all 8 workgroups see all the table's
+// lookups and each owns D/8 dims (>= 4), so the long ordered chains of tiny hot tables run
+// on 8 CUs. A slot whose rows do not fit in LDS streams its sorted lookups through a stage
+// (segments carried across chunks by the same lane group); one with more than 4096 keys
+// sorts in the caller's workspace. There is no per-batch limit.
+// Wide-table SGD keeps the |W| hierarchy with the flat protocol (atomicMax growth, dirty
+// flags for shrunk holders, tracked finalize).
+// ------------------------------------------------------------------------------------
+constexpr int FB_TPB = 512;
+constexpr int FB_LDS = 156 * 1024;   // dynamic LDS of a workgroup (+ ~1.5 KiB static: 160 KiB)
+constexpr int FB_STAGE = 8192;       // floats of the streaming stage
+constexpr int FB_PFR = 12;           // prefetched float4 per thread held across the sort
+constexpr int FB_SB = 4;             // segments in flight per lane group
+static_assert(FB_TPB == SORT_TPB, "the sort helpers assume the workgroup size");
 
-// K4b --------------------------------------------------------------------------------
-struct SegArgs {
+template <int LPR>
+struct FGeom {
+    static constexpr int D = LPR * 4;
+    static constexpr int DSPLIT = LPR < SPLIT ? LPR : SPLIT;  // dim slices (>= 4 dims each)
+};
+
+struct FArgs {
     float* W;
     uint8_t* packed;
     float* rowmax;
@@ -2837,46 +2372,68 @@ struct SegArgs {
     const float* pscale;
     const int64_t* meta;
     uint32_t* err;
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    int64_t B;
+    int pool1;
     const float* dy;
     int64_t dst_t, dst_b;
     int T;
     int ste;
-    float nlr;                   // -lr
-    int repack;                  // MODE 0/2: repack touched INT4 rows with pscale
-    int32_t* ws_rows;            // MODE 1 outputs
+    float nlr;
+    int repack;
+    const int32_t* tmask;
+    const int64_t* ws_cap_base;  // MODE 1 outputs
+    int32_t* ws_rows;
     float* ws_vals;
+    int32_t* ws_ucount;
     float* ws_absmax;
-    SortWs ws;
+    uint64_t* gkey;              // [T*S][Lc] spill of slots with > SORT_LDS_KEYS keys
+    uint64_t* gtmp;
+    uint32_t* gbag;
     int64_t Lc;
 };
 
-// per-table constants staged in LDS by every K4b workgroup
-struct TabLds {
-    int64_t rb[MAX_TABLES];
-    uint32_t bb[MAX_TABLES];     // blocks / superblocks / rows < 2^32 (checked on the host)
-    uint32_t sbb[MAX_TABLES];
-    uint32_t nrows[MAX_TABLES];
-    float s[MAX_TABLES];
-    float rp[MAX_TABLES];
-};
-
-DQRM_INLINE void stage_tables(const SegArgs& a, TabLds* tl, int mode) {
-    const Meta m = make_meta(a.meta, a.T);
-    for (int t = threadIdx.x; t < a.T; t += SEG_TPB) {
-        tl->rb[t] = m.row_base[t];
-        tl->nrows[t] = (uint32_t)m.num_rows[t];
-        tl->bb[t] = (uint32_t)m.blk_base[t];
-        tl->sbb[t] = (uint32_t)m.sblk_base[t];
-        tl->s[t] = a.scale[t];
-        tl->rp[t] = (mode != 1 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+// workspace: the spill regions, only when a slot can exceed the in-LDS key capacity
+__host__ __device__ inline int64_t fused_ws_layout(unsigned char* base, int T, int64_t Lc, FArgs* fa) {
+    if (Lc <= SORT_LDS_KEYS) {
+        if (fa) { fa->gkey = nullptr; fa->gtmp = nullptr; fa->gbag = nullptr; }
+        return 16;
     }
+    const int64_t n = (int64_t)T * SPLIT * Lc;
+    const int64_t o1 = align16(n * 8), o2 = o1 + align16(n * 8), o3 = o2 + align16(n * 4);
+    if (fa) {
+        fa->gkey = reinterpret_cast<uint64_t*>(base);
+        fa->gtmp = reinterpret_cast<uint64_t*>(base + o1);
+        fa->gbag = reinterpret_cast<uint32_t*>(base + o2);
+    }
+    return o3;
 }
 
-// |W| hierarchy upkeep of one updated row of a wide table (the flat protocol, see
-// flat_row_update): growth by atomicMax on the non-negative float bits, a shrunk block-max
-// holder flags its block and superblock for the tracked finalize.
-DQRM_INLINE void row_upkeep(const SegArgs& a, int t, int64_t grow, uint32_t x, int64_t bb, int64_t sbb, float old_rm,
-                            float rm, float old_blk) {
+// row-range slot of a row (slot_rows' inverse): the largest s with floor(nblk*s/SPLIT) <= blk
+DQRM_INLINE int slot_of_row(uint32_t row, int64_t nblk) {
+    const uint32_t blk = row >> 8, nb = (uint32_t)nblk;  // 32-bit: nblk < 2^24
+    return (int)((SPLIT * (blk + 1) + nb - 1) / nb) - 1;
+}
+
+template <int OP>
+DQRM_INLINE float4 seg_op4(float4 acc, float4 v, float nlr) {
+    if (OP == OP_FMA) {
+        acc.x = fmaf(v.x, nlr, acc.x); acc.y = fmaf(v.y, nlr, acc.y);
+        acc.z = fmaf(v.z, nlr, acc.z); acc.w = fmaf(v.w, nlr, acc.w);
+    } else if (OP == OP_AXPY) {
+        acc.x = acc.x + v.x * nlr; acc.y = acc.y + v.y * nlr;
+        acc.z = acc.z + v.z * nlr; acc.w = acc.w + v.w * nlr;
+    } else {
+        acc.x = acc.x + v.x; acc.y = acc.y + v.y; acc.z = acc.z + v.z; acc.w = acc.w + v.w;
+    }
+    return acc;
+}
+
+// |W| hierarchy upkeep of one updated row of a wide table (see flat_row_update)
+DQRM_INLINE void fused_row_upkeep(const FArgs& a, int t, int64_t grow, uint32_t x, int64_t bb, int64_t sbb,
+                                  float old_rm, float rm, float old_blk) {
     a.rowmax[grow] = rm;
     const int64_t blk = x >> 8;
     const int64_t sb = sbb + (blk >> 8);
@@ -2893,280 +2450,223 @@ DQRM_INLINE void row_upkeep(const SegArgs& a, int t, int64_t grow, uint32_t x, i
     }
 }
 
-template <int OP>
-DQRM_INLINE float seg_op(float acc, float v, float nlr) {
-    if (OP == OP_FMA) return fmaf(v, nlr, acc);
-    if (OP == OP_AXPY) return acc + v * nlr;
-    return acc + v;
-}
-
-// MODE 1: max|grad| into the slot's ws_absmax (order-free atomicMax on the non-negative
-// float bits)
-DQRM_INLINE void absmax_to_slot(const SegArgs& a, int k, float am) {
-    atomicMax(reinterpret_cast<unsigned int*>(a.ws_absmax) + k, __float_as_uint(am));
-}
-
-// the same for the wave's (slot, value) pairs of the lanes with `valid`: one atomic per
-// distinct slot per wave (a slot's records are one contiguous run of the list, so a wave's
-// records come from one or two slots). Wave-uniform call.
-DQRM_INLINE void wave_slot_max(const SegArgs& a, int k, float am, bool valid) {
-    uint64_t pend = __ballot(valid);
-    while (pend) {
-        const int l = __ffsll((long long)pend) - 1;
-        const int k0 = __shfl(k, l, WAVE);
-        const bool mine = valid && k == k0;
-        const uint64_t mm = __ballot(mine);
-        const float v = wave_max(mine ? am : 0.0f);
-        if ((int)(threadIdx.x % WAVE) == l) absmax_to_slot(a, k0, v);
-        pend &= ~mm;
-    }
-}
-
-// one short-record chunk; the list length, the table constants and the records are
-// loaded in one round trip (records past the list are read from the workspace's capacity
-// and masked), then every record's W row and dy rows in a second
-template <int LPR, int MODE>
-DQRM_INLINE void short_records(const SegArgs& a, TabLds* tl, int r_begin, unsigned int (*s_am)[SEG_SB * 2]) {
-    constexpr int D = LPR * 4;
-    using G = SegGeom<LPR>;
-    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
-    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
-    const int nrec = (int)a.ws.ctr[3];
-    uint4 rec[SEG_SB], bg[SEG_SB];
-    bool act[SEG_SB];
-    const int64_t rlim = (int64_t)a.T * a.Lc;  // the list's capacity
-#pragma unroll
-    for (int b = 0; b < SEG_SB; ++b) {
-        const int r = r_begin + grp + b * G::NG;
-        rec[b] = r < rlim ? a.ws.rec[r] : make_uint4(0u, 0u, 0u, 0u);
-        bg[b] = r < rlim ? a.ws.rbag[r] : make_uint4(0u, 0u, 0u, 0u);
-    }
-    stage_tables(a, tl, MODE);
-    if (r_begin >= nrec) return;  // uniform
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < SEG_SB; ++b) {
-        const int r = r_begin + grp + b * G::NG;
-        act[b] = r < nrec && (rec[b].z >> 11) - 1u < (uint32_t)LONG_SEG;  // 1..LONG_SEG (0: empty)
-    }
-    DIAG_W(3);
-    float4 wold[SEG_SB], v[SEG_SB][4];
-    float oblk[SEG_SB], am[SEG_SB];
-#pragma unroll
-    for (int b = 0; b < SEG_SB; ++b) {  // every segment's W row and lookups (<= 4) in flight
-        if (!act[b]) continue;
-        const int t = (int)(rec[b].z & 2047u) / SPLIT;
-        const int len = (int)(rec[b].z >> 11);
-        const float* dyt = a.dy + (int64_t)t * a.dst_t;
-        const int64_t grow = tl->rb[t] + rec[b].x;
-        if (MODE != 1) {
-            wold[b] = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
-            oblk[b] = tl->nrows[t] > BLK ? a.blkmax[tl->bb[t] + (rec[b].x >> 8)] : 0.0f;
-        }
-        v[b][0] = reinterpret_cast<const float4*>(dyt + (int64_t)rec[b].y * a.dst_b)[sub];
-        if (len > 1) v[b][1] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].x * a.dst_b)[sub];
-        if (len > 2) v[b][2] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].y * a.dst_b)[sub];
-        if (len > 3) v[b][3] = reinterpret_cast<const float4*>(dyt + (int64_t)bg[b].z * a.dst_b)[sub];
-    }
-    DIAG_W(4);
-#pragma unroll
-    for (int b = 0; b < SEG_SB; ++b) {
-        am[b] = 0.0f;
-        if (!act[b]) continue;
-        const int k = (int)(rec[b].z & 2047u), t = k / SPLIT;
-        const int len = (int)(rec[b].z >> 11);
-        const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, tl->s[t], a.ste, 0};
-        bool first = true;
-        float4 acc = MODE != 1 ? wold[b] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            if (c < len) acc = combine<OP>(acc, src.finish(v[b][c]), first, a.nlr);
-        if (len > 4) {  // 5..LONG_SEG (rare): the slot's sorted keys from the record's first key on
-            const uint64_t* sk = a.ws.skey + (int64_t)k * a.Lc + bg[b].w;
-            float4 q[4];
-            for (int j = 4; j < len; j += 4) {
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (j + c < len) q[c] = src.fetch(key_lo(sk[j + c]), sub);
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (j + c < len) acc = combine<OP>(acc, src.finish(q[c]), first, a.nlr);
-            }
-        }
-        const uint32_t x = rec[b].x;
-        const int64_t grow = tl->rb[t] + x;
-        if (MODE == 1) {
-            const uint32_t e = rec[b].w;
-            am[b] = group_max<LPR>(abs_max4(acc));
-            if (e != 0xFFFFFFFFu) {
-                reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * D)[sub] = acc;
-                if (sub == 0) a.ws_rows[e] = (int32_t)x;
-            }
-        } else {
-            reinterpret_cast<float4*>(a.W + grow * D)[sub] = acc;
-            if (a.repack) pack4_row(acc, a.packed + grow * (D / 2), sub, tl->rp[t]);
-            if (tl->nrows[t] > BLK) {
-                const float old_rm = group_max<LPR>(abs_max4(wold[b]));
-                const float rm = group_max<LPR>(abs_max4(acc));
-                if (sub == 0) row_upkeep(a, t, grow, x, tl->bb[t], tl->sbb[t], old_rm, rm, oblk[b]);
-            }
-        }
-    }
-    DIAG_W(5);
-    if (MODE == 1) {  // slot maxima: per wave then per workgroup, one atomic per distinct slot
-        const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
-        int nk = 0;
-#pragma unroll
-        for (int b = 0; b < SEG_SB; ++b) {  // the wave's distinct (slot, max) pairs -> s_am[w]
-            const bool valid = act[b] && sub == 0;
-            const int kk = (int)(rec[b].z & 2047u);
-            uint64_t pend = __ballot(valid);
-            while (pend) {
-                const int l = __ffsll((long long)pend) - 1;
-                const int k0 = __shfl(kk, l, WAVE);
-                const bool mine = valid && kk == k0;
-                const float v = wave_max(mine ? am[b] : 0.0f);
-                pend &= ~__ballot(mine);
-                int q = 0;  // merge into the wave's list (at most 2*SEG_SB distinct slots)
-                while (q < nk && (int)s_am[w][q] != k0) ++q;
-                if (lane == 0) {
-                    if (q < nk) {
-                        s_am[w][SEG_SB + q] = max(s_am[w][SEG_SB + q], __float_as_uint(v));
-                    } else if (nk < SEG_SB) {
-                        s_am[w][nk] = (unsigned)k0;
-                        s_am[w][SEG_SB + nk] = __float_as_uint(v);
-                    } else {
-                        absmax_to_slot(a, k0, v);  // list full (never for ordered runs)
-                    }
-                }
-                if (q >= nk && nk < SEG_SB) ++nk;
-            }
-        }
-        __shared__ int s_nk[SEG_TPB / WAVE];
-        if (lane == 0) s_nk[w] = nk;
-        __syncthreads();
-        if (threadIdx.x == 0) {  // merge the waves' lists, one atomic per distinct slot
-            unsigned int ks[SEG_TPB / WAVE * SEG_SB], vs[SEG_TPB / WAVE * SEG_SB];
-            int m = 0;
-            for (int ww = 0; ww < SEG_TPB / WAVE; ++ww)
-                for (int q = 0; q < s_nk[ww]; ++q) {
-                    const unsigned int k0 = s_am[ww][q], v = s_am[ww][SEG_SB + q];
-                    int p = 0;
-                    while (p < m && ks[p] != k0) ++p;
-                    if (p < m) vs[p] = max(vs[p], v); else { ks[m] = k0; vs[m] = v; ++m; }
-                }
-            for (int p = 0; p < m; ++p) atomicMax(reinterpret_cast<unsigned int*>(a.ws_absmax) + ks[p], vs[p]);
-        }
-    }
-}
-
-// largest k in [0, nk) with p[k] <= e (p ascending, p[0] <= e)
-DQRM_INLINE int seg_search(const int* p, int nk, int e) {
-    int lo = 0, hi = nk - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (p[mid] <= e) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-struct LongLds {
-    int lp[LMAXK + 1];  // long-stream position of each owned segment (relative), + end
-    int st[LMAXK];      // first key
-    uint32_t row[LMAXK];
-    uint32_t e[LMAXK];  // MODE 1: ws entry
+// One workgroup's segment outputs. LG lanes (float4 each) per segment, at float4 offset
+// q0 = dim0/4 of the row.
+struct FOut {
+    int t;
+    int64_t rb, bb, sbb;
+    bool wide_upkeep;         // SGD on a row-split wide table: rowmax + flat protocol
+    float r_pack;
+    const int* ufirst;        // MODE 1: first segment of each row-range slot (LDS)
+    const int64_t* cb;        // MODE 1: coalesced workspace slot bases (LDS, SPLIT + 1)
+    int64_t nblk;
+    int q0;
+    // SGD on a row-split slot of <= FB_AGG blocks: per-block growth / shrink aggregated in
+    // LDS (a slot owns its blocks), one update per block instead of one atomic per row
+    unsigned int* bgrow;
+    unsigned int* bshr;
+    int64_t b0s;
 };
+constexpr int FB_AGG = 64;
 
-// A long item: the long segments of slot k whose long-stream start falls in one
-// LONG_RANGE chunk, dimension slice z. Their lookups (this slice of each dy row) stream
-// through the LDS stage CE at a time, dim-major; dim-lane group g combines segments
-// j = g (mod NGL) strictly in lookup order, carrying its running row in registers into the
-// next chunk (only the chunk's last segment can continue, and the same group owns it there).
-template <int LPR, int MODE, bool FULL>
-DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float* stage, LongLds* ll) {
+template <int LPR, int MODE, int LG>
+DQRM_INLINE void fused_write(const FArgs& a, const FOut& o, int u, uint32_t x, float4 acc, float4 wold, float oblk,
+                             int lane, float& amax) {
     constexpr int D = LPR * 4;
-    using G = SegGeom<LPR>;
-    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
-    constexpr int SW = FULL ? D : D / G::DS;  // floats of each row this item owns
-    constexpr int GL = SW < WAVE ? SW : WAVE;
-    constexpr int NDL = SW / GL;
-    constexpr int NGL = SEG_TPB / GL;
-    constexpr int F4 = SW / 4;
-    constexpr int CE = LSTAGE / SW;           // lookups per stage chunk
-    constexpr int SP = CE + 4;                // stage pitch of one dim
-    constexpr int FM = LSTAGE / 4 / SEG_TPB;  // float4 fetched per thread per chunk
-    const int k = (int)(item.x & 0xFFFFu), z = (int)(item.x >> 16), t = k / SPLIT;
-    const int dim0 = FULL ? 0 : z * SW;
-    const int kf = (int)item.y, nk = (int)item.z - kf;
-    const int64_t Lc = a.Lc;
-    const uint4* __restrict__ lrec = a.ws.lrec + (int64_t)k * Lc;
-    __syncthreads();  // the previous item is done with the LDS
-    const int E0 = (int)lrec[kf].w;
-    for (int i = threadIdx.x; i <= nk; i += SEG_TPB) {
-        if (i < nk) {
-            const uint4 r = lrec[kf + i];
-            ll->lp[i] = (int)r.w - E0;
-            ll->row[i] = r.x;
-            ll->st[i] = (int)r.y;
-            ll->e[i] = r.z;
-        } else {
-            ll->lp[i] = (int)item.w - E0;
+    const int64_t grow = o.rb + x;
+    if (MODE == 1) {
+        const int s = slot_of_row(x, o.nblk);
+        const int64_t e = o.cb[s] + (u - o.ufirst[s]);
+        if (e < o.cb[s + 1]) {
+            reinterpret_cast<float4*>(a.ws_vals + e * D)[o.q0 + lane] = acc;
+            if (o.q0 == 0 && lane == 0) a.ws_rows[e] = (int32_t)x;
+        }
+        amax = fmaxf(amax, abs_max4(acc));
+    } else {
+        reinterpret_cast<float4*>(a.W + grow * D)[o.q0 + lane] = acc;
+        if (a.repack) pack4_row(acc, a.packed + grow * (D / 2), o.q0 + lane, o.r_pack);
+        if (o.wide_upkeep) {
+            const float old_rm = group_max<LG>(abs_max4(wold));
+            const float rm = group_max<LG>(abs_max4(acc));
+            if (lane == 0) {
+                if (o.bgrow) {
+                    a.rowmax[grow] = rm;
+                    const int jb = (int)((x >> 8) - o.b0s);
+                    atomicMax(&o.bgrow[jb], __float_as_uint(rm));
+                    if (old_rm == oblk && rm < old_rm) o.bshr[jb] = 1u;
+                } else {
+                    fused_row_upkeep(a, o.t, grow, x, o.bb, o.sbb, old_rm, rm, oblk);
+                }
+            }
         }
     }
-    __syncthreads();
-    const int64_t rb = tl->rb[t], bb = tl->bb[t], sbb = tl->sbb[t];
-    const uint64_t* __restrict__ skey = a.ws.skey + (int64_t)k * Lc;
-    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, tl->s[t], a.ste, dim0 / 4};
-    const float r_pack = tl->rp[t];
-    const int E = ll->lp[nk];
+}
+
+// Prefetched path: every gathered lookup's row slice sits in LDS at dyl[g * LG + lane].
+// the ordered chain of sorted lookups [e, e1) of one segment from the prefetched rows:
+// gather positions 4 per 16-B read, two batches of 8 rows in flight (double buffer)
+template <int LG, int OP>
+DQRM_INLINE float4 walk_prefetched(float4 acc, const float4* dyl, const uint32_t* gsp, int e, int e1, int lane,
+                                   float nlr) {
+    for (; e < e1 && (e & 3); ++e) acc = seg_op4<OP>(acc, dyl[gsp[e] * LG + lane], nlr);
+    if (e + 8 <= e1) {
+        const uint4* g4 = reinterpret_cast<const uint4*>(gsp);
+        float4 va[8], vb[8];
+        auto load8 = [&](float4 (&v)[8], int ee) {
+            const uint4 p = g4[ee / 4], q = g4[ee / 4 + 1];
+            v[0] = dyl[p.x * LG + lane]; v[1] = dyl[p.y * LG + lane]; v[2] = dyl[p.z * LG + lane];
+            v[3] = dyl[p.w * LG + lane]; v[4] = dyl[q.x * LG + lane]; v[5] = dyl[q.y * LG + lane];
+            v[6] = dyl[q.z * LG + lane]; v[7] = dyl[q.w * LG + lane];
+        };
+        auto add8 = [&](const float4 (&v)[8]) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) acc = seg_op4<OP>(acc, v[c], nlr);
+        };
+        load8(va, e);
+        while (true) {
+            const bool m1 = e + 16 <= e1;
+            if (m1) load8(vb, e + 8);
+            add8(va);
+            e += 8;
+            if (!m1) break;
+            const bool m2 = e + 16 <= e1;
+            if (m2) load8(va, e + 8);
+            add8(vb);
+            e += 8;
+            if (!m2) break;
+        }
+    }
+    for (; e < e1; ++e) acc = seg_op4<OP>(acc, dyl[gsp[e] * LG + lane], nlr);
+    return acc;
+}
+
+template <int LPR, int MODE, int LG>
+DQRM_INLINE void fused_segments_lds(const FArgs& a, const FOut& o, const uint64_t* keys, const uint32_t* gsp,
+                                    const uint32_t* hpos, int U, int n, const float4* dyl, float& amax) {
+    constexpr int D = LPR * 4;
+    constexpr int NG = FB_TPB / LG;
+    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
+    const int lane = threadIdx.x % LG, grp = threadIdx.x / LG;
+    for (int u0 = grp; u0 < U; u0 += NG * FB_SB) {
+        int h[FB_SB], e1[FB_SB];
+        uint32_t x[FB_SB];
+        float4 wold[FB_SB];
+        float oblk[FB_SB];
+#pragma unroll
+        for (int b = 0; b < FB_SB; ++b) {  // the W rows of all SB segments in flight
+            const int u = u0 + b * NG;
+            h[b] = 0; e1[b] = 0; x[b] = 0;
+            if (u < U) {
+                h[b] = (int)hpos[u];
+                e1[b] = u + 1 < U ? (int)hpos[u + 1] : n;
+                x[b] = key_row(keys[h[b]]);
+                if (MODE != 1) {
+                    const int64_t grow = o.rb + x[b];
+                    wold[b] = reinterpret_cast<const float4*>(a.W + grow * D)[o.q0 + lane];
+                    oblk[b] = o.wide_upkeep ? a.blkmax[o.bb + (x[b] >> 8)] : 0.0f;
+                }
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < FB_SB; ++b) {
+            const int u = u0 + b * NG;
+            if (u >= U) continue;
+            float4 acc;
+            int e = h[b];
+            if (MODE == 1) {
+                acc = dyl[gsp[e] * LG + lane];
+                ++e;
+            } else {
+                acc = wold[b];
+            }
+            acc = walk_prefetched<LG, OP>(acc, dyl, gsp, e, e1[b], lane, a.nlr);  // strictly in lookup order
+            fused_write<LPR, MODE, LG>(a, o, u, x[b], acc, wold[b], oblk[b], lane, amax);
+        }
+    }
+}
+
+// Staged path (long chains, or rows that do not fit in LDS): after the sort, the sorted
+// lookups' row slices stream through a DIM-MAJOR stage (stage[dim * SP + entry], CE entries
+// per chunk), so a lane owning one dimension reads 4 consecutive lookups per 16-B LDS read
+// and the ordered chain runs at add latency. Dim-lane group g (GL lanes, NDL dims each)
+// combines segments u = g (mod NGL), carrying its running row in registers into the next
+// chunk (only a chunk's last segment continues, and the same group owns it there).
+template <int LPR, int MODE, int LG>
+DQRM_INLINE void fused_segments_staged(const FArgs& a, const FOut& o, const uint64_t* keys, const uint32_t* bags,
+                                       const uint32_t* hpos, int U, int n, float* stage, int stage_floats,
+                                       const DySource& src, float& amax) {
+    constexpr int D = LPR * 4;
+    constexpr int SW = LG * 4;
+    constexpr int GL = SW < 16 ? SW : (SW / 4 > 16 ? SW / 4 : 16);  // <= 4 dims per lane, >= 8 groups
+    constexpr int NDL = SW / GL;
+    constexpr int NGL = FB_TPB / GL;
+    constexpr int OP = MODE == 0 ? OP_FMA : (MODE == 2 ? OP_AXPY : OP_SUM);
+    constexpr int FQ = 16;  // (lookup, float4) items per thread in flight
+    // SGD: W rows of a group's next WB segments loaded in one round trip (<= 32 KiB of LDS)
+    constexpr int WB0 = 8192 / (NGL * (SW + 1));
+    constexpr int WB = WB0 < 1 ? 1 : (WB0 > 8 ? 8 : WB0);
+    // SGD: per-group LDS area for the batch of W row slices and their old block maxima
+    float* wbuf = stage + (MODE != 1 ? stage_floats - NGL * WB * (SW + 1) : 0);
+    if (MODE != 1) stage_floats -= NGL * WB * (SW + 1);
+    int CE = (stage_floats / SW - 4) & ~3;
+    CE = CE < n ? CE : ((n + 3) & ~3);
+    const int SP = CE + 4;
     const int lig = threadIdx.x % GL, g = threadIdx.x / GL;
-    float acc[NDL];
+    const int dim0 = o.q0 * 4;
+    float* wb = wbuf + g * WB * (SW + 1);
+    auto seg_of = [&](int e) {  // segment holding sorted position e
+        int lo = 0, hi = U - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if ((int)hpos[mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    };
+    float acc[NDL], wo[NDL];
     float orm = 0.0f, oblk = 0.0f;
 #pragma unroll
-    for (int d = 0; d < NDL; ++d) acc[d] = 0.0f;
-    for (int c0 = 0; c0 < E; c0 += CE) {
-        const int ce = min(CE, E - c0);
-        {  // fetch the chunk: thread-contiguous (lookup, float4) items, one segment search per
-           // thread then a forward walk; keys first, then this slice of every dy row
-            const int q0 = threadIdx.x * FM;
-            uint32_t bag[FM];
-            if (q0 / F4 < ce) {
-                int j = seg_search(ll->lp, nk, c0 + q0 / F4);
-                uint32_t bb0 = 0;
+    for (int d = 0; d < NDL; ++d) { acc[d] = 0.0f; wo[d] = 0.0f; }
+    for (int c0 = 0; c0 < n; c0 += CE) {
+        const int ce = min(CE, n - c0);
+        for (int q0 = threadIdx.x; q0 < ce * LG; q0 += FB_TPB * FQ) {  // fetch, FQ items in flight
+            float4 v[FQ];
 #pragma unroll
-                for (int f = 0; f < FM; ++f) {
-                    const int q = q0 + f, el = q / F4;
-                    if (el < ce && (f == 0 || q % F4 == 0)) {
-                        const int e = c0 + el;
-                        while (e >= ll->lp[j + 1]) ++j;
-                        bb0 = key_lo(skey[ll->st[j] + (e - ll->lp[j])]);
-                    }
-                    bag[f] = bb0;
-                }
-            }
-            float4 v[FM];
-#pragma unroll
-            for (int f = 0; f < FM; ++f) {
-                const int q = q0 + f;
-                if (q / F4 < ce) v[f] = src.fetch(bag[f], q % F4);
+            for (int f = 0; f < FQ; ++f) {
+                const int q = q0 + f * FB_TPB;
+                if (q < ce * LG) v[f] = src.fetch(bags[key_lo(keys[c0 + q / LG])], q % LG);
             }
 #pragma unroll
-            for (int f = 0; f < FM; ++f) {
-                const int q = q0 + f, el = q / F4;
-                if (el < ce) {
+            for (int f = 0; f < FQ; ++f) {
+                const int q = q0 + f * FB_TPB;
+                if (q < ce * LG) {
                     const float4 x = src.finish(v[f]);
-                    float* col = stage + (4 * (q % F4)) * SP + el;
+                    float* col = stage + (4 * (q % LG)) * SP + q / LG;
                     col[0] = x.x; col[SP] = x.y; col[2 * SP] = x.z; col[3 * SP] = x.w;
                 }
             }
         }
         __syncthreads();
-        const int jfc = seg_search(ll->lp, nk, c0), jlc = seg_search(ll->lp, nk, c0 + ce - 1);
-        for (int j = jfc + ((g - jfc % NGL) + NGL) % NGL; j <= jlc; j += NGL) {
-            const int sb = ll->lp[j], se = ll->lp[j + 1];
+        const int uf = seg_of(c0), ul = seg_of(c0 + ce - 1);
+        const int ug = uf + ((g - uf % NGL) + NGL) % NGL;  // this group's first segment here
+        for (int u = ug; u <= ul; u += NGL) {
+            const int jb = ((u - ug) / NGL) % WB;  // slot in the group's W batch
+            if (MODE != 1 && jb == 0) {  // the next WB segments' W slices (those that begin here)
+#pragma unroll
+                for (int j = 0; j < WB; ++j) {
+                    const int uu = u + j * NGL;
+                    if (uu <= ul && (int)hpos[uu] >= c0) {
+                        const uint32_t xx = key_row(keys[hpos[uu]]);
+                        const int64_t gr = o.rb + xx;
+#pragma unroll
+                        for (int d = 0; d < NDL; ++d) wb[j * (SW + 1) + lig + GL * d] = a.W[gr * D + dim0 + lig + GL * d];
+                        if (lig == 0) wb[j * (SW + 1) + SW] = o.wide_upkeep ? a.blkmax[o.bb + (xx >> 8)] : 0.0f;
+                    }
+                }
+            }
+            const int sb = (int)hpos[u], se = u + 1 < U ? (int)hpos[u + 1] : n;
+            const uint32_t x = key_row(keys[sb]);
+            const int64_t grow = o.rb + x;
             const bool begin = sb >= c0;
-            const uint32_t x = ll->row[j];
-            const int64_t grow = rb + x;
             int e = (begin ? sb : c0) - c0;
             const int e1 = (se < c0 + ce ? se : c0 + ce) - c0;
             const float* col[NDL];
@@ -3179,22 +2679,20 @@ DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float
                     ++e;
                 } else {
 #pragma unroll
-                    for (int d = 0; d < NDL; ++d) acc[d] = a.W[grow * D + dim0 + lig + GL * d];
-                    if (FULL) {
+                    for (int d = 0; d < NDL; ++d) { acc[d] = wb[jb * (SW + 1) + lig + GL * d]; wo[d] = acc[d]; }
+                    if (o.wide_upkeep) {
                         float mx = 0.0f;
 #pragma unroll
-                        for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
+                        for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(wo[d]));
                         orm = group_max<GL>(mx);
-                        oblk = a.blkmax[bb + (x >> 8)];
+                        oblk = wb[jb * (SW + 1) + SW];
                     }
                 }
             }
-            // strictly ordered chain: peel to a 16-B boundary, then 16-B LDS reads, the next
-            // VB float4 per dim in flight while the current ones are combined (ping-pong)
-            for (; e < e1 && (e & 3); ++e)
+            for (; e < e1 && (e & 3); ++e)  // to a 16-B boundary
 #pragma unroll
                 for (int d = 0; d < NDL; ++d) acc[d] = seg_op<OP>(acc[d], col[d][e], a.nlr);
-            constexpr int VB = NDL >= 4 ? 1 : 4 / NDL;
+            constexpr int VB = NDL >= 4 ? 1 : 4 / NDL;  // float4 per dim per batch
             constexpr int BE = 4 * VB;
             float4 xa[VB][NDL], xb[VB][NDL];
             auto loadb = [&](float4 (&xx)[VB][NDL], int jj) {
@@ -3211,7 +2709,7 @@ DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float
                         acc[d] = seg_op<OP>(seg_op<OP>(seg_op<OP>(seg_op<OP>(acc[d], xx[vv][d].x, a.nlr), xx[vv][d].y,
                                                                   a.nlr), xx[vv][d].z, a.nlr), xx[vv][d].w, a.nlr);
             };
-            if (e + BE <= e1) {
+            if (e + BE <= e1) {  // ping-pong: the next batch in flight while this one is added
                 loadb(xa, e);
                 while (true) {
                     const bool m1 = e + 2 * BE <= e1;
@@ -3226,47 +2724,47 @@ DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float
                     if (!m2) break;
                 }
             }
-            for (; e + 4 <= e1; e += 4)
-#pragma unroll
-                for (int d = 0; d < NDL; ++d) {
-                    const float4 xx = *reinterpret_cast<const float4*>(col[d] + e);
-                    acc[d] = seg_op<OP>(seg_op<OP>(seg_op<OP>(seg_op<OP>(acc[d], xx.x, a.nlr), xx.y, a.nlr), xx.z, a.nlr),
-                                        xx.w, a.nlr);
-                }
             for (; e < e1; ++e)
 #pragma unroll
                 for (int d = 0; d < NDL; ++d) acc[d] = seg_op<OP>(acc[d], col[d][e], a.nlr);
             if (se > c0 + ce) continue;  // continues in the next chunk (same group, acc carried)
             if (MODE == 1) {
-                const uint32_t ew = ll->e[j];
-                float mx = 0.0f;
+                const int sl = slot_of_row(x, o.nblk);
+                const int64_t ew = o.cb[sl] + (u - o.ufirst[sl]);
+                if (ew < o.cb[sl + 1]) {
 #pragma unroll
-                for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
-                mx = group_max<GL>(mx);
-                if (ew != 0xFFFFFFFFu) {
-#pragma unroll
-                    for (int d = 0; d < NDL; ++d) a.ws_vals[(int64_t)ew * D + dim0 + lig + GL * d] = acc[d];
+                    for (int d = 0; d < NDL; ++d) a.ws_vals[ew * D + dim0 + lig + GL * d] = acc[d];
                     if (dim0 == 0 && lig == 0) a.ws_rows[ew] = (int32_t)x;
                 }
-                if (lig == 0) absmax_to_slot(a, k, mx);
+#pragma unroll
+                for (int d = 0; d < NDL; ++d) amax = fmaxf(amax, fabsf(acc[d]));
             } else {
 #pragma unroll
                 for (int d = 0; d < NDL; ++d) a.W[grow * D + dim0 + lig + GL * d] = acc[d];
                 if (a.repack) {  // even lanes pack their nibble with the odd neighbour's
 #pragma unroll
                     for (int d = 0; d < NDL; ++d) {
-                        const int q = (int)fake_quant(acc[d], r_pack, -8.0f, 7.0f) + 8;
-                        const int qn = __shfl_xor(q, 1, WAVE);
+                        const int qv = (int)fake_quant(acc[d], o.r_pack, -8.0f, 7.0f) + 8;
+                        const int qn = __shfl_xor(qv, 1, WAVE);
                         const int dim = dim0 + lig + GL * d;
-                        if ((dim & 1) == 0) a.packed[grow * (D / 2) + dim / 2] = (uint8_t)(q | (qn << 4));
+                        if ((dim & 1) == 0) a.packed[grow * (D / 2) + dim / 2] = (uint8_t)(qv | (qn << 4));
                     }
                 }
-                if (FULL) {
+                if (o.wide_upkeep) {
                     float mx = 0.0f;
 #pragma unroll
                     for (int d = 0; d < NDL; ++d) mx = fmaxf(mx, fabsf(acc[d]));
                     const float rm = group_max<GL>(mx);
-                    if (lig == 0) row_upkeep(a, t, grow, x, bb, sbb, orm, rm, oblk);
+                    if (lig == 0) {
+                        if (o.bgrow) {
+                            a.rowmax[grow] = rm;
+                            const int jb = (int)((x >> 8) - o.b0s);
+                            atomicMax(&o.bgrow[jb], __float_as_uint(rm));
+                            if (orm == oblk && rm < orm) o.bshr[jb] = 1u;
+                        } else {
+                            fused_row_upkeep(a, o.t, grow, x, o.bb, o.sbb, orm, rm, oblk);
+                        }
+                    }
                 }
             }
         }
@@ -3274,35 +2772,243 @@ DQRM_INLINE void long_item(const SegArgs& a, const TabLds* tl, uint4 item, float
     }
 }
 
-template <int LPR, int MODE>
-__global__ void __launch_bounds__(SEG_TPB) k_bwd_segments(SegArgs a) {
-    using G = SegGeom<LPR>;
-    __shared__ __attribute__((aligned(16))) float s_stage[LSTAGE + 4 * 256];
-    __shared__ unsigned int s_am[SEG_TPB / WAVE][SEG_SB * 2];   // MODE 1: per wave (slot, max) pairs
-    __shared__ LongLds s_ll;
-    __shared__ TabLds s_tl;
-    // grid.x: LONG_WGS workgroups looping over the long items first (the long chains are
-    // the critical path, so they are dispatched first), then one per US-record chunk
-    const bool is_long = (int)blockIdx.x < LONG_WGS;
-    if (is_long) {
-        const int nli = (int)a.ws.ctr[4];
-        if ((int)blockIdx.x >= nli) return;
-        stage_tables(a, &s_tl, MODE);
-        for (int w = blockIdx.x; w < nli; w += LONG_WGS) {
-            const uint4 item = a.ws.litem[w];
-            const int t = (int)(item.x & 0xFFFFu) / SPLIT;
-            __syncthreads();  // s_tl staged
-            if (MODE != 1 && s_tl.nrows[t] > BLK)
-                long_item<LPR, MODE, true>(a, &s_tl, item, s_stage, &s_ll);
-            else
-                long_item<LPR, MODE, false>(a, &s_tl, item, s_stage, &s_ll);
-        }
+template <int LPR, int MODE, int LG>
+DQRM_INLINE void fused_slot(const FArgs& a, unsigned char* lds, int k, int t, int s, bool dsplit, int z, int64_t r0,
+                            int64_t r1, int* s_scan, int* s_wl, int* s_ufirst, int64_t* s_cb, float& amax,
+                            const int64_t (&pre)[8], int per) {
+    constexpr int D = LPR * 4;
+    constexpr int SW = LG * 4;  // dims this workgroup owns
+    const Meta m = make_meta(a.meta, a.T);
+    const int64_t nrows = m.num_rows[t];
+    const int64_t ib = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
+    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ib;
+    if (L > a.Lc) {  // more lookups than the caller planned for: skipped, flagged
+        if (threadIdx.x == 0 && (dsplit ? s == 0 : s == SPLIT - 1)) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        if (MODE == 1 && threadIdx.x < SPLIT && (!dsplit || z == 0)) s_ufirst[threadIdx.x] = 0;
         return;
     }
+    // 1. gather (keys into LDS at offset 0 when they fit)
+    uint64_t* lkeys = reinterpret_cast<uint64_t*>(lds);
+    bool in_lds;
+    uint64_t* gk = a.gkey ? a.gkey + (int64_t)k * a.Lc : nullptr;
+    const bool report = dsplit ? s == 0 : s == SPLIT - 1;
+    const int n = per > 0 ? gather_slot_keys_pre(lkeys, gk, &in_lds, s_scan, pre, per, a.B, nrows, r0, r1, report, a.err)
+                          : gather_slot_keys(lkeys, gk, &in_lds, s_scan, a.off + (int64_t)t * a.B, a.idx + ib, a.B,
+                                             L, nrows, r0, r1, report, a.err, a.pool1 != 0);
+    if (n == 0) return;
+    uint64_t* keys = in_lds ? lkeys : a.gkey + (int64_t)k * a.Lc;
+    // LDS carve for n keys: keys | tmp (radix ping-pong / bitonic exchange / heads) | bags | data
+    const int64_t o_tmp = align16((int64_t)n * 8);
+    const int64_t o_bag = o_tmp + align16((int64_t)(n > FB_TPB ? n : FB_TPB) * 8);
+    const int64_t o_dat = o_bag + align16((int64_t)n * 4);
+    uint64_t* tmp = in_lds ? reinterpret_cast<uint64_t*>(lds + o_tmp) : a.gtmp + (int64_t)k * a.Lc;
+    uint32_t* bags = in_lds ? reinterpret_cast<uint32_t*>(lds + o_bag) : a.gbag + (int64_t)k * a.Lc;
+    unsigned char* data = in_lds ? lds + o_dat : lds;
+    // prefetch (gather order) when the slot's rows fit and its segments are short on average
+    // (a wide slot, or a dim-split table with enough rows); long chains take the staged path
+    const int64_t span_rows = r1 - r0;
+    const bool pf = in_lds && o_dat + (int64_t)n * SW * 4 <= FB_LDS && (int64_t)n <= 4 * span_rows;
+    DIAG_T(1);
+    // 2. prefetch this workgroup's slice of every gathered lookup's dy row into registers:
+    //    the loads stay in flight across the sort (barriers wait for LDS traffic only)
+    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, dsplit ? z * LG : 0};
+    float4 pfv[FB_PFR];
+    if (pf) {
+#pragma unroll
+        for (int f = 0; f < FB_PFR; ++f) {
+            const int q = threadIdx.x + FB_TPB * f;
+            if (q < n * LG) pfv[f] = src.fetch(key_lo(lkeys[q / LG]), q % LG);
+        }
+    }
+    __syncthreads();  // every key read: now rewrite them
+    for (int g = threadIdx.x; g < n; g += FB_TPB) {  // keys -> (row, gather position), bags aside
+        const uint64_t x = keys[g];
+        bags[g] = key_lo(x);
+        keys[g] = (x & 0xFFFFFFFF00000000ull) | (uint64_t)g;
+    }
+    __syncthreads();
+    DIAG_T(6);
+    // 3. sort by row
+    const uint32_t span = (uint32_t)(r1 - r0);
+    const int nbits = span <= 1 ? 0 : 32 - __builtin_clz(span - 1);
+    if (nbits > 12 && n <= FB_TPB)  // a sparse wide slot (~1 key per bucket): one MSD pass + fix-up
+        msd_sort_rows(keys, tmp, n, (uint32_t)r0, nbits, reinterpret_cast<int*>(data), s_scan, s_wl + FB_TPB / WAVE);
+    else
+        radix_sort_rows(keys, tmp, n, (uint32_t)r0, nbits, reinterpret_cast<int*>(data), s_scan);
+    DIAG_T(2);
+    // the prefetched rows land in LDS (the sort's histogram region is free again); rows past
+    // the register budget are loaded now
+    float4* dyl = reinterpret_cast<float4*>(data);
+    if (pf) {
+#pragma unroll
+        for (int f = 0; f < FB_PFR; ++f) {
+            const int q = threadIdx.x + FB_TPB * f;
+            if (q < n * LG) dyl[q] = src.finish(pfv[f]);
+        }
+        for (int q = threadIdx.x + FB_TPB * FB_PFR; q < n * LG; q += FB_TPB)
+            dyl[q] = src.load(bags[q / LG], q % LG);
+    }
+    // 4. heads (first sorted key of every distinct row) -> hpos (tmp is free)
+    uint32_t* hpos = reinterpret_cast<uint32_t*>(tmp);
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const uint64_t lt = lanemask_lt();
+    int U;
+    {
+        const int kpl = (n + FB_TPB - 1) / FB_TPB;
+        const int i0 = w * WAVE * kpl + lane;
+        auto is_head = [&](int i) { return i < n && (i == 0 || key_row(keys[i]) != key_row(keys[i - 1])); };
+        int hc = 0;
+        for (int q = 0; q < kpl; ++q) hc += (int)__popcll(__ballot(is_head(i0 + q * WAVE)));
+        if (lane == 0) s_wl[w] = hc;
+        __syncthreads();
+        int run = 0;
+        U = 0;
+        for (int q = 0; q < FB_TPB / WAVE; ++q) { const int c = s_wl[q]; run += q < w ? c : 0; U += c; }
+        for (int q = 0; q < kpl; ++q) {
+            const int i = i0 + q * WAVE;
+            const bool hh = is_head(i);
+            const uint64_t hm = __ballot(hh);
+            if (hh) hpos[run + __popcll(hm & lt)] = (uint32_t)i;
+            run += (int)__popcll(hm);
+        }
+        __syncthreads();
+    }
+    DIAG_T(3);
+    // prefetched path: the sorted gather positions as a compact u32 array (the bags are no
+    // longer needed), read 4 at a time by the walk
+    uint32_t* gsp = bags;
+    if (pf) {
+        for (int e = threadIdx.x; e < n; e += FB_TPB) gsp[e] = key_lo(keys[e]);
+        __syncthreads();
+    }
+    // MODE 1: first segment of every row-range slot (dim-split tables span several slots)
+    const int64_t nblk = ceil_div(nrows, BLK);
+    if (MODE == 1) {
+        if (threadIdx.x < SPLIT) s_wl[threadIdx.x] = 0;
+        __syncthreads();
+        if (dsplit) {
+            for (int u = threadIdx.x; u < U; u += FB_TPB) atomicAdd(&s_wl[slot_of_row(key_row(keys[hpos[u]]), nblk)], 1);
+            __syncthreads();
+            if (threadIdx.x < SPLIT) {
+                int run = 0;
+                for (int q = 0; q < (int)threadIdx.x; ++q) run += s_wl[q];
+                s_ufirst[threadIdx.x] = run;
+            }
+        } else if (threadIdx.x < SPLIT) {
+            s_ufirst[threadIdx.x] = 0;
+            s_wl[threadIdx.x] = (int)threadIdx.x == s ? U : 0;
+        }
+        __syncthreads();
+    }
+    FOut o;
+    o.t = t;
+    o.rb = m.row_base[t];
+    o.bb = m.blk_base[t];
+    o.sbb = m.sblk_base[t];
+    o.wide_upkeep = MODE != 1 && !dsplit;  // SGD row split implies > 256 rows
+    o.r_pack = (MODE != 1 && a.repack) ? 1.0f / a.pscale[t] : 0.0f;
+    o.ufirst = s_ufirst;
+    o.cb = s_cb;
+    o.nblk = nblk;
+    o.q0 = dsplit ? z * LG : 0;
+    // per-block aggregation of the SGD hierarchy upkeep (LDS after the stage / rows)
+    __shared__ unsigned int s_bgrow[FB_AGG], s_bshr[FB_AGG];
+    const int64_t b0s = r0 >> 8, nbs = ((r1 + BLK - 1) >> 8) - b0s;
+    const bool agg = o.wide_upkeep && nbs <= FB_AGG;
+    o.bgrow = agg ? s_bgrow : nullptr;
+    o.bshr = agg ? s_bshr : nullptr;
+    o.b0s = b0s;
+    if (agg) {
+        if (threadIdx.x < FB_AGG) { s_bgrow[threadIdx.x] = 0u; s_bshr[threadIdx.x] = 0u; }
+        __syncthreads();
+    }
+    if (pf)
+        fused_segments_lds<LPR, MODE, LG>(a, o, keys, gsp, hpos, U, n, dyl, amax);
+    else
+        fused_segments_staged<LPR, MODE, LG>(a, o, keys, bags, hpos, U, n, reinterpret_cast<float*>(data),
+                                             (int)((FB_LDS - (data - lds)) / 4), src, amax);
+    if (agg) {  // one update per block: growth by max (the slot owns the block), shrunk holders flagged
+        __syncthreads();
+        if (threadIdx.x < nbs) {
+            const int64_t blk = b0s + threadIdx.x;
+            const float cand = __uint_as_float(s_bgrow[threadIdx.x]);
+            const float old_blk = a.blkmax[o.bb + blk];
+            const int64_t sb = o.sbb + (blk >> 8);
+            if (cand > old_blk) {
+                a.blkmax[o.bb + blk] = cand;
+                if (cand > a.sblkmax[sb]) {
+                    atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(cand));
+                    if (cand > a.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(cand));
+                }
+            }
+            if (s_bshr[threadIdx.x]) {
+                a.bdirty[o.bb + blk] = 1;
+                a.sdirty[sb] = 1;
+            }
+        }
+    }
+    DIAG_W(4);
+    (void)D;
+}
+
+template <int LPR, int MODE>
+__global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
+    using FG = FGeom<LPR>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int s_scan[FB_TPB / WAVE + 1];
+    __shared__ int s_wl[2 * (FB_TPB / WAVE) + 1];
+    __shared__ int s_ufirst[SPLIT];
+    __shared__ int64_t s_cb[SPLIT + 1];
+    __shared__ float s_red[FB_TPB / WAVE];
+    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
     DIAG_T(0);
-    const int r_begin = ((int)blockIdx.x - LONG_WGS) * G::US;
-    short_records<LPR, MODE>(a, &s_tl, r_begin, s_am);
-    DIAG_W(6);
+    // Criteo form with <= 8 bags per thread: the thread's indices are loaded right away, in
+    // parallel with the table metadata (no dependent round trip before the gather)
+    int64_t pre[8];
+    const int per = (a.pool1 && a.B <= (int64_t)FB_TPB * 8) ? (int)((a.B + FB_TPB - 1) / FB_TPB) : 0;
+    if (per > 0) {
+        const int64_t* ti = a.idx + (int64_t)t * a.B + (int64_t)threadIdx.x * per;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pre[j] = (j < per && (int64_t)threadIdx.x * per + j < a.B) ? ti[j] : -1;
+    }
+    const Meta m = make_meta(a.meta, a.T);
+    const int64_t nrows = m.num_rows[t];
+    const int64_t nblk = ceil_div(nrows, BLK);
+    const bool dsplit = MODE == 1 ? nblk < SPLIT : nrows <= BLK;
+    const bool masked = MODE == 2 && a.tmask != nullptr && a.tmask[t] == 0;
+    int64_t r0 = 0, r1 = nrows;
+    if (!dsplit) slot_rows(nrows, s, r0, r1);
+    const bool active = !masked && (dsplit ? s < FG::DSPLIT : r0 < r1);
+    if (MODE == 1) {
+        if (threadIdx.x <= SPLIT) s_cb[threadIdx.x] = a.ws_cap_base[t * SPLIT + threadIdx.x];
+        if (threadIdx.x < SPLIT) { s_ufirst[threadIdx.x] = 0; s_wl[threadIdx.x] = 0; }
+    }
+    __syncthreads();
+    float amax = 0.0f;
+    if (active) {  // uniform
+        if (dsplit)
+            fused_slot<LPR, MODE, LPR / FG::DSPLIT>(a, lds, k, t, s, true, s, r0, r1, s_scan, s_wl, s_ufirst, s_cb,
+                                                    amax, pre, per);
+        else
+            fused_slot<LPR, MODE, LPR>(a, lds, k, t, s, false, 0, r0, r1, s_scan, s_wl, s_ufirst, s_cb, amax, pre, per);
+    }
+    if (MODE == 1) {  // the slot's max|grad| (dim-split: this slice's), and the slot counts
+        amax = wave_max(amax);
+        if (threadIdx.x % WAVE == 0) s_red[threadIdx.x / WAVE] = amax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float r = 0.0f;
+            for (int q = 0; q < FB_TPB / WAVE; ++q) r = fmaxf(r, s_red[q]);
+            a.ws_absmax[k] = r;
+        }
+        if (threadIdx.x < SPLIT && (dsplit ? s == 0 : (int)threadIdx.x == s)) {
+            const int64_t cap = s_cb[threadIdx.x + 1] - s_cb[threadIdx.x];
+            int c = s_wl[threadIdx.x];
+            if (c > cap) { flag_error(a.err, DQRM_ERRF_OVERFLOW); c = (int)cap; }
+            a.ws_ucount[t * SPLIT + threadIdx.x] = c;
+        }
+    }
+    DIAG_W(5);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3551,36 +3257,28 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     const dqrm_table_set* set = c.set;
     const int T = set->num_tables, D = set->dim;
     const int64_t Lc = bwd_lookup_cap(c.batch);
-    if (Lc > 0x3fffffffll || (int64_t)T * Lc > 0xffffffffll)
+    if (Lc > 0x3fffffffll)
         return set_error(DQRM_E_CAPACITY, "%s: max_lookups %lld too large", who, (long long)Lc);
     if (set->total_rows > 0xffffffffll)
         return set_error(DQRM_E_CAPACITY, "%s: more than 2^32 rows", who);
-    const int64_t need = sort_ws_layout(nullptr, T, Lc, nullptr);
+    FArgs fa{};
+    const int64_t need = fused_ws_layout(nullptr, T, Lc, nullptr);
     if (!c.ws || (int64_t)c.ws_bytes < need || (((uintptr_t)c.ws) & 15))
         return set_error(DQRM_E_WORKSPACE, "%s: workspace needs %lld bytes, 16-B aligned (got %zu)", who,
                          (long long)need, c.ws_bytes);
-    SortWs ws;
-    sort_ws_layout(reinterpret_cast<unsigned char*>(c.ws), T, Lc, &ws);
-    SortArgs sa{};
-    sa.idx = c.batch->idx; sa.off = c.batch->off; sa.idx_base = c.batch->idx_base; sa.B = c.batch->num_bags;
-    sa.pool1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-    sa.meta = set->meta; sa.T = T; sa.err = set->err; sa.ws = ws; sa.Lc = Lc; sa.tmask = c.tmask;
-    sa.ws_cap_base = c.ws_cap_base; sa.ws_ucount = c.ws_ucount; sa.ws_absmax = c.ws_absmax;
-    SegArgs ga{};
-    ga.W = set->W; ga.packed = set->packed; ga.rowmax = set->rowmax; ga.blkmax = set->blkmax;
-    ga.sblkmax = set->sblkmax; ga.tmax = set->tmax; ga.sdirty = set->sdirty; ga.bdirty = set->bdirty;
-    ga.scale = set->scale; ga.pscale = set->pscale; ga.meta = set->meta; ga.err = set->err;
-    ga.dy = c.dy; ga.dst_t = c.dst_t; ga.dst_b = c.dst_b; ga.T = T; ga.ste = c.ste; ga.nlr = -c.lr;
-    ga.repack = c.repack; ga.ws_rows = c.ws_rows; ga.ws_vals = c.ws_vals; ga.ws_absmax = c.ws_absmax;
-    ga.ws = ws; ga.Lc = Lc;
-    int rc = allow_lds(k_sort_slots<MODE>, SORT_LDS);
-    if (rc) return rc;
+    fused_ws_layout(reinterpret_cast<unsigned char*>(c.ws), T, Lc, &fa);
+    fa.W = set->W; fa.packed = set->packed; fa.rowmax = set->rowmax; fa.blkmax = set->blkmax;
+    fa.sblkmax = set->sblkmax; fa.tmax = set->tmax; fa.sdirty = set->sdirty; fa.bdirty = set->bdirty;
+    fa.scale = set->scale; fa.pscale = set->pscale; fa.meta = set->meta; fa.err = set->err;
+    fa.idx = c.batch->idx; fa.off = c.batch->off; fa.idx_base = c.batch->idx_base; fa.B = c.batch->num_bags;
+    fa.pool1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    fa.dy = c.dy; fa.dst_t = c.dst_t; fa.dst_b = c.dst_b; fa.T = T; fa.ste = c.ste; fa.nlr = -c.lr;
+    fa.repack = c.repack; fa.tmask = c.tmask; fa.ws_cap_base = c.ws_cap_base; fa.ws_rows = c.ws_rows;
+    fa.ws_vals = c.ws_vals; fa.ws_ucount = c.ws_ucount; fa.ws_absmax = c.ws_absmax; fa.Lc = Lc;
+    int rc = 0;
     DISPATCH_LPR(D, {
-        using G = SegGeom<LPR>;
-        sa.ds = G::DS;
-        hipLaunchKernelGGL(k_sort_slots<MODE>, dim3(T * SPLIT), dim3(SORT_TPB), SORT_LDS, st, sa);
-        const int64_t nxs = ((int64_t)T * Lc + G::US - 1) / G::US;  // record chunks (records <= lookups)
-        hipLaunchKernelGGL((k_bwd_segments<LPR, MODE>), dim3((unsigned)(LONG_WGS + nxs)), dim3(SEG_TPB), 0, st, ga);
+        if ((rc = allow_lds(k_bwd_fused<LPR, MODE>, FB_LDS))) return rc;
+        hipLaunchKernelGGL((k_bwd_fused<LPR, MODE>), dim3(T * SPLIT), dim3(FB_TPB), FB_LDS, st, fa);
     });
     LAUNCH_CHECK();
     if (MODE != 1) return launch_finalize(set, st, true);
@@ -3737,7 +3435,7 @@ static int check_batch(const dqrm_batch* batch, const char* who) {
 
 size_t dqrm_bwd_workspace_bytes(int num_tables, int64_t max_lookups) {
     if (num_tables <= 0 || num_tables > MAX_TABLES || max_lookups < 0) return 0;
-    return (size_t)sort_ws_layout(nullptr, num_tables, max_lookups > 0 ? max_lookups : 1, nullptr);
+    return (size_t)fused_ws_layout(nullptr, num_tables, max_lookups > 0 ? max_lookups : 1, nullptr);
 }
 
 int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
