@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark: DQRM data-parallel QAT embedding step on MI355X (1..8 GPUs, one process each).
+"""Benchmark: DQRM's QAT embedding step on MI355X (1..8 GPUs, one process each).
 
-A step = one pass of the hot path over one synthetic batch per rank:
-  forward   26-table fake-quant EmbeddingBag (exact per-step table scale, FP32-row gather)
-  backward  STE + sparse backward + coalesce + local INT8 grad scale        (K4)
-  comm      RCCL all-gather of the [T] scales, quantize-pack to INT8       (K5)
-            RCCL all-gather of the fixed-capacity {rows, int8} payloads
-  update    decode all ranks' payloads, integer union-sum, dequant, SGD    (K6)
-At N=1 there is nothing to exchange: K5 + K6 run as one fused kernel (dqrm_apply_local:
-the same quantize, dequantize and SGD arithmetic, bit-identical W; --unfused-local runs the
-payload round trip instead).
-The MLP/interaction layers are outside the north-star path (SURVEY.md §8) and are not run;
-the upstream gradient dL/dy is a fixed synthetic tensor.
+--mode dp  (default; BASELINE configs 4-5) one data-parallel QAT step per rank:
+  forward   26-table fake-quant EmbeddingBag (exact per-step table scale, FP32-row gather;
+            with --scale-period P --use-packed: INT4 rows between the periodic scale refreshes)
+  backward  STE + sparse backward + coalesce + local INT8 grad scale        (k_bwd_fused)
+  comm      RCCL all-gather of the per-slot max|grad|, quantize-pack to INT8, RCCL
+            all-gather of the fixed-capacity {rows, int8} payloads
+  update    decode all ranks' payloads, integer union-sum, dequant, SGD (+ INT4 repack)
+  At N=1 there is nothing to exchange: quantize-pack + apply run fused (dqrm_apply_local,
+  the same arithmetic, bit-identical W; --unfused-local times the payload round trip).
+--mode fwd (BASELINE config 2) the forward alone.
+--mode sgd (BASELINE config 3) forward + fused STE/sparse-backward/SGD (dqrm_emb_bwd_sgd).
+--graph captures one step per resident batch in a HIP graph (torch.cuda.CUDAGraph) and
+replays it, taking the host launch path out of the timed region (the B=128 configs are
+launch-bound).
+
+The MLP/interaction layers are outside the north-star path (SURVEY.md 8) and are not run;
+the upstream gradient dL/dy is a fixed synthetic tensor. The MLP's INT8 gradient exchange
+(8(f) #1) is timed in its own phase, outside the step.
 
 Prints ONE JSON line (rank 0). N=1 by default; N>1 is launched by torch.distributed.run.
+A run whose kernels raised device error flags prints value null and exits with status 3.
 """
 from __future__ import annotations
 
@@ -29,43 +37,39 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 
 import deep_quantized_recommendation_model_dqrm_amd as dq  # noqa: E402
 from deep_quantized_recommendation_model_dqrm_amd import _lib as L  # noqa: E402
-import gen_inputs as G  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd.workloads import (  # noqa: E402
+    CONFIGS as _CONFIGS, MLPS, synthetic_indices)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-
-CONFIGS = {
-    # BASELINE.json configs[4]: Criteo-Terabyte shape, D=64, ~773M rows: the reference TB
-    # profile (--max-ind-range=10M) with its six >=1M-row tables scaled x16
-    "terabyte": dict(rows=[n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS], dim=64),
-    # the reference's actual TB run (49.1M rows)
-    "terabyte_ref": dict(rows=G.TERABYTE_ROWS, dim=64),
-    # BASELINE.json configs[2-3]: Criteo-Kaggle, D=16
-    "kaggle": dict(rows=G.KAGGLE_ROWS, dim=16),
-}
-# the reference scripts' MLPs (bash_scripts/): Kaggle --arch-mlp-bot=13-512-256-64-16
-# --arch-mlp-top=512-256-1; Terabyte 13-512-256-64 / 512-512-256-1; the top MLP's input is
-# D + T(T+1)/2 (dot interaction of T+1 vectors, dlrm_s_pytorch_single_gpu.py create_mlp)
-MLPS = {
-    "terabyte": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
-    "terabyte_ref": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
-    "kaggle": ([13, 512, 256, 64, 16], [16 + 351, 512, 256, 1]),
-}
+CONFIGS = {k: dict(rows=r, dim=d) for k, (r, d) in _CONFIGS.items()}
+# host tables of the PyTorch-CPU baseline: the reference's own TB run stands in for the
+# 773 M-row profile (its 198 GB of FP32 rows exceed one bench run's host-memory budget)
+CPU_TABLES = {"terabyte": "terabyte_ref", "terabyte_ref": "terabyte_ref", "kaggle": "kaggle"}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="terabyte", choices=sorted(CONFIGS))
+    p.add_argument("--mode", default="dp", choices=["dp", "fwd", "sgd"],
+                   help="dp: data-parallel QAT step; fwd: forward only; sgd: forward + fused sparse SGD")
     p.add_argument("--batch-per-gpu", type=int, default=2048,
-                   help="samples per rank per step (reference TB mini-batch 2048)")
+                   help="samples per rank per step (weak scaling; reference TB mini-batch 2048)")
+    p.add_argument("--global-batch", type=int, default=0,
+                   help="strong scaling: samples per step over all ranks, each rank taking its "
+                        "get_my_slice share (SURVEY 8(d) C5: 2048 over 8 GPUs)")
     p.add_argument("--grad-bits", type=int, default=8)
     p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--scale-period", type=int, default=0,
+                   help="refresh the table scales every P steps (q_m_n_q_g.py:303-315); 0 = every step")
+    p.add_argument("--use-packed", action="store_true",
+                   help="with --scale-period: gather INT4 rows between refreshes, repack touched rows")
+    p.add_argument("--graph", action="store_true", help="replay each step from a captured HIP graph (N=1)")
     p.add_argument("--index-dist", default="uniform", choices=["uniform", "zipf"])
     p.add_argument("--num-batches", type=int, default=8, help="distinct resident batches cycled")
     p.add_argument("--gather-batch", type=int, default=65536,
@@ -74,6 +78,7 @@ def parse():
     p.add_argument("--mlp-iters", type=int, default=50,
                    help="iterations of the MLP INT8 gradient exchange phase (0 = skip)")
     p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="time budget of the CPU baseline sample")
     p.add_argument("--seed", type=int, default=123)
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl (= RCCL on ROCm) for measurements; gloo only to rehearse N>1 on one GPU")
@@ -83,14 +88,16 @@ def parse():
                    help="bracket the dominant kernel with HIP events on every k-th timed step")
     p.add_argument("--traffic-profile", default=None,
                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; "
-                        "default profiles/r1_<config>_summary.json when present")
-    return p.parse_args()
+                        "default profiles/r2_<config>_summary.json when present")
+    return p.parse_args(argv)
 
 
 PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "kaggle": "kaggle"}
 KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
     "emb_fwd": "k_emb_fwd<{lpr},",
-    "bwd_coalesce": "k_table_bwd<{lpr}, 1>",
+    "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
+    "bwd_coalesce": "k_bwd_fused<{lpr}, 1>",
+    "bwd_sgd": "k_bwd_fused<{lpr}, 0>",
     "grad_quant_pack": "k_quant_pack<{lpr}>",
     "apply_sparse_update": "k_apply_flat<{lpr}>",
     "apply_local": "k_apply_local<{lpr}>",
@@ -100,7 +107,7 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
 def pmc_traffic(path, phase, D):
     """HBM bytes per launch of the phase's kernel from a committed rocprofv3 PMC summary
     (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
-    if not path or not os.path.exists(path):
+    if not path or not os.path.exists(path) or phase not in KERNEL_SYMBOL:
         return None
     prefix = KERNEL_SYMBOL[phase].format(lpr=D // 4)
     for name, v in json.load(open(path))["kernels"].items():
@@ -110,29 +117,47 @@ def pmc_traffic(path, phase, D):
     return None
 
 
+def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
+    """Algorithmic bytes per launch: what the algorithm must move, no more.
+    L = T*B lookups, U = distinct (table, row) pairs. Criteo-form batches
+    (DQRM_BATCH_POOLING_ONE) never read the offsets."""
+    L = T * B
+    offs = 0 if pool1 else T * B * 8
+    pk = U * (D // 2) if repack else 0
+    return {
+        # index + FP32 row per lookup, FP32 output row per bag, the [T] scales
+        "emb_fwd": L * (D * 4 + 8) + offs + L * D * 4 + T * 4,
+        "emb_fwd_packed": L * (D // 2 + 8) + offs + L * D * 4 + T * 4,
+        # index + dy row per lookup; one coalesced {row, D x f32} record per distinct row
+        "bwd_coalesce": L * 8 + offs + L * D * 4 + U * (D * 4 + 4),
+        # index + dy row per lookup; W row read+write and |W| row max per distinct row
+        "bwd_sgd": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
+        "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
+        "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4 + pk,
+        "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4 + pk,
+    }[phase]
+
+
 def make_batches(rows, B_global, rank, world, count, seed, dist_kind, device):
     """Global Criteo-form batches [T, B_global] generated identically on every rank, each
     rank keeping its contiguous slice (get_my_slice, dlrm_s_pytorch_single_gpu.py:989-993)."""
-    g = torch.Generator(device=device)
-    out = []
     sl = dq.get_my_slice(B_global, world, rank)
-    for k in range(count):
-        g.manual_seed(seed * 1000 + k)
-        cols = []
-        for n in rows:
-            if dist_kind == "uniform":
-                cols.append(torch.randint(0, n, (B_global,), generator=g, device=device, dtype=torch.int64))
-            else:  # Zipf(1.05)-like power law via inverse transform on a log scale
-                u = torch.rand(B_global, generator=g, device=device, dtype=torch.float64)
-                z = torch.floor(torch.exp(u * np.log(float(n)))) - 1
-                cols.append(z.clamp_(0, n - 1).to(torch.int64))
-        P = torch.stack(cols)[:, sl].contiguous()
-        out.append(dq.LookupBatch.pooling_one(P))
-    return out
+    return [dq.LookupBatch.pooling_one(
+        synthetic_indices(rows, B_global, seed * 1000 + k, dist_kind, device)[:, sl].contiguous())
+        for k in range(count)]
 
 
 def timed_events(n):
     return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+
+
+def phase_names(mode, use_packed, fused):
+    fwd = "emb_fwd_packed" if use_packed else "emb_fwd"
+    if mode == "fwd":
+        return [fwd]
+    if mode == "sgd":
+        return [fwd, "bwd_sgd"]
+    return [fwd, "bwd_coalesce"] + (["apply_local"] if fused else ["grad_quant_pack", "apply_sparse_update"])
 
 
 def main():
@@ -140,10 +165,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            print("N>1 must be launched with torch.distributed.run", file=sys.stderr)
-            sys.exit(2)
+    if world == 1 and a.gpus > 1:
+        print("N>1 must be launched with torch.distributed.run", file=sys.stderr)
+        sys.exit(2)
+    if a.use_packed and a.scale_period <= 0:
+        print("--use-packed needs --scale-period P > 0", file=sys.stderr)
+        sys.exit(2)
+    if a.graph and world > 1:
+        print("--graph runs at N=1 only (the collectives stay eager)", file=sys.stderr)
+        sys.exit(2)
+    strong = a.global_batch > 0
+    if strong and a.global_batch % world:  # the reference skips such batches (parallel_comm.py:1855-1856)
+        print(f"--global-batch {a.global_batch} is not divisible by {world} ranks", file=sys.stderr)
+        sys.exit(2)
     ndev = torch.cuda.device_count()
     local = local % max(ndev, 1)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
@@ -154,42 +188,61 @@ def main():
         else:  # gloo: functional rehearsal of the N>1 path (e.g. several ranks on one GPU)
             dist.init_process_group("gloo")
     cfg = CONFIGS[a.config]
-    rows, D, B = cfg["rows"], cfg["dim"], a.batch_per_gpu
+    rows, D = cfg["rows"], cfg["dim"]
     T = len(rows)
+    B_global = a.global_batch if strong else a.batch_per_gpu * world
+    B = B_global // world
 
     t0 = time.time()
-    ts = dq.EmbeddingTableSet(rows, D, device=dev, packed=a.gather_batch > 0, init="uniform", seed=a.seed)
-    batches = make_batches(rows, B * world, rank, world, a.num_batches, a.seed, a.index_dist, dev)
+    ts = dq.EmbeddingTableSet(rows, D, device=dev, packed=a.gather_batch > 0 or a.use_packed, init="uniform",
+                              seed=a.seed)
+    batches = make_batches(rows, B_global, rank, world, a.num_batches, a.seed, a.index_dist, dev)
     dy = torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + rank)) * 0.05
     y = torch.empty(T, B, D, device=dev)
-    ex = dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits)
-    kern = ex.kernels
+    ex = dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits) if a.mode == "dp" else None
+    if a.use_packed:
+        ts.refresh_scale_and_pack(4)
     torch.cuda.synchronize()
     setup_s = time.time() - t0
 
     # N=1: quantize-pack + apply fused (dqrm_apply_local; same quantize/dequantize/SGD
     # arithmetic, bit-identical W, no payload since nothing is exchanged)
     fused = world == 1 and not a.unfused_local
-    names = (["emb_fwd", "bwd_coalesce", "apply_local"] if fused
-             else ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"])
+    repack = a.use_packed
+    names = phase_names(a.mode, a.use_packed, fused)
 
-    def step(i, ev=None, only=None):
-        """One QAT step. ev: per-phase (start, end) events; only: bracket just that phase."""
+    def step(i, ev=None, only=None, refresh=None):
+        """One step of the selected mode. ev: per-phase (start, end) events; only: bracket
+        just that phase; refresh: refresh the table scales (default: by --scale-period)."""
         b = batches[i % len(batches)]
+        if refresh is None:
+            refresh = a.scale_period <= 0 or i % a.scale_period == 0
 
         def mark(j, k):
             if ev is not None and (only is None or only == j):
                 ev[j][k].record()
 
         mark(0, 0)
-        ts.forward(b, bits=4, refresh_scale=True, out=y)
+        if a.use_packed:
+            if refresh:  # periodic refresh: new scales, tables whose scale moved are repacked
+                ts.refresh_scale_and_pack(4)
+            ts.forward(b, bits=4, refresh_scale=False, use_packed=True, out=y)
+        else:
+            ts.forward(b, bits=4, refresh_scale=refresh, out=y)
         mark(0, 1)
+        if a.mode == "fwd":
+            return
         mark(1, 0)
+        if a.mode == "sgd":
+            ts.backward_sgd(b, dy, a.lr, repack=repack)
+            mark(1, 1)
+            return
+        kern = ex.kernels
         kern.coalesce(b, dy, ex.ws, True, "tbd")
         mark(1, 1)
         if fused:
             mark(2, 0)
-            kern.apply_local(ex.ws, a.grad_bits, ex.s_avg, a.lr, False)
+            kern.apply_local(ex.ws, a.grad_bits, ex.s_avg, a.lr, repack)
             mark(2, 1)
             return
         if ex.world == 1:
@@ -207,30 +260,64 @@ def main():
             gathered = ex.gathered
         mark(3, 0)
         kern.apply(ex.cap_base, ex.cap_total, gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg, a.lr,
-                   L.DQRM_UPD_DP, False)
+                   L.DQRM_UPD_DP, repack)
         mark(3, 1)
 
     for i in range(a.warmup):
         step(i)
-    # per-phase breakdown (untimed): every kernel bracketed by events; picks the dominant one
+    torch.cuda.synchronize()
+    # per-phase breakdown (untimed, eager): every phase bracketed by events; picks the dominant.
+    # Periodic mode: steady-state steps only; the refresh (every P steps) is timed apart.
     nb = max(10, min(50, a.steps))
     bev = [timed_events(len(names)) for _ in range(nb)]
     for i in range(nb):
-        step(i, bev[i])
+        step(i, bev[i], refresh=a.scale_period <= 0)
     torch.cuda.synchronize()
-    kms = {n: float(np.mean([bev[i][j][0].elapsed_time(bev[i][j][1]) for i in range(nb)])) for j, n in enumerate(names)}
+    refresh_ms = None
+    if a.use_packed:  # new scales from the |W| hierarchy + INT4 repack of every table whose scale moved
+        rev = timed_events(3)
+        for e0, e1 in rev:
+            ts.pscale.fill_(float("nan"))
+            e0.record()
+            ts.refresh_scale_and_pack(4)
+            e1.record()
+        torch.cuda.synchronize()
+        refresh_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in rev]))
+    kms = {n: float(np.mean([bev[i][j][0].elapsed_time(bev[i][j][1]) for i in range(nb)]))
+           for j, n in enumerate(names)}
     dom = max(kms, key=kms.get)
     dj = names.index(dom)
+
+    graphs = None
+    if a.graph:  # one captured step per resident batch; periodic refresh steps stay eager
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        graphs = []
+        with torch.cuda.stream(s):
+            for k in range(len(batches)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    step(k, refresh=a.scale_period <= 0)
+                graphs.append(g)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+    def run(i, ev=None):
+        if graphs is None or (a.scale_period > 1 and i % a.scale_period == 0):
+            step(i, ev, only=dj)
+        else:
+            graphs[i % len(graphs)].replay()
+
     # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
     # it runs on) on every sample_every-th step, so the events barely perturb the timing
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [timed_events(len(names)) for _ in range(a.steps)]
-    sampled = [i for i in range(a.steps) if i % a.sample_every == 0]
+    sampled = [] if graphs is not None else [i for i in range(a.steps) if i % a.sample_every == 0]
     t_start = time.perf_counter()
     for i in range(a.steps):
-        step(a.warmup + i, evs[i] if i % a.sample_every == 0 else None, only=dj)
+        run(a.warmup + i, evs[i] if i in sampled else None)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -239,49 +326,26 @@ def main():
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    dom_ms = float(np.mean([evs[i][dj][0].elapsed_time(evs[i][dj][1]) for i in sampled]))
+    dom_ms = (float(np.mean([evs[i][dj][0].elapsed_time(evs[i][dj][1]) for i in sampled])) if sampled
+              else kms[dom])  # graph replay: the eager breakdown's average
 
-    # algorithmic bytes per launch; unique counts from the last step
-    U = int(ex.ws.ucount.sum().item())
-    L_tot = T * B
-    alg = {
-        "emb_fwd": L_tot * (D * 4 + 8) + T * B * 8 + T * B * D * 4 + T * 4,
-        "bwd_coalesce": L_tot * 8 + T * B * 8 + L_tot * D * 4 + U * (D * 4 + 4),
-        "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
-        "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4,
-        "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4,
-    }
-    achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
+    # algorithmic bytes per launch; distinct rows of the last step's batch
+    if ex is not None:
+        U = int(ex.ws.ucount.sum().item())
+    else:
+        P = batches[(a.warmup + a.steps - 1) % len(batches)].idx.view(T, -1)
+        U = int(sum(torch.unique(P[t]).numel() for t in range(T)))
+    alg = alg_bytes(dom, T, B, D, U, world, pool1=True, repack=repack)
+    achieved = alg / (dom_ms * 1e-3) / 1e9
     err = ts.read_errors()
 
-    # INT4 packed-gather bandwidth phase (north-star gather metric), outside the timed step
-    gather = None
-    if a.gather_batch > 0:
-        ts.refresh_scale_and_pack(4)
-        Bg = a.gather_batch
-        gb = make_batches(rows, Bg, 0, 1, 2, a.seed + 7, a.index_dist, dev)
-        yg = torch.empty(T, Bg, D, device=dev)
-        for i in range(5):
-            ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
-        gev = timed_events(a.gather_iters)
-        for i in range(a.gather_iters):
-            gev[i][0].record()
-            ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
-            gev[i][1].record()
-        torch.cuda.synchronize()
-        g_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in gev]))
-        g_bytes = T * Bg * (D // 2 + 8 + 8 + D * 4) + T * 4
-        g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
-        gather = {"kernel": "k_emb_fwd (INT4 packed, pooling 1)", "bags_per_table": Bg, "ms": round(g_ms, 4),
-                  "alg_bytes": g_bytes, "GBps": round(g_gbs, 1), "frac_of_peak": round(g_gbs / HBM_PEAK_GBS, 4),
-                  "bytes_per_lookup": D // 2 + 8 + 8 + D * 4}
-        del yg, gb
-
+    gather = gather_phase(a, ts, rows, T, D, dev) if a.gather_batch > 0 else None
     mlp = dense_phase(a, dev, world, rank) if a.mlp_iters > 0 else None
 
-    cpu = None  # the CPU baseline is an N=1 figure: rank 0 of a single-rank run only
+    cpu = cpu_c = None  # the CPU baselines are N=1 figures: a single-rank run only
     if world == 1 and a.cpu_baseline:
-        cpu = cpu_baseline(rows, D, min(B, 2048), a.seed)
+        cpu = cpu_baseline_torch(a, B)
+        cpu_c = cpu_baseline_oracle(a, min(B, 2048))
 
     # replicas must stay bit-identical (deterministic kernels, same exchanged data): compare a
     # checksum of every rank's W bit patterns and table maxima (outside the timed region)
@@ -294,41 +358,65 @@ def main():
         replicas_match = all(torch.equal(allcs[0], c) for c in allcs)
     else:
         replicas_match = True
-    prof = a.traffic_profile or os.path.join(ROOT, "profiles", f"r1_{PROFILE_TAG[a.config]}_summary.json")
+    prof = a.traffic_profile or os.path.join(ROOT, "profiles", f"r2_{PROFILE_TAG[a.config]}_summary.json")
     traffic = pmc_traffic(prof, dom, D)
     if rank == 0:
-        value = world * B * a.steps / elapsed
+        value = B_global * a.steps / elapsed
+        metric = {
+            "dp": "QAT-step samples/sec (DP embedding QAT step: INT4 fake-quant gather + sparse SGD + "
+                  "INT8 sparse-grad all-reduce)",
+            "fwd": "forward samples/sec (INT4 fake-quant EmbeddingBag forward, 26 tables)",
+            "sgd": "QAT-step samples/sec (1-GPU embedding QAT step: INT4 fake-quant gather + fused sparse SGD)",
+        }[a.mode]
+        coll = None
+        if a.mode == "dp":
+            coll = {"world_size": world, "backend": a.dist_backend if world > 1 else None,
+                    "per_step": 2 if world > 1 else 0,
+                    "scale_allgather_bytes_per_rank": ex.ws.absmax.numel() * 4,
+                    "payload_allgather_bytes_per_rank": int(ex.payload_bytes)}
         line = {
-            "metric": "QAT-step samples/sec (DP embedding QAT step: INT4 fake-quant gather + sparse SGD + INT8 sparse-grad all-reduce)",
-            "value": round(value, 1),
+            "metric": metric,
+            "value": round(value, 1) if err == 0 else None,
             "unit": "samples/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "us_per_step": round(elapsed / a.steps * 1e6, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32 (int4 fake-quant activations, int8 gradients)",
-            "data": "synthetic (uniform-random Criteo-form indices, U(+-sqrt(1/n)) tables, N(0,0.05) dL/dy)"
-            if a.index_dist == "uniform" else "synthetic (power-law indices)",
+            "data": ("synthetic (uniform-random Criteo-form indices, U(+-sqrt(1/n)) tables, N(0,0.05) dL/dy)"
+                     if a.index_dist == "uniform" else "synthetic (power-law indices)"),
             "config": {
-                "workload": f"criteo-{a.config} embedding QAT step",
-                "tables": T, "total_rows": sum(rows), "emb_dim": D,
-                "batch_per_gpu": B, "global_batch": B * world, "pooling": 1,
-                "grad_bits": a.grad_bits, "scale_period": 1, "parallelism": f"dp{world} (tables replicated)",
+                "workload": f"criteo-{a.config} embedding " + {"dp": "QAT step", "fwd": "forward",
+                                                               "sgd": "QAT step (fused SGD)"}[a.mode],
+                "mode": a.mode, "tables": T, "total_rows": sum(rows), "emb_dim": D,
+                "batch_per_gpu": B, "global_batch": B_global, "pooling": 1,
+                "grad_bits": a.grad_bits if a.mode == "dp" else None,
+                "scale_period": max(a.scale_period, 1), "packed_int4_forward": a.use_packed,
+                "hip_graph": a.graph, "parallelism": f"dp{world} (tables replicated)",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic["bytes"] if traffic else None, "traffic_unit": "bytes/launch",
                          "traffic_src": traffic,
-                         "alg_bytes_per_launch": alg[dom], "avg_launch_ms": round(dom_ms, 5),
+                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 5),
                          "timed_launches": len(sampled)},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
-            "kernels_ms_note": "untimed breakdown pass, every kernel bracketed by events",
+            "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events "
+                               "(apply_local and bwd_sgd include the |W| hierarchy finalize launch)",
+            "scale_refresh_ms": round(refresh_ms, 4) if refresh_ms is not None else None,
+            "scale_refresh_note": ("full INT4 repack of all tables (worst case: every scale moved), once per "
+                                   f"{a.scale_period} steps" if refresh_ms is not None else None),
+            "launch_share": (round(max(0.0, 1.0 - sum(kms.values()) / (elapsed / a.steps * 1e3)), 4)
+                             if not a.graph else None),
+            "collectives": coll,
             "int4_gather": gather,
             "mlp_grad_exchange": mlp,
             "cpu_baseline": cpu,
+            "cpu_baseline_oracle_c": cpu_c,
             "device_errors": err,
             "replicas_bit_identical": replicas_match,
             "setup_s": round(setup_s, 1),
@@ -337,6 +425,32 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if err:  # a step that dropped or mis-indexed lookups is not a measurement
+        print(f"device error flags 0x{err:x}", file=sys.stderr)
+        sys.exit(3)
+
+
+def gather_phase(a, ts, rows, T, D, dev):
+    """INT4 packed-gather bandwidth phase (north-star gather metric), outside the timed step."""
+    ts.refresh_scale_and_pack(4)
+    Bg = a.gather_batch
+    gb = make_batches(rows, Bg, 0, 1, 2, a.seed + 7, a.index_dist, dev)
+    yg = torch.empty(T, Bg, D, device=dev)
+    for i in range(5):
+        ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
+    gev = timed_events(a.gather_iters)
+    for i in range(a.gather_iters):
+        gev[i][0].record()
+        ts.forward(gb[i % 2], refresh_scale=False, use_packed=True, out=yg)
+        gev[i][1].record()
+    torch.cuda.synchronize()
+    g_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in gev]))
+    per = D // 2 + 8 + D * 4  # packed row + int64 index + f32 output row (offsets unread, pooling 1)
+    g_bytes = T * Bg * per + T * 4
+    g_gbs = g_bytes / (g_ms * 1e-3) / 1e9
+    return {"kernel": "k_emb_fwd_packed (INT4 rows, pooling 1)", "bags_per_table": Bg, "ms": round(g_ms, 4),
+            "alg_bytes": g_bytes, "GBps": round(g_gbs, 1), "frac_of_peak": round(g_gbs / HBM_PEAK_GBS, 4),
+            "bytes_per_lookup": per}
 
 
 def dense_phase(a, dev, world, rank):
@@ -352,10 +466,10 @@ def dense_phase(a, dev, world, rank):
     layers = []
     for dims in (bot, top):
         for i, o in zip(dims[:-1], dims[1:]):
-            l = torch.nn.Linear(i, o).to(dev)
-            l.weight.grad = torch.randn(o, i, device=dev, generator=g) * 1e-3
-            l.bias.grad = torch.randn(o, device=dev, generator=g) * 1e-3
-            layers.append(l)
+            lin = torch.nn.Linear(i, o).to(dev)
+            lin.weight.grad = torch.randn(o, i, device=dev, generator=g) * 1e-3
+            lin.bias.grad = torch.randn(o, device=dev, generator=g) * 1e-3
+            layers.append(lin)
     ex = DenseGradExchange(layers, grad_bits=8)
     P = ex.channels.total_elems
     wire_b = ex.wire.element_size()
@@ -383,16 +497,98 @@ def dense_phase(a, dev, world, rank):
             "note": "median of per-iteration HIP events; exchange+apply of all layers"}
 
 
-def cpu_baseline(rows, D, B, seed):
-    """The oracle (C restatement of the reference path, single thread) on a bounded sample:
-    tables capped at 1M rows (host RAM), a few full QAT steps incl. the reference's per-step
-    full-table |W| scan. kind = "port" (the reference itself cannot run here)."""
+class _FakeQuantSTE(torch.autograd.Function):
+    """SymmetricQuantFunction (quant_utils.py:316-363) followed by the dequant
+    (q_m_n_q_g.py:393): q = clamp(round(1/s * x + 0)), y = q * s; backward (g * s) / s."""
+
+    @staticmethod
+    def forward(ctx, x, s, bits):
+        ctx.s = s
+        n = 2 ** (bits - 1) - 1
+        return torch.clamp(torch.round(1.0 / s * x + 0), -n - 1, n) * s
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g * ctx.s) / ctx.s, None, None
+
+
+def cpu_threads() -> int:
+    """Host threads this process may use: OMP_NUM_THREADS (16 on the GPU box, its CPU
+    share) when set, else every CPU."""
+    return int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+
+
+def cpu_baseline_torch(a, B, rows_override=None):
+    """The reference's step in PyTorch on the host CPU, on a bounded sample: per step and
+    table, the full-table min/max scale (quant_utils.py:141-194), nn.EmbeddingBag(mode="sum",
+    sparse=True) forward, fake quant + dequant with the STE backward, autograd to the sparse
+    COO grad; then --mode dp: quantize_emb_grad at one rank (coalesce, max|g|/127 scale,
+    round/clamp, s_q_g_p_c.py:850-890) and W.add_(-lr * grad * scale) (:601-628); --mode
+    sgd: torch.optim.SGD's sparse step; --mode fwd: the forward alone. kind "port": the
+    reference itself may not be run here."""
+    torch.set_num_threads(cpu_threads())
+    cores = torch.get_num_threads()
+    tables = CPU_TABLES[a.config]
+    rows, D = (rows_override, _CONFIGS[tables][1]) if rows_override else _CONFIGS[tables]
+    T = len(rows)
+    g = torch.Generator().manual_seed(a.seed)
+    t_init = time.perf_counter()
+    embs = []
+    tile = torch.empty(1 << 18, D).uniform_(-1.0, 1.0, generator=g)  # CPU RNG is one thread: tile it
+    for n in rows:
+        w = torch.empty(n, D)
+        for r0 in range(0, n, tile.shape[0]):
+            k = min(tile.shape[0], n - r0)
+            torch.mul(tile[:k], float(np.sqrt(1 / n)), out=w[r0:r0 + k])
+        embs.append(torch.nn.EmbeddingBag(n, D, mode="sum", sparse=True, _weight=w))
+    init_s = time.perf_counter() - t_init
+    off = torch.arange(B, dtype=torch.int64)
+    opt = torch.optim.SGD([e.weight for e in embs], lr=a.lr) if a.mode == "sgd" else None
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        idx = [torch.randint(0, n, (B,), generator=g) for n in rows]
+        ys = []
+        for t, e in enumerate(embs):
+            with torch.no_grad():
+                mn, mx = torch.aminmax(e.weight)
+                s = torch.clamp(torch.maximum(mn.abs(), mx.abs()), min=1e-8) / 7.0
+            ys.append(_FakeQuantSTE.apply(e(idx[t], off), s, 4))
+        if a.mode != "fwd":
+            torch.autograd.backward(ys, [torch.full_like(y, 1e-3) for y in ys])
+            if opt is not None:
+                opt.step()
+                opt.zero_grad(set_to_none=True)
+            else:
+                with torch.no_grad():
+                    for e in embs:
+                        gc = e.weight.grad.coalesce()
+                        v = gc.values()
+                        sg = torch.clamp(v.abs().max(), min=1e-8) / 127.0
+                        q = torch.clamp(torch.round(1.0 / sg * v), -128, 127)
+                        e.weight.add_(torch.sparse_coo_tensor(gc.indices(), q * sg, gc.shape), alpha=-a.lr)
+                        e.weight.grad = None
+        steps += 1
+        el = time.perf_counter() - t0
+        if el > a.cpu_seconds or steps >= 500:
+            break
+    gb = sum(rows) * D * 4 / 1e9
+    return {"value": round(steps * B / el, 1), "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} {a.mode} steps of B={B}: the reference's op sequence in PyTorch-CPU "
+                      f"({cores} threads) on the '{tables}' tables ({sum(rows):,} rows x {D}, {gb:.1f} GB"
+                      + (", standing in for the 773 M-row GPU workload" if a.config == "terabyte" else "")
+                      + f"); table init {init_s:.1f} s untimed"}
+
+
+def cpu_baseline_oracle(a, B):
+    """Secondary figure: the oracle's C restatement (test infrastructure, one thread) on
+    tables capped at 1 M rows, a few seconds of dp steps."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     O.build()
+    rows, D = _CONFIGS[CPU_TABLES[a.config]]
     cap_rows = [min(n, 1_000_000) for n in rows]
-    rs = np.random.RandomState(seed)
+    rs = np.random.RandomState(a.seed)
     Ws = [rs.uniform(-np.sqrt(1 / n), np.sqrt(1 / n), (n, D)).astype(np.float32) for n in cap_rows]
     T = len(rows)
     t0 = time.perf_counter()
@@ -408,10 +604,11 @@ def cpu_baseline(rows, D, B, seed):
         O.dp_step(Ws, [[(P[t], np.arange(B)) for t in range(T)]], [[dyc[t] for t in range(T)]], s_fwd, 0.1, 8)
         steps += 1
         el = time.perf_counter() - t0
-        if el > 10.0 or steps >= 50:
+        if el > a.cpu_seconds / 3 or steps >= 50:
             break
     return {"value": round(steps * B / el, 1), "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"{steps} QAT steps, B={B}, {T} tables capped at 1M rows (D={D}), oracle C restatement, 1 thread"}
+            "sample": f"{steps} dp steps, B={B}, {T} tables capped at 1M rows (D={D}), oracle C restatement, "
+                      "1 thread"}
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ backed by hand-written HIP kernels behind the C ABI in ``include/dqrm.h`` (libdq
 from . import _lib
 from ._build import LIB_PATH, build
 from .tables import CoalescedGrad, EmbeddingTableSet, LookupBatch, default_caps, reference_scale
-from .comm import SparseGradExchange, get_my_slice, payload_bytes
+from .comm import MultiSetExchange, SparseGradExchange, get_my_slice, payload_bytes
 from .dense import DenseGradExchange
 from . import quant_modules_not_quantize_grad, sgd_quantized_gradients, sgd_quantized_gradients_parallel_comm
 from .quant_modules_not_quantize_grad import QuantEmbeddingBagCollection, QuantEmbeddingBagTwo
@@ -27,6 +27,7 @@ __all__ = [
     "default_caps",
     "reference_scale",
     "SparseGradExchange",
+    "MultiSetExchange",
     "get_my_slice",
     "payload_bytes",
     "DenseGradExchange",

@@ -58,11 +58,15 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_bwd_sgd",
     "dqrm_coalesce_slot_caps",
     "dqrm_emb_bwd_coalesce",
+    "dqrm_emb_bwd_lookup_grad",
+    "dqrm_rows_changed",
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
+    "dqrm_grad_quant_pack_strided",
     "dqrm_grad_quant_pack_ranked",
     "dqrm_emb_local_update",
     "dqrm_apply_sparse_update",
+    "dqrm_apply_sparse_update_strided",
     "dqrm_apply_local",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
@@ -173,10 +177,16 @@ def load(path: str | None = None) -> C.CDLL:
             C.c_int,
             [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, P, C.c_size_t, P],
         ),
+        "dqrm_emb_bwd_lookup_grad": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P]),
+        "dqrm_rows_changed": (C.c_int, [TS, P, C.c_int64, C.c_int, P]),
         "dqrm_payload_bytes": (C.c_size_t, [C.c_int, C.c_int64, C.c_int, C.c_int]),
         "dqrm_grad_quant_pack": (
             C.c_int,
             [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, C.c_int, P, C.c_int64, P, P, P],
+        ),
+        "dqrm_grad_quant_pack_strided": (
+            C.c_int,
+            [C.c_int, C.c_int, P, C.c_int64, P, P, P, P, C.c_int64, C.c_int, C.c_int, P, C.c_int64, P, P, P],
         ),
         "dqrm_grad_quant_pack_ranked": (
             C.c_int,
@@ -189,6 +199,10 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_apply_sparse_update": (
             C.c_int,
             [TS, P, C.c_int64, P, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
+        ),
+        "dqrm_apply_sparse_update_strided": (
+            C.c_int,
+            [TS, P, C.c_int64, P, C.c_size_t, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
         ),
         "dqrm_apply_local": (
             C.c_int,

@@ -59,20 +59,25 @@ class HipExchangeKernels:
         self.tables.backward_coalesce(batch, dy, ws, ste=ste, layout=layout)
 
     def quant_pack(self, ws, absmax_all, num_ranks, grad_bits, cap_base, cap_total, s_avg, payload):
+        """absmax_all [N, T*S] may be a column slice of a wider gathered buffer (its row
+        stride is passed as the pitch); payload a 16-B aligned slice of a wider one."""
         t = self.tables
+        pitch = absmax_all.stride(0) if absmax_all is not None and absmax_all.dim() == 2 else t.T * L.DQRM_TABLE_SPLIT
         L.check(
-            self.lib.dqrm_grad_quant_pack(
+            self.lib.dqrm_grad_quant_pack_strided(
                 t.T, t.D, _ptr(ws.slot_cap_base), ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount),
-                _ptr(absmax_all), num_ranks, grad_bits, _ptr(cap_base), cap_total, _ptr(s_avg), _ptr(payload),
-                _stream_handle()),
+                _ptr(absmax_all), pitch, num_ranks, grad_bits, _ptr(cap_base), cap_total, _ptr(s_avg),
+                _ptr(payload), _stream_handle()),
             "dqrm_grad_quant_pack",
         )
 
     def apply(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack):
+        """gathered [N, payload_bytes] may be a column slice of a wider gathered buffer."""
         t = self.tables
+        pitch = gathered.stride(0) if gathered.dim() == 2 else payload_bytes
         L.check(
-            self.lib.dqrm_apply_sparse_update(
-                C.byref(t.c), _ptr(cap_base), cap_total, _ptr(gathered), payload_bytes, num_ranks,
+            self.lib.dqrm_apply_sparse_update_strided(
+                C.byref(t.c), _ptr(cap_base), cap_total, _ptr(gathered), payload_bytes, pitch, num_ranks,
                 grad_bits, _ptr(s_avg), float(lr), mode, 4 if repack else 0, _stream_handle()),
             "dqrm_apply_sparse_update",
         )
@@ -107,6 +112,35 @@ def payload_bytes(num_tables: int, cap_total: int, dim: int, grad_bits: int) -> 
     return a16(4 * num_tables * L.DQRM_TABLE_SPLIT) + a16(4 * cap_total) + a16(cap_total * dim * elem)
 
 
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, world: int | None = None) -> None:
+    """out [N, ...] <- every rank's inp, in rank order. nccl (RCCL on ROCm): one
+    all_gather_into_tensor straight into `out` over xGMI; gloo: staged through host memory
+    when the tensors live on the GPU (functional rehearsal only)."""
+    world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
+    if world == 1:
+        out.view(-1)[: inp.numel()].copy_(inp.view(-1))
+        return
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        # RCCL reads/writes raw device memory: a dtype, layout or size mismatch would be
+        # silent corruption, so check what the collective assumes before issuing it
+        if out.dtype != inp.dtype:
+            raise TypeError(f"all_gather dtype mismatch: out {out.dtype}, inp {inp.dtype}")
+        if not (out.is_contiguous() and inp.is_contiguous()):
+            raise ValueError("all_gather needs contiguous tensors")
+        if out.numel() != world * inp.numel():
+            raise ValueError(f"all_gather size mismatch: out {out.numel()} != {world} x {inp.numel()}")
+        if not (out.is_cuda and inp.is_cuda and out.device == inp.device):
+            raise ValueError("RCCL all_gather needs both tensors on this rank's GPU")
+        dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=group)
+    elif out.is_cuda:  # Gloo gathers host tensors: stage through host memory (debug / rehearsal)
+        host = out.cpu()
+        dist.all_gather(list(host.unbind(0)), inp.cpu(), group=group)
+        out.copy_(host)
+    else:
+        dist.all_gather(list(out.unbind(0)), inp, group=group)
+
+
 class SparseGradExchange:
     """Per-step DP embedding update: coalesce -> all-gather of per-slot max|grad| ->
     scale average + quantize-pack -> payload all-gather -> decode + SGD.
@@ -118,7 +152,10 @@ class SparseGradExchange:
     """
 
     def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None,
-                 kernels: ExchangeKernels | None = None, device=None):
+                 kernels: ExchangeKernels | None = None, device=None, absmax_buf: torch.Tensor | None = None,
+                 payload_buf: torch.Tensor | None = None):
+        """absmax_buf / payload_buf: caller-owned slices of buffers several sets gather
+        together (MultiSetExchange); the per-set gather buffers are then not allocated."""
         if not (grad_bits == 32 or 2 <= grad_bits <= 16):
             raise ValueError("grad_bits must be 2..16 or 32")
         self.tables = tables
@@ -131,7 +168,7 @@ class SparseGradExchange:
         self.device = dev
         self.kernels = kernels if kernels is not None else HipExchangeKernels(tables)
         T = tables.T
-        self.ws = CoalescedGrad.allocate(tables.num_rows, max_lookups, tables.D, dev)
+        self.ws = CoalescedGrad.allocate(tables.num_rows, max_lookups, tables.D, dev, absmax=absmax_buf)
         self.caps = default_caps(tables.num_rows, max_lookups)
         base = [0]
         for c in self.caps:
@@ -139,25 +176,20 @@ class SparseGradExchange:
         self.cap_total = base[-1]
         self.cap_base = torch.tensor(base, dtype=torch.int64, device=dev)
         self.payload_bytes = payload_bytes(T, self.cap_total, tables.D, grad_bits)
-        self.absmax_all = torch.zeros(self.world, T * L.DQRM_TABLE_SPLIT, dtype=torch.float32, device=dev)
         self.s_avg = torch.zeros(T, dtype=torch.float32, device=dev)
-        self.payload = torch.zeros(self.payload_bytes, dtype=torch.uint8, device=dev)
-        self.gathered = torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8, device=dev)
+        shared = payload_buf is not None
+        if shared and (payload_buf.numel() != self.payload_bytes or payload_buf.dtype != torch.uint8
+                       or payload_buf.data_ptr() % 16):
+            raise ValueError("payload_buf must be a 16-B aligned uint8 [payload_bytes] tensor")
+        self.payload = payload_buf if shared else torch.zeros(self.payload_bytes, dtype=torch.uint8, device=dev)
+        self.absmax_all = None if shared else torch.zeros(self.world, T * L.DQRM_TABLE_SPLIT, dtype=torch.float32,
+                                                          device=dev)
+        self.gathered = None if shared else torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8,
+                                                        device=dev)
 
     # -------------------------------------------------------------- collectives
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        if self.world == 1:
-            out[0].copy_(inp)
-            return
-        backend = dist.get_backend(self.group)
-        if backend == "nccl":  # RCCL on ROCm: one all-gather straight into the output
-            dist.all_gather_into_tensor(out.view(-1), inp.view(-1), group=self.group)
-        elif out.is_cuda:  # Gloo gathers host tensors: stage through host memory (debug / rehearsal)
-            host = out.cpu()
-            dist.all_gather(list(host.unbind(0)), inp.cpu(), group=self.group)
-            out.copy_(host)
-        else:
-            dist.all_gather(list(out.unbind(0)), inp, group=self.group)
+        all_gather_into(out, inp, self.group, self.world)
 
     # -------------------------------------------------------------- the step
     def exchange(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True, layout: str = "tbd") -> torch.Tensor:
@@ -246,10 +278,90 @@ class SparseGradExchange:
         return torch.from_numpy(a / np.float32(2 ** (self.grad_bits - 1) - 1))
 
 
+class MultiSetExchange:
+    """One exchange for several table sets: the unchanged DP driver's ModuleList of 26
+    single-table QuantEmbeddingBagTwo modules (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:380)
+    gets the same TWO collectives per step as one 26-table set, instead of the reference's
+    2 blocking collectives per table (s_q_g_p_c.py:278-315):
+      per set   coalesce into its workspace, its per-slot max|grad| landing in its slice
+                of one concatenated [sum T*S] buffer
+      1 x       all-gather of the concatenated maxima
+      per set   quantize-pack into its slice of one concatenated payload (the strided
+                quant-pack reads its column of the gathered maxima)
+      1 x       all-gather of the concatenated payloads
+      per set   decode its column of the gathered payloads + SGD (strided apply)
+    Per-set results are bit-identical to a SparseGradExchange per set."""
+
+    def __init__(self, sets, max_lookups, grad_bits: int = 8, group=None, kernels=None, device=None):
+        sets = list(sets)
+        if not sets:
+            raise ValueError("no table sets")
+        ml = list(max_lookups) if isinstance(max_lookups, (list, tuple)) else [int(max_lookups)] * len(sets)
+        self.sets = sets
+        self.grad_bits = grad_bits
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.max_lookups = [int(m) for m in ml]
+        dev = torch.device(device if device is not None else sets[0].device)
+        S = L.DQRM_TABLE_SPLIT
+        ts_n = [s.T * S for s in sets]
+        pb_n = [payload_bytes(s.T, sum(default_caps(s.num_rows, m)), s.D, grad_bits) for s, m in zip(sets, ml)]
+        self.am_off = [sum(ts_n[:i]) for i in range(len(sets) + 1)]
+        self.pl_off = [sum(pb_n[:i]) for i in range(len(sets) + 1)]
+        self.absmax = torch.zeros(self.am_off[-1], dtype=torch.float32, device=dev)
+        self.payload = torch.zeros(self.pl_off[-1], dtype=torch.uint8, device=dev)
+        self.absmax_all = torch.zeros(self.world, self.am_off[-1], dtype=torch.float32, device=dev)
+        self.gathered = torch.zeros(self.world, self.pl_off[-1], dtype=torch.uint8, device=dev)
+        ks = kernels if kernels is not None else [None] * len(sets)
+        self.parts = [
+            SparseGradExchange(s, m, grad_bits=grad_bits, group=group, kernels=k, device=dev,
+                               absmax_buf=self.absmax[self.am_off[i]: self.am_off[i + 1]],
+                               payload_buf=self.payload[self.pl_off[i]: self.pl_off[i + 1]])
+            for i, (s, m, k) in enumerate(zip(sets, ml, ks))]
+
+    def exchange(self, items) -> list[torch.Tensor]:
+        """items[i] = (batch, dy, ste, layout) of set i, or None (no backward: the set sends
+        no rows). Returns each set's averaged gradient scale (emb_scaling_factor)."""
+        gb, N = self.grad_bits, self.world
+        for p, it in zip(self.parts, items):
+            if it is None:
+                p.ws.ucount.zero_()
+                p.ws.absmax.zero_()
+            else:
+                batch, dy, ste, layout = it
+                p.kernels.coalesce(batch, dy, p.ws, ste, layout)
+        if gb != 32 and N > 1:
+            all_gather_into(self.absmax_all, self.absmax, self.group, N)
+        for i, p in enumerate(self.parts):
+            am = (self.absmax_all[:, self.am_off[i]: self.am_off[i + 1]] if gb != 32 and N > 1
+                  else p.ws.absmax.view(1, -1))
+            p.kernels.quant_pack(p.ws, am, N, gb, p.cap_base, p.cap_total, p.s_avg, p.payload)
+        if N > 1:
+            all_gather_into(self.gathered, self.payload, self.group, N)
+        return [p.s_avg for p in self.parts]
+
+    def apply(self, lr: float, mode: int | None = None, repack=False) -> None:
+        """weight_update_parallel_comm's embedding branch for every set; repack: bool or
+        one bool per set."""
+        gb, N = self.grad_bits, self.world
+        if mode is None:
+            mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
+        rp = list(repack) if isinstance(repack, (list, tuple)) else [bool(repack)] * len(self.parts)
+        for i, p in enumerate(self.parts):
+            g = self.gathered[:, self.pl_off[i]: self.pl_off[i + 1]] if N > 1 else p.payload.view(1, -1)
+            p.kernels.apply(p.cap_base, p.cap_total, g, p.payload_bytes, N, gb, p.s_avg, lr, mode, rp[i])
+
+    @property
+    def collective_bytes(self) -> tuple[int, int]:
+        """Bytes each rank contributes to the two all-gathers (maxima, payloads)."""
+        return self.absmax.numel() * 4, self.payload.numel()
+
+
 def get_my_slice(n: int, my_size: int, my_rank: int) -> slice:
     """Contiguous per-rank batch slice (dlrm_s_pytorch_single_gpu.py:989-993)."""
     k, m = divmod(n, my_size)
     return slice(my_rank * k + min(my_rank, m), (my_rank + 1) * k + min(my_rank + 1, m), 1)
 
 
-__all__ = ["SparseGradExchange", "HipExchangeKernels", "payload_bytes", "get_my_slice"]
+__all__ = ["SparseGradExchange", "MultiSetExchange", "HipExchangeKernels", "payload_bytes", "get_my_slice",
+           "all_gather_into"]

@@ -1471,7 +1471,8 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
                                                     int64_t ws_cap_total, const int32_t* __restrict__ ws_rows,
                                                     const float* __restrict__ ws_vals,
                                                     const int32_t* __restrict__ ws_ucount,
-                                                    const float* __restrict__ absmax_all, int N, int bits,
+                                                    const float* __restrict__ absmax_all, int64_t am_pitch,
+                                                    int N, int bits,
                                                     const int64_t* __restrict__ cap_base, int64_t cap_total,
                                                     float* __restrict__ s_avg, unsigned char* __restrict__ payload,
                                                     const int32_t* __restrict__ tbits,
@@ -1493,7 +1494,7 @@ __global__ void __launch_bounds__(512) k_quant_pack(int T, const int64_t* __rest
     if (threadIdx.x < SPLIT) s_cnt[threadIdx.x] = send ? ws_ucount[t * SPLIT + threadIdx.x] : 0;
     if (quant)
         for (int j = threadIdx.x; j < N * SPLIT; j += blockDim.x)
-            s_am[j] = absmax_all[((int64_t)(j / SPLIT) * T + t) * SPLIT + (j % SPLIT)];
+            s_am[j] = absmax_all[(int64_t)(j / SPLIT) * am_pitch + t * SPLIT + (j % SPLIT)];
     __syncthreads();
     if (threadIdx.x == 0) {
         const int cap = (int)(cap_base[t + 1] - cap_base[t]);
@@ -3186,6 +3187,105 @@ int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
     return (int)b;
 }
 
+// ------------------------------------------------------------------------------------
+// Rows rewritten outside libdqrm (torch.optim.SGD stepping on the grad_mode="sparse" COO):
+// one lane group per listed slab row recomputes its rowmax (and, repack, its INT4 row with
+// the frozen pscale) and flags its block and superblock; the untracked finalize then
+// re-reduces exactly those blocks and every table maximum.
+// ------------------------------------------------------------------------------------
+template <int LPR>
+__global__ void __launch_bounds__(256) k_rows_changed(const float* __restrict__ W, float* __restrict__ rowmax,
+                                                      uint8_t* __restrict__ bdirty, uint8_t* __restrict__ sdirty,
+                                                      uint8_t* __restrict__ packed, const float* __restrict__ pscale,
+                                                      const int64_t* __restrict__ meta, int T,
+                                                      const int64_t* __restrict__ rows, int64_t n, int64_t total,
+                                                      uint32_t* __restrict__ err) {
+    constexpr int G = 256 / LPR;
+    const int lane = threadIdx.x % LPR;
+    const Meta m = make_meta(meta, T);
+    for (int64_t i = (int64_t)blockIdx.x * G + threadIdx.x / LPR; i < n; i += (int64_t)gridDim.x * G) {
+        const int64_t g = rows[i];
+        if (g < 0 || g >= total) {
+            if (lane == 0) flag_error(err, DQRM_ERRF_INDEX);
+            continue;
+        }
+        const int t = find_table(m.row_base, T, g);
+        const int64_t r = g - m.row_base[t];
+        const float4 w = reinterpret_cast<const float4*>(W + g * (LPR * 4))[lane];
+        float v = abs_max4(w);
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, LPR));
+        if (packed) pack_row_int4<LPR>(w, packed, g, lane, 1.0f / pscale[t]);
+        if (lane == 0) {
+            rowmax[g] = v;
+            bdirty[m.blk_base[t] + r / BLK] = 1;
+            sdirty[m.sblk_base[t] + r / ((int64_t)BLK * SBLK_BLOCKS)] = 1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Per-lookup (uncoalesced) sparse gradient, the form nn.EmbeddingBag(sparse=True) hands to
+// autograd (embedding_bag_backward's sparse branch: indices = the input indices, values =
+// the bag's gradient row once per lookup, in lookup order): lookup j of table t gets
+// rows[j] = row_base[t] + idx[j] and vals[j] = (dy[t, bag(j)] * s_t) / s_t (STE,
+// quant_utils.py:349-363). One lane group per bag, its dy row loaded once and stored for
+// each of its lookups (coalesced float4 stores), grid (bag chunks, tables).
+// ------------------------------------------------------------------------------------
+struct LgArgs {
+    const int64_t* meta;
+    const float* scale;
+    uint32_t* err;
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    const float* dy;
+    int64_t dst_t, dst_b;
+    int64_t B;
+    int64_t* rows;
+    float* vals;
+    int T;
+    int ste;
+    int pool1;
+};
+
+template <int LPR>
+__global__ void __launch_bounds__(256) k_lookup_grad(LgArgs a) {
+    const int t = blockIdx.y;
+    constexpr int G = 256 / LPR;
+    const int lane = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int D = LPR * 4;
+    const float s = a.scale[t];
+    const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
+    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    const int64_t B = a.B;
+    const int64_t* __restrict__ off = a.off + (int64_t)t * B;
+    const bool p1 = a.pool1 && L == B;
+    for (int64_t b = (int64_t)blockIdx.x * G + grp; b < B; b += (int64_t)gridDim.x * G) {
+        int64_t s0 = p1 ? b : off[b];
+        int64_t s1 = p1 ? b + 1 : ((b + 1 < B) ? off[b + 1] : L);
+        if (s0 < 0 || s1 > L || s1 < s0) {
+            if (lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
+            s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+            s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+        }
+        if (s1 == s0) continue;
+        float4 g = reinterpret_cast<const float4*>(a.dy + (int64_t)t * a.dst_t + b * a.dst_b)[lane];
+        if (a.ste) { g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s; }
+        for (int64_t j = s0; j < s1; ++j) {
+            int64_t r = a.idx[ibase + j];
+            float4 v = g;
+            if (r < 0 || r >= nrows) {  // flagged; the entry becomes a zero row on the table's row 0
+                if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+                r = 0;
+                v = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            if (lane == 0) a.rows[ibase + j] = rowbase + r;
+            reinterpret_cast<float4*>(a.vals + (ibase + j) * D)[lane] = v;
+        }
+    }
+}
+
 #define DISPATCH_LPR(D, ...)                                  \
     switch ((D) / 4) {                                        \
         case 1: { constexpr int LPR = 1; __VA_ARGS__; } break;  \
@@ -3455,6 +3555,54 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     return launch_bwd<0>(c, (hipStream_t)stream, "dqrm_emb_bwd_sgd");
 }
 
+int dqrm_rows_changed(const dqrm_table_set* set, const int64_t* rows, int64_t n, int repack_bits, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && !rows)) return set_error(DQRM_E_INVALID, "%s: bad row list", "dqrm_rows_changed");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_rows_changed",
+                         repack_bits);
+    if (n == 0) return DQRM_OK;
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* pk = repack_bits == 4 ? set->packed : nullptr;
+    DISPATCH_LPR(set->dim, {
+        constexpr int G = 256 / LPR;
+        hipLaunchKernelGGL(k_rows_changed<LPR>, dim3(grid_for(n, G, 4096)), dim3(256), 0, st, set->W, set->rowmax,
+                           set->bdirty, set->sdirty, pk, set->pscale, set->meta, set->num_tables, rows, n,
+                           set->total_rows, (uint32_t*)set->err);
+    });
+    LAUNCH_CHECK();
+    return launch_finalize(set, st, false);
+}
+
+int dqrm_emb_bwd_lookup_grad(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                             int64_t dy_stride_t, int64_t dy_stride_b, int ste, int64_t* rows, float* vals,
+                             void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_lookup_grad"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0",
+                         "dqrm_emb_bwd_lookup_grad");
+    if (!rows || !vals || (((uintptr_t)vals) & 15))
+        return set_error(DQRM_E_INVALID, "%s: rows / 16-B aligned vals required", "dqrm_emb_bwd_lookup_grad");
+    if (batch->num_bags <= 0) return DQRM_OK;
+    LgArgs a;
+    a.meta = set->meta; a.scale = set->scale; a.err = (uint32_t*)set->err; a.idx = batch->idx; a.off = batch->off;
+    a.idx_base = batch->idx_base; a.dy = dy; a.dst_t = dy_stride_t; a.dst_b = dy_stride_b; a.B = batch->num_bags;
+    a.rows = rows; a.vals = vals; a.T = set->num_tables; a.ste = ste;
+    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_LPR(set->dim, {
+        constexpr int G = 256 / LPR;
+        int64_t gx = (a.B + G - 1) / G;
+        if (gx > 4096) gx = 4096;
+        hipLaunchKernelGGL(k_lookup_grad<LPR>, dim3((unsigned)gx, (unsigned)a.T), dim3(256), 0, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
 int64_t dqrm_coalesce_slot_caps(const int64_t* num_rows_host, int num_tables, int64_t max_lookups,
                                 int64_t* ws_cap_base_host) {
     if (!num_rows_host || !ws_cap_base_host || num_tables <= 0 || max_lookups < 0)
@@ -3498,10 +3646,11 @@ size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_b
     return (size_t)payload_layout(num_tables, cap_total, dim, grad_bits).bytes;
 }
 
-int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
-                         const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
-                         const float* absmax_all, int num_ranks, int grad_bits, const int64_t* cap_base,
-                         int64_t cap_total, float* s_avg, void* payload, void* stream) {
+int dqrm_grad_quant_pack_strided(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                                 const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                                 const float* absmax_all, int64_t absmax_pitch, int num_ranks, int grad_bits,
+                                 const int64_t* cap_base, int64_t cap_total, float* s_avg, void* payload,
+                                 void* stream) {
     if (num_tables <= 0 || num_tables > MAX_TABLES || num_ranks <= 0 || num_ranks > 64)
         return set_error(DQRM_E_INVALID, "%s: bad num_tables/num_ranks", "dqrm_grad_quant_pack");
     if (!(grad_bits == 32 || (grad_bits >= 2 && grad_bits <= 16)))
@@ -3509,15 +3658,29 @@ int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, in
     if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !cap_base || !payload ||
         (grad_bits != 32 && (!absmax_all || !s_avg)))
         return set_error(DQRM_E_INVALID, "%s: null pointer", "dqrm_grad_quant_pack");
+    if (num_ranks > 1 && absmax_pitch < (int64_t)num_tables * SPLIT)
+        return set_error(DQRM_E_INVALID, "%s: absmax pitch %lld < %d", "dqrm_grad_quant_pack",
+                         (long long)absmax_pitch, num_tables * SPLIT);
+    if (((uintptr_t)payload) & 15)
+        return set_error(DQRM_E_INVALID, "%s: payload must be 16-B aligned", "dqrm_grad_quant_pack");
     hipStream_t st = (hipStream_t)stream;
     DISPATCH_LPR(dim, {
         hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
                            num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, absmax_all,
-                           num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload,
+                           absmax_pitch, num_ranks, grad_bits, cap_base, cap_total, s_avg, (unsigned char*)payload,
                            (const int32_t*)nullptr, (const float*)nullptr);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
+}
+
+int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                         const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                         const float* absmax_all, int num_ranks, int grad_bits, const int64_t* cap_base,
+                         int64_t cap_total, float* s_avg, void* payload, void* stream) {
+    return dqrm_grad_quant_pack_strided(num_tables, dim, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount,
+                                        absmax_all, (int64_t)num_tables * SPLIT, num_ranks, grad_bits, cap_base,
+                                        cap_total, s_avg, payload, stream);
 }
 
 int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
@@ -3532,7 +3695,7 @@ int dqrm_grad_quant_pack_ranked(int num_tables, int dim, const int64_t* ws_cap_b
     DISPATCH_LPR(dim, {
         hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
                            num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount,
-                           (const float*)nullptr, 1, 8, cap_base, cap_total, (float*)nullptr,
+                           (const float*)nullptr, (int64_t)0, 1, 8, cap_base, cap_total, (float*)nullptr,
                            (unsigned char*)payload, table_bits, table_scale);
     });
     LAUNCH_CHECK();
@@ -3556,9 +3719,10 @@ int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, co
     return launch_bwd<2>(c, (hipStream_t)stream, "dqrm_emb_local_update");
 }
 
-int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
-                             const void* payloads, size_t payload_bytes, int num_ranks, int grad_bits,
-                             const float* s_avg, float lr, int mode, int repack_bits, void* stream) {
+int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                                     const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
+                                     int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
+                                     void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS || !payloads || !cap_base)
@@ -3567,13 +3731,16 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
         return set_error(DQRM_E_INVALID, "%s: mode/grad_bits mismatch (%d)", "dqrm_apply_sparse_update", grad_bits);
     if (payload_bytes != dqrm_payload_bytes(set->num_tables, cap_total, set->dim, grad_bits))
         return set_error(DQRM_E_INVALID, "%s: payload_bytes mismatch", "dqrm_apply_sparse_update");
+    if (rank_pitch < payload_bytes || (rank_pitch & 15) || (((uintptr_t)payloads) & 15))
+        return set_error(DQRM_E_INVALID, "%s: rank pitch %zu / payload alignment", "dqrm_apply_sparse_update",
+                         rank_pitch);
     if (repack_bits && (repack_bits != 4 || !set->packed))
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_apply_sparse_update", repack_bits);
     ApplyArgs a;
     a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
     a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.pscale = set->pscale; a.meta = set->meta;
     a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
-    a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)payload_bytes;
+    a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)rank_pitch;  // rank stride
     a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
     a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty; a.tmax = set->tmax;
     hipStream_t st = (hipStream_t)stream;
@@ -3604,6 +3771,13 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
     }
     LAUNCH_CHECK();
     return launch_finalize(set, st, flat);
+}
+
+int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                             const void* payloads, size_t payload_bytes, int num_ranks, int grad_bits,
+                             const float* s_avg, float lr, int mode, int repack_bits, void* stream) {
+    return dqrm_apply_sparse_update_strided(set, cap_base, cap_total, payloads, payload_bytes, payload_bytes,
+                                            num_ranks, grad_bits, s_avg, lr, mode, repack_bits, stream);
 }
 
 int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int64_t ws_cap_total,

@@ -11,8 +11,9 @@ state-dict keys (:258-280, :288), and its semantics (:317-398):
   * test_mode forward: the last training scale is reused (:331);
   * full_precision_flag: plain FP32 EmbeddingBag sum;
   * backward: STE (g*s)/s (quant_utils.py:349-363), then one of
-      grad_mode="sparse"    -> a coalesced sparse COO ``embedding_bag.weight.grad``
-                               (usable by torch.optim.SGD or the DP hooks below),
+      grad_mode="sparse"    -> the uncoalesced sparse COO ``embedding_bag.weight.grad``
+                               nn.EmbeddingBag(sparse=True) produces (one entry per
+                               lookup), for torch.optim.SGD,
       grad_mode="fused_sgd" -> the update W -= lr * grad is applied inside the backward
                                kernel with torch.optim.SGD's rounding (per lookup, in order),
       grad_mode="dp"        -> the gradient is kept on device for
@@ -31,11 +32,32 @@ import torch
 from torch import nn
 
 from . import _lib as L
-from .comm import SparseGradExchange
 from .tables import EmbeddingTableSet, LookupBatch
 
 
 _DEFAULT_GRAD_MODE = "sparse"
+_ERROR_CHECK_EVERY = 1
+
+
+def set_error_check_interval(steps: int) -> None:
+    """Read the tables' device error flags (out-of-range index, bad offsets) every `steps`
+    training calls -- in the module's forward for grad_mode "sparse" / "fused_sgd", in
+    weight_update_parallel_comm for "dp" -- and raise DQRMError when one is set (ATen raises
+    on such input). 0 = never. Each read synchronises the host with the stream once."""
+    global _ERROR_CHECK_EVERY
+    _ERROR_CHECK_EVERY = max(0, int(steps))
+
+
+def error_check_due(owner) -> bool:
+    n = getattr(owner, "_dqrm_err_calls", 0) + 1
+    owner._dqrm_err_calls = n
+    return _ERROR_CHECK_EVERY > 0 and n % _ERROR_CHECK_EVERY == 0
+
+
+def raise_device_errors(flags: int) -> None:
+    if flags:
+        raise L.DQRMError(f"embedding kernels flagged device errors 0x{flags:x} (1 = index out of range, "
+                          "2 = bad offsets, 4 = more lookups than max_lookups)")
 
 
 def set_default_grad_mode(mode: str) -> None:
@@ -109,10 +131,25 @@ class _QuantEmbeddingBase(nn.Module):
         self.scale_period = int(scale_period)
         self.use_packed_int4 = bool(use_packed_int4)
         self._pending = None      # (batch, dy, ste, layout) for grad_mode == "dp"
-        self._exchange = None     # SparseGradExchange used by the DP hooks
+        self._exchange = None     # SparseGradExchange of the ranking-range hooks
         self._ready = None        # grad bits of an exchanged, not yet applied update
         self._counters = None     # host mirror of (now_iteration, iteration_bound, iteration_nt)
         self._rr = None           # ranking range: (bits host int32 [T], bits dev, scale dev) of this step
+        self._ext_rows = None     # rows of the last sparse grad handed to an optimizer (grad_mode "sparse")
+
+    def _sync_external_update(self) -> None:
+        """grad_mode "sparse": the optimizer stepped W on the rows of the last COO outside
+        libdqrm; bring their maxima (the refreshing forward's full-table scale) and INT4 rows
+        up to date before the next forward reads them."""
+        if self._ext_rows is not None:
+            self._tset.rows_changed(self._ext_rows, repack=self._use_packed(False))
+            self._ext_rows = None
+
+    def _check_errors(self, test_mode: bool) -> None:
+        """grad_mode "sparse" / "fused_sgd": flags raised by the previous call's kernels
+        surface here, at the next training call (the DP hooks check them for "dp")."""
+        if self.grad_mode != "dp" and not test_mode and error_check_due(self):
+            raise_device_errors(self._tset.read_errors())
 
     # ------------------------------------------------------------ scale refresh logic
     def _refresh_due(self, fp: bool, test_mode: bool) -> bool:
@@ -159,24 +196,12 @@ class _QuantEmbeddingBase(nn.Module):
         return self._sparse_grad(batch, dy, ste, layout)
 
     def _sparse_grad(self, batch, dy, ste, layout):
-        ex = SparseGradExchange(self._tset, max(batch.max_lookups, 1), grad_bits=32, device=self._tset.device)
-        self._tset.backward_coalesce(batch, dy, ex.ws, ste=ste, layout=layout)
-        ws = ex.ws
-        rows, vals = [], []
-        uc = ws.ucount.cpu().tolist()
-        base = ws.slot_base
-        for k, u in enumerate(uc):
-            if u:  # slot k = t * DQRM_TABLE_SPLIT + s; table-local rows -> slab rows
-                t = k // L.DQRM_TABLE_SPLIT
-                rows.append(ws.rows[base[k]: base[k] + u].to(torch.int64) + self._tset.row_base[t])
-                vals.append(ws.vals[base[k]: base[k] + u])
-        R, D = self._tset.R, self._tset.D
-        dev = self._tset.device
-        if not rows:
-            return torch.sparse_coo_tensor(torch.zeros(1, 0, dtype=torch.int64, device=dev),
-                                           torch.zeros(0, D, device=dev), (R, D))
-        g_rows = torch.cat(rows).to(torch.int64)
-        return torch.sparse_coo_tensor(g_rows.view(1, -1), torch.cat(vals), (R, D))._coalesced_(True)
+        """The uncoalesced COO nn.EmbeddingBag(sparse=True) yields: one (row, STE'd dy row)
+        entry per lookup, in lookup order (one libdqrm launch, no host sync). torch.optim.SGD
+        then adds it to W exactly as it adds the reference's own embedding gradient."""
+        rows, vals = self._tset.lookup_grad(batch, dy, ste=ste, layout=layout)
+        self._ext_rows = rows
+        return torch.sparse_coo_tensor(rows.view(1, -1), vals, (self._tset.R, self._tset.D), is_coalesced=False)
 
 
 class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
@@ -231,6 +256,8 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
 
     def forward(self, input, offsets=None, per_sample_weights=None, full_precision_flag=False, test_mode=False):
         fp = bool(full_precision_flag or self.full_precision_flag)
+        self._check_errors(test_mode)
+        self._sync_external_update()
         if self.quant_mode not in ("symmetric", "speed_symmetric", "asymmetric"):
             raise ValueError("unknown quant mode: {}".format(self.quant_mode))
         refresh = self._refresh_due(fp, test_mode)
@@ -252,6 +279,8 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
     def load_state_dict(self, state_dict, strict=True, assign=False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
         self._tset.refresh_absmax()  # W changed outside the kernels: rebuild the |W| hierarchy
+        if self._tset.packed is not None:  # the loaded rows, packed with their own scales
+            self._tset.repack_all(self.embedding_bit)
         self._counters = None
         return out
 
@@ -294,6 +323,8 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         """lS_o / lS_i: per-table lists or stacked [T, B] tensors (dlrm_data_pytorch.py:328-345).
         layout "list" -> list of T [B, D] tensors (apply_emb's ly); "btd" -> [B, T, D]."""
         fp = bool(full_precision_flag or self.full_precision_flag)
+        self._check_errors(test_mode)
+        self._sync_external_update()
         refresh = self._refresh_due(fp, test_mode)
         batch = LookupBatch(lS_i, lS_o, device=self._tset.device)
         if refresh and self._use_packed(fp):
@@ -310,8 +341,11 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
     def load_state_dict(self, state_dict, strict=True, assign=False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
         self._tset.refresh_absmax()
+        if self._tset.packed is not None:  # the loaded rows, packed with their own scales
+            self._tset.repack_all(self.embedding_bit)
         self._counters = None
         return out
 
 
-__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode"]
+__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode",
+           "set_error_check_interval"]

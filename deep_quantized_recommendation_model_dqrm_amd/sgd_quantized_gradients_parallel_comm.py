@@ -9,12 +9,19 @@ used by the data-parallel drivers (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:185
 ``model`` exposes ``emb_l`` / ``bot_l`` / ``top_l`` as the reference's DLRM_Net does. The
 embedding tables must be this package's modules built with ``grad_mode="dp"``: their
 backward leaves the upstream gradient on the device, and the embedding branch below runs
-the fused exchange (libdqrm kernels + two all-gathers for ALL tables of a module) instead of
-the reference's 2 blocking Gloo collectives per table. Results per table are the
-reference's: the averaged scale lands in ``emb_scaling_factor`` and the update applied by
-``weight_update_parallel_comm`` is W += -lr * ((sum_r q_r) * 1/N) * s  (integer sums exact).
+ONE fused exchange for all modules of ``emb_l`` -- a QuantEmbeddingBagCollection or the
+unchanged driver's ModuleList of 26 QuantEmbeddingBagTwo alike (comm.MultiSetExchange:
+libdqrm kernels + two all-gathers per step) -- instead of the reference's 2 blocking Gloo
+collectives per table. Results per table are the reference's: the averaged scale lands in
+``emb_scaling_factor`` and the update applied by ``weight_update_parallel_comm`` is
+W += -lr * ((sum_r q_r) * 1/N) * s  (integer sums exact). After the update the hooks read
+the tables' device error flags (one shared word, one read per step; every
+``set_error_check_interval`` steps) and raise DQRMError if a kernel flagged bad input.
 
-The MLP branch (QuantLinear / nn.Linear layers of bot_l, top_l) runs
+The MLP branch (QuantLinear-like layers of bot_l, top_l -- those carrying
+``weight_scaling_factor``, as the reference's isinstance(QuantLinear / LinearCompressedGrad)
+checks select, s_q_g_p_c.py:339,376,632,652; plain nn.Linear only after
+``set_mlp_plain_linear(True)``) runs
 quantize_linear_grad / quantize_bias_grad (s_q_g_p_c.py:892-961) for all layers as one
 channel table through libdqrm's dense kernels (dense.DenseGradExchange): one all-gather of
 the per-channel scales and one exact integer-valued fp16 all-reduce per step instead of 4
@@ -27,9 +34,19 @@ import torch.distributed as dist
 from torch import nn
 
 from . import _lib as L
-from .comm import SparseGradExchange
+from .comm import MultiSetExchange, SparseGradExchange
 from .dense import DenseGradExchange
-from .quant_modules_not_quantize_grad import _QuantEmbeddingBase
+from .quant_modules_not_quantize_grad import (_QuantEmbeddingBase, error_check_due, raise_device_errors,
+                                              set_error_check_interval)
+
+_MLP_PLAIN_LINEAR = False
+
+
+def set_mlp_plain_linear(include: bool) -> None:
+    """Also exchange/update plain nn.Linear MLP layers (the reference touches only
+    QuantLinear / LinearCompressedGrad layers and leaves plain Linear ones alone)."""
+    global _MLP_PLAIN_LINEAR
+    _MLP_PLAIN_LINEAR = bool(include)
 
 
 # ---------------------------------------------------------------------------- helpers
@@ -52,7 +69,8 @@ def _linear_layers(model, name: str) -> list[nn.Module]:
     seq = getattr(model, name, None)
     if seq is None:
         raise Warning("Cannot find the list of {} linear layers".format("bottom" if name == "bot_l" else "top"))
-    return [l for l in seq if isinstance(l, nn.Linear) or hasattr(l, "weight_scaling_factor")]
+    return [l for l in seq if type(l).__name__ in ("QuantLinear", "LinearCompressedGrad")
+            or (isinstance(l, nn.Linear) and _MLP_PLAIN_LINEAR)]
 
 
 def _detach_grad(g: torch.Tensor) -> None:
@@ -73,20 +91,37 @@ def _ensure_exchange(m: _QuantEmbeddingBase, grad_bits: int, group) -> SparseGra
     return ex
 
 
-def _exchange_module(m: _QuantEmbeddingBase, number_of_gpus: int, grad_bits: int, group) -> None:
-    if m.grad_mode != "dp":
-        raise ValueError("grad_update_parallel_comm needs embedding modules built with grad_mode='dp'")
-    if m._pending is None:
-        return  # no backward since the last update: nothing to communicate
-    if _world(group) != number_of_gpus:
-        raise ValueError(f"number_of_gpus={number_of_gpus} but the process group has {_world(group)} ranks")
-    batch, dy, ste, layout = m._pending
-    ex = _ensure_exchange(m, grad_bits, group)
-    s_avg = ex.exchange(batch, dy, ste=ste, layout=layout)
-    if grad_bits != 32:
-        m.emb_scaling_factor.copy_(s_avg.view_as(m.emb_scaling_factor))
-    m._pending = None
-    m._ready = grad_bits
+def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group) -> MultiSetExchange:
+    """The model's one exchange over all its embedding modules (cached; rebuilt when the
+    modules, bits, group or a batch beyond the planned lookups change). The modules' table
+    sets share one device error word so one read per step covers them all."""
+    need = [max(m._pending[0].max_lookups if m._pending is not None else 1, 1) for m in mods]
+    key = (tuple(id(m._tset) for m in mods), grad_bits, id(group), _world(group))
+    ex = getattr(model, "_dqrm_emb_exchange", None)
+    if ex is None or ex[0] != key or any(n > c for n, c in zip(need, ex[1].max_lookups)):
+        caps = need if ex is None or ex[0] != key else [max(n, c) for n, c in zip(need, ex[1].max_lookups)]
+        ex = (key, MultiSetExchange([m._tset for m in mods], caps, grad_bits=grad_bits, group=group,
+                                    device=mods[0]._tset.device))
+        model._dqrm_emb_exchange = ex
+        word = mods[0]._tset.err
+        for m in mods[1:]:
+            m._tset.share_error_word(word)
+    return ex[1]
+
+
+def _check_device_errors(model, mods: list[_QuantEmbeddingBase]) -> None:
+    """Raise if any kernel of this step flagged bad input (out-of-range index or offset,
+    understated max_lookups): the reference would have raised in ATen instead of training
+    on. One read (host sync) per distinct error word."""
+    if not error_check_due(model):
+        return
+    seen = set()
+    for m in mods:
+        ptr = m._tset.err.data_ptr()
+        if ptr in seen:
+            continue
+        seen.add(ptr)
+        raise_device_errors(m._tset.read_errors())
 
 
 def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, num_bits=16, ranking_range=False,
@@ -97,8 +132,8 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
     if emb_grad_quantized and not ranking_range and not 2 <= int(num_bits) <= 16:
         raise ValueError("num_bits must be in 2..16 for quantized embedding gradients")
     with torch.no_grad():
-        for m in _emb_modules(model):
-            if ranking_range and emb_grad_quantized:  # :280-301, per-table bits from grad_precision_and_scale
+        if ranking_range and emb_grad_quantized:  # :280-301, per-table bits from grad_precision_and_scale
+            for m in _emb_modules(model):
                 if m._pending is None:
                     continue
                 if m._rr is None:
@@ -106,8 +141,24 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
                                        "(dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1897-1898)")
                 m._exchange.exchange_ranked(m._rr[1], m._rr[2])
                 m._ready = "ranked"
-            else:
-                _exchange_module(m, number_of_gpus, int(num_bits) if emb_grad_quantized else 32, group)
+        else:
+            mods = _emb_modules(model)
+            for m in mods:
+                if m.grad_mode != "dp":
+                    raise ValueError("grad_update_parallel_comm needs embedding modules built with grad_mode='dp'")
+            if any(m._pending is not None for m in mods):
+                if _world(group) != number_of_gpus:
+                    raise ValueError(f"number_of_gpus={number_of_gpus} but the process group has "
+                                     f"{_world(group)} ranks")
+                bits = int(num_bits) if emb_grad_quantized else 32
+                ex = _emb_exchange(model, mods, bits, group)
+                s_avg = ex.exchange([m._pending for m in mods])
+                for m, s in zip(mods, s_avg):
+                    if bits != 32:
+                        m.emb_scaling_factor.copy_(s.view_as(m.emb_scaling_factor))
+                    m._pending = None
+                    m._ready = bits
+                model._dqrm_emb_ready = (ex, bits, mods)
         _mlp_grad_update(model, number_of_gpus, mlp_layer_quantized, group)
 
 
@@ -147,7 +198,19 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
     if use_ec:
         raise NotImplementedError("error compensation (use_ec) is off in the reference's scripts and not built")
     with torch.no_grad():
-        for m in _emb_modules(model):
+        mods = _emb_modules(model)
+        batched = getattr(model, "_dqrm_emb_ready", None)
+        if batched is not None:  # the one exchange of grad_update_parallel_comm (:601-628)
+            ex, bits, bmods = batched
+            if (bits != 32) != bool(emb_grad_quantized):
+                raise ValueError("emb_grad_quantized differs from the one used by grad_update_parallel_comm")
+            if update_embedding:
+                ex.apply(lr, mode=L.DQRM_UPD_DP if bits != 32 else L.DQRM_UPD_FP32,
+                         repack=[m._use_packed(False) for m in bmods])
+            for m in bmods:
+                m._ready = None
+            model._dqrm_emb_ready = None
+        for m in mods:
             ready = getattr(m, "_ready", None)
             if ready is None:
                 continue
@@ -165,13 +228,7 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
                 m._pending = None
                 m._ready = None
                 m._rr = None
-                continue
-            if update_embedding:
-                if (ready != 32) != bool(emb_grad_quantized):
-                    raise ValueError("emb_grad_quantized differs from the one used by grad_update_parallel_comm")
-                mode = L.DQRM_UPD_DP if ready != 32 else L.DQRM_UPD_FP32
-                m._exchange.apply(lr, mode=mode, repack=m._use_packed(False))
-            m._ready = None
+        _check_device_errors(model, mods)
         ex = getattr(model, "_dqrm_dense_ready", None)
         if ex is not None:  # MLP branch (:630-668), one libdqrm launch for all layers
             if (ex.grad_bits != 32) != bool(mlp_layer_quantized):
@@ -182,6 +239,7 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
 
 def clear_gradients(model) -> None:
     """s_q_g_p_c.py:714-734, plus dropping any not-yet-exchanged embedding gradient."""
+    model._dqrm_emb_ready = None
     with torch.no_grad():
         for _, param in model.named_parameters():
             if param.grad is not None:
@@ -212,7 +270,7 @@ def weight_syncc(dlrm, num_gpus, group=None) -> None:
             for m in _emb_modules(dlrm):
                 m._tset.refresh_absmax()
                 if m._tset.packed is not None:
-                    m._tset.refresh_scale_and_pack(m.embedding_bit)
+                    m._tset.repack_all(m.embedding_bit)
 
 
 def quantized_gradients_update(model, arg, lr, num_gpus) -> None:
@@ -299,4 +357,5 @@ def grad_precision_and_scale(model, number_of_gpus, rank_for_debug=None, output_
 grad_upduate_parallel_comm = grad_update_parallel_comm
 
 __all__ = ["grad_update_parallel_comm", "grad_upduate_parallel_comm", "weight_update_parallel_comm",
-           "clear_gradients", "weight_syncc", "quantized_gradients_update", "grad_precision_and_scale"]
+           "clear_gradients", "weight_syncc", "quantized_gradients_update", "grad_precision_and_scale",
+           "set_mlp_plain_linear", "set_error_check_interval"]

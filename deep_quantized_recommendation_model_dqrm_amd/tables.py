@@ -193,11 +193,30 @@ class EmbeddingTableSet:
         """Recompute the |W| max hierarchy from W (after any external write to W)."""
         L.check(self.lib.dqrm_refresh_absmax(C.byref(self._c), _stream_handle()), "dqrm_refresh_absmax")
 
+    def repack_all(self, bits: int = 4) -> None:
+        """After W was rewritten outside the kernels (weight_syncc, load_state_dict): new
+        scales from the |W| hierarchy and EVERY table's INT4 rows repacked (a table whose
+        scale happens not to move still has new rows)."""
+        self.pscale.fill_(float("nan"))
+        self.refresh_scale_and_pack(bits)
+
     def refresh_scale_and_pack(self, bits: int = 4) -> None:
         L.check(
             self.lib.dqrm_refresh_scale_and_pack(C.byref(self._c), bits, _stream_handle()),
             "dqrm_refresh_scale_and_pack",
         )
+
+    def share_error_word(self, word: torch.Tensor) -> None:
+        """Raise this set's device error flags into `word` (int32 [1] on the same device)
+        from the next call on, so one read covers several sets (the DP hooks over a
+        ModuleList of per-table modules read one word per step). Pending flags carry over."""
+        if word.dtype != torch.int32 or word.numel() != 1 or word.device != self.err.device:
+            raise ValueError("the shared error word must be one int32 on the set's device")
+        if word.data_ptr() == self.err.data_ptr():
+            return
+        word.bitwise_or_(self.err)
+        self.err = word
+        self._c.err = _ptr(word)
 
     def read_errors(self, clear: bool = True) -> int:
         f = C.c_uint32(0)
@@ -300,6 +319,29 @@ class EmbeddingTableSet:
             "dqrm_emb_local_update",
         )
 
+    def rows_changed(self, rows: torch.Tensor, repack: bool = False) -> None:
+        """Rows (slab ids, device i64) rewritten outside the kernels, e.g. by torch.optim.SGD
+        on the lookup_grad COO: refresh their maxima in the |W| hierarchy (and INT4 rows)."""
+        rows = rows.to(device=self.device, dtype=torch.int64).contiguous()
+        L.check(self.lib.dqrm_rows_changed(C.byref(self._c), _ptr(rows), rows.numel(), 4 if repack else 0,
+                                           _stream_handle()), "dqrm_rows_changed")
+
+    def lookup_grad(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True,
+                    layout: str = "tbd") -> tuple[torch.Tensor, torch.Tensor]:
+        """Uncoalesced per-lookup sparse gradient (dqrm_emb_bwd_lookup_grad): slab rows
+        i64 [L] and STE'd dy rows f32 [L, D], in lookup order -- the COO that
+        nn.EmbeddingBag(sparse=True)'s backward yields."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        Lk = int(batch.idx.numel())
+        rows = torch.empty(Lk, dtype=torch.int64, device=self.device)
+        vals = torch.empty(Lk, self.D, dtype=torch.float32, device=self.device)
+        L.check(
+            self.lib.dqrm_emb_bwd_lookup_grad(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
+                                              _ptr(rows), _ptr(vals), _stream_handle()),
+            "dqrm_emb_bwd_lookup_grad",
+        )
+        return rows, vals
+
     def backward_coalesce(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad",
                           ste: bool = True, layout: str = "tbd") -> None:
         """STE + sparse backward + coalesce + per-slot max |grad| (s_q_g_p_c.py:850-861)."""
@@ -339,17 +381,23 @@ class CoalescedGrad:
     absmax: torch.Tensor         # f32 [T*S]
 
     @classmethod
-    def allocate(cls, num_rows: Sequence[int], max_lookups: int, dim: int, device) -> "CoalescedGrad":
+    def allocate(cls, num_rows: Sequence[int], max_lookups: int, dim: int, device,
+                 absmax: torch.Tensor | None = None) -> "CoalescedGrad":
+        """absmax: caller-owned f32 [T*S] view to write the per-slot maxima into (a slice of
+        a buffer several sets gather together), else allocated here."""
         base = slot_caps(num_rows, max_lookups)
         W = base[-1]
         TS = len(num_rows) * L.DQRM_TABLE_SPLIT
+        if absmax is not None and (absmax.numel() != TS or absmax.dtype != torch.float32
+                                   or not absmax.is_contiguous()):
+            raise ValueError("absmax must be a contiguous f32 [T*S] tensor")
         return cls(
             slot_base=base,
             slot_cap_base=torch.tensor(base, dtype=torch.int64, device=device),
             rows=torch.zeros(max(W, 1), dtype=torch.int32, device=device),
             vals=torch.zeros(max(W, 1), dim, dtype=torch.float32, device=device),
             ucount=torch.zeros(TS, dtype=torch.int32, device=device),
-            absmax=torch.zeros(TS, dtype=torch.float32, device=device),
+            absmax=absmax if absmax is not None else torch.zeros(TS, dtype=torch.float32, device=device),
         )
 
     @property

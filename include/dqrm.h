@@ -203,6 +203,25 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
                           int32_t* ws_ucount, float* ws_absmax, void* workspace, size_t workspace_bytes,
                           void* stream);
 
+/* Per-lookup (uncoalesced) sparse gradient, the COO nn.EmbeddingBag(mode="sum",
+ * sparse=True) produces (embedding_bag_backward, sparse branch): for every lookup j of
+ * table t, in lookup order, rows[j] = row_base[t] + idx[j] (slab row) and
+ * vals[j][:] = (dy[t, bag(j)] * s_t) / s_t (ste != 0, quant_utils.py:349-363; s_t =
+ * set->scale[t], the forward's scale) or dy[t, bag(j)]. j runs over the batch's flat
+ * lookup positions (idx_base). The grad_mode="sparse" module hands this to
+ * torch.optim.SGD (dlrm_s_pytorch_single_gpu.py:1943-1950), which then adds lookup by
+ * lookup as with the reference's own embedding grad. rows i64 [L], vals f32 [L][D]. */
+int dqrm_emb_bwd_lookup_grad(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                             int64_t dy_stride_t, int64_t dy_stride_b, int ste, int64_t* rows, float* vals,
+                             void* stream);
+
+/* Rows of W rewritten outside libdqrm -- torch.optim.SGD stepping on the
+ * dqrm_emb_bwd_lookup_grad COO: recompute their row maxima, re-reduce their blocks,
+ * superblocks and table maxima (the next refreshing forward's scale is then the full-table
+ * max again, quant_utils.py:141-194) and, repack_bits == 4, repack their INT4 rows with the
+ * frozen packing scale. rows: slab rows (device i64 [n], duplicates allowed). */
+int dqrm_rows_changed(const dqrm_table_set* set, const int64_t* rows, int64_t n, int repack_bits, void* stream);
+
 /* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
  *   [counts i32 T*S | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
  *   int8 (bits<=8) / int16 (bits<=16) / f32 (bits==32, unquantized path)]
@@ -224,6 +243,16 @@ int dqrm_grad_quant_pack(int num_tables, int dim, const int64_t* ws_cap_base, in
                          const float* absmax_all, int num_ranks, int grad_bits,
                          const int64_t* cap_base, int64_t cap_total, float* s_avg, void* payload,
                          void* stream);
+
+/* dqrm_grad_quant_pack with the ranks' max|grad| rows absmax_pitch floats apart
+ * (absmax_all[r * absmax_pitch + t*S + s]; >= T*S): one all-gather of several table sets'
+ * concatenated ws_absmax serves every set (the DP hooks over a ModuleList of per-table
+ * modules, sgd_quantized_gradients_parallel_comm.py). payload 16-B aligned. */
+int dqrm_grad_quant_pack_strided(int num_tables, int dim, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                                 const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
+                                 const float* absmax_all, int64_t absmax_pitch, int num_ranks, int grad_bits,
+                                 const int64_t* cap_base, int64_t cap_total, float* s_avg, void* payload,
+                                 void* stream);
 
 /* Ranking-range mixed-precision gradients (grad_precision_and_scale
  * s_q_g_p_c.py:158-255 decides a bit width per table: 0, 8 or 32). Quantize-pack with a
@@ -261,6 +290,14 @@ int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base,
                              int64_t cap_total, const void* payloads, size_t payload_bytes,
                              int num_ranks, int grad_bits, const float* s_avg, float lr,
                              int mode, int repack_bits, void* stream);
+
+/* dqrm_apply_sparse_update with rank r's payload at payloads + r * rank_pitch
+ * (rank_pitch >= payload_bytes, multiple of 16): one all-gather of several sets'
+ * concatenated payloads, each set decoding its own column of the gathered buffer. */
+int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                                     const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
+                                     int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
+                                     void* stream);
 
 /* Single-rank DP step (num_ranks == 1, mode DQRM_UPD_DP), dqrm_grad_quant_pack and
  * dqrm_apply_sparse_update fused: the table scale s = clamp(max_s ws_absmax[t*S+s], 1e-8)

@@ -33,15 +33,71 @@ def test_workload_shapes(bench):
         assert top[0] == D + T * (T + 1) // 2
 
 
-def test_pmc_traffic_reads_committed_summary(bench):
-    path = os.path.join(ROOT, "profiles", "r1_tb_summary.json")
-    if not os.path.exists(path):
-        pytest.skip("no committed TB PMC summary")
-    t = bench.pmc_traffic(path, "bwd_coalesce", 64)
-    assert t is not None and t["bytes"] > 0 and t["profiled_avg_us"] > 0
-    assert t["source"] == os.path.join("profiles", "r1_tb_summary.json")
-    assert bench.pmc_traffic(os.path.join(ROOT, "profiles", "missing.json"), "bwd_coalesce", 64) is None
+def test_pmc_traffic_lookup(bench, tmp_path):
+    """roofline.traffic comes from a tools/prof_summary.py summary: the phase's kernel is
+    matched by its template prefix (LPR = D/4), absent files or kernels give None."""
+    summ = {"kernels": {
+        "k_bwd_fused<16, 1>(FArgs)": {"avg_us": 25.5, "hbm_bytes_per_launch": 4.5e7},
+        "k_bwd_fused<16, 0>(FArgs)": {"avg_us": 50.0, "hbm_bytes_per_launch": 9.0e7},
+        "k_emb_fwd<4, 2>(FwdArgs)": {"avg_us": 9.0, "hbm_bytes_per_launch": None},
+    }}
+    path = tmp_path / "s.json"
+    path.write_text(json.dumps(summ))
+    t = bench.pmc_traffic(str(path), "bwd_coalesce", 64)
+    assert t["bytes"] == 45_000_000 and t["profiled_avg_us"] == 25.5
+    assert bench.pmc_traffic(str(path), "bwd_sgd", 64)["bytes"] == 90_000_000
+    assert bench.pmc_traffic(str(path), "bwd_coalesce", 16) is None  # LPR 4 not profiled
+    assert bench.pmc_traffic(str(path), "emb_fwd", 16) is None  # no PMC pass for it
+    assert bench.pmc_traffic(str(tmp_path / "missing.json"), "bwd_coalesce", 64) is None
     assert bench.pmc_traffic(None, "bwd_coalesce", 64) is None
+    for name in sorted(os.listdir(os.path.join(ROOT, "profiles"))):  # committed summaries parse
+        if name.startswith("r2_") and name.endswith("_summary.json"):
+            for ph in bench.KERNEL_SYMBOL:
+                bench.pmc_traffic(os.path.join(ROOT, "profiles", name), ph, 64)
+
+
+def test_alg_bytes_pooling_one_reads_no_offsets(bench):
+    T, B, D, U = 26, 2048, 64, 40000
+    L = T * B
+    assert bench.alg_bytes("bwd_coalesce", T, B, D, U) == L * 8 + L * D * 4 + U * (D * 4 + 4)
+    assert bench.alg_bytes("bwd_coalesce", T, B, D, U, pool1=False) - bench.alg_bytes(
+        "bwd_coalesce", T, B, D, U) == T * B * 8
+    assert bench.alg_bytes("emb_fwd_packed", T, B, D, U) == L * (D // 2 + 8) + L * D * 4 + T * 4
+    assert bench.alg_bytes("apply_local", T, B, D, U, repack=True) - bench.alg_bytes(
+        "apply_local", T, B, D, U) == U * D // 2
+    assert bench.alg_bytes("apply_sparse_update", T, B, D, U, world=8) > bench.alg_bytes(
+        "apply_sparse_update", T, B, D, U, world=1)
+    assert set(bench.KERNEL_SYMBOL) >= {n for m in ("dp", "fwd", "sgd") for f in (True, False)
+                                        for n in bench.phase_names(m, f, f)}
+
+
+def test_phase_names(bench):
+    assert bench.phase_names("fwd", False, True) == ["emb_fwd"]
+    assert bench.phase_names("sgd", True, True) == ["emb_fwd_packed", "bwd_sgd"]
+    assert bench.phase_names("dp", False, True) == ["emb_fwd", "bwd_coalesce", "apply_local"]
+    assert bench.phase_names("dp", False, False) == ["emb_fwd", "bwd_coalesce", "grad_quant_pack",
+                                                     "apply_sparse_update"]
+
+
+@pytest.mark.parametrize("mode", ["dp", "sgd", "fwd"])
+def test_cpu_baseline_torch_runs(bench, mode):
+    """The PyTorch-CPU restatement of the reference step runs on small tables and reports
+    the threads it used."""
+    a = bench.parse(["--mode", mode, "--cpu-seconds", "0.2", "--config", "kaggle"])
+    r = bench.cpu_baseline_torch(a, 64, rows_override=[100, 7, 3000])
+    assert r["value"] > 0 and r["cores"] == bench.cpu_threads() and r["kind"] == "port"
+    assert r["unit"] == "samples/s" and mode in r["sample"]
+
+
+def test_fake_quant_ste_matches_reference_form(bench):
+    import torch
+
+    x = torch.tensor([0.0, 0.05, -0.3, 1.0, -1.0, 0.149], requires_grad=True)
+    s = torch.tensor(0.1)
+    y = bench._FakeQuantSTE.apply(x, s, 4)
+    assert torch.equal(y, torch.clamp(torch.round(1.0 / s * x.detach()), -8, 7) * s)
+    y.backward(torch.full_like(y, 0.3))
+    assert torch.equal(x.grad, (torch.full_like(y, 0.3) * s) / s)
 
 
 def test_committed_bench_line_fields():
@@ -64,3 +120,10 @@ def test_multi_gpu_needs_distributed_launcher():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "torch.distributed.run" in p.stderr
+
+
+def test_bench_rejects_inconsistent_flags():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--use-packed"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2 and "--scale-period" in p.stderr

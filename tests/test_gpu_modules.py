@@ -26,6 +26,17 @@ def dq():
     return d
 
 
+@pytest.fixture(autouse=True)
+def plain_linear_mlp():
+    """The tiny models below use plain nn.Linear MLP layers; opt them into the MLP exchange
+    (the reference itself exchanges only QuantLinear layers)."""
+    from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+
+    H.set_mlp_plain_linear(True)
+    yield
+    H.set_mlp_plain_linear(False)
+
+
 def _qebt(n, D, W, **kw):
     from deep_quantized_recommendation_model_dqrm_amd.quant_modules_not_quantize_grad import QuantEmbeddingBagTwo
 
@@ -46,11 +57,16 @@ def test_quant_embedding_bag_two_forward_and_sparse_grad(dq):
     dy = G.upstream_grad(1, len(off), D, 5)[0]
     y.backward(torch.from_numpy(dy).cuda())
     g = m.embedding_bag.weight.grad
-    assert g.is_sparse
-    g = g.coalesce()  # already unique + sorted: a no-op on the values
+    # nn.EmbeddingBag(sparse=True)'s form: one entry per lookup, in lookup order, the
+    # STE'd gradient row of its bag (uncoalesced)
+    assert g.is_sparse and not g.is_coalesced()
+    bag = np.repeat(np.arange(len(off)), np.diff(np.append(off, len(idx))))
+    np.testing.assert_array_equal(g._indices()[0].cpu().numpy(), idx)
+    np.testing.assert_array_equal(g._values().cpu().numpy(), ((dy * f32(s)) / f32(s))[bag])
     r_o, v_o, _ = O.emb_bwd_coalesce(n, idx, off, dy, s)
-    np.testing.assert_array_equal(g.indices()[0].cpu().numpy(), r_o)
-    np.testing.assert_array_equal(g.values().cpu().numpy(), v_o)
+    gc = g.coalesce()  # ATen's coalesce: same rows, sums in its own order
+    np.testing.assert_array_equal(gc.indices()[0].cpu().numpy(), r_o)
+    np.testing.assert_allclose(gc.values().cpu().numpy(), v_o, rtol=0, atol=1e-6)
     # test_mode reuses the training scale; full precision is the plain bag sum
     y_t = m(x, o, test_mode=True)
     np.testing.assert_array_equal(y_t.detach().cpu().numpy(), y_o)
@@ -62,6 +78,44 @@ def test_quant_embedding_bag_two_forward_and_sparse_grad(dq):
                  "iteration_bound", "iteration_nt"):
         assert hasattr(m, name)
     assert m.embedding_bag.weight.shape == (n, D)
+
+
+def test_sparse_grad_sgd_step_matches_kaggle_pool1(dq, golden_dir):
+    """The single-GPU driver unchanged (dlrm_s_pytorch_single_gpu.py:1943-1950): 26
+    QuantEmbeddingBagTwo(grad_mode="sparse") + torch.optim.SGD(lr=0.1).step() on their
+    uncoalesced grads, against kaggle_pool1.npz (the reference's modules + SGD in torch-CPU).
+    The first forward is bit-exact. W: ATen-ROCm's sparse add (index_add_ of alpha * value)
+    and torch-CPU's per-lookup add round differently, so W (|W| <= 0.58 here) and the
+    later forwards, whose table scale follows max|W|, are held to 1e-6 absolute (most
+    elements agree to the bit). The |W| maxima follow ATen's writes (dqrm_rows_changed)."""
+    import os
+    from test_oracle_golden import regen_single
+
+    fx = dict(np.load(os.path.join(golden_dir, "kaggle_pool1.npz")))
+    Ws, batches, dys = regen_single(fx)
+    mods = nn.ModuleList([_qebt(w.shape[0], w.shape[1], w, grad_mode="sparse") for w in Ws])
+    opt = torch.optim.SGD([m.embedding_bag.weight for m in mods], lr=float(fx["lr"]))
+    for k, ((idxs, offs), dy) in enumerate(zip(batches, dys)):
+        opt.zero_grad()
+        ys = [m(torch.from_numpy(i).cuda(), torch.from_numpy(o).cuda()) for m, i, o in zip(mods, idxs, offs)]
+        for t, (m, y) in enumerate(zip(mods, ys)):
+            if k == 0:  # from the fixture's own tables: bit-exact
+                np.testing.assert_array_equal(y.detach().cpu().numpy(), fx[f"y{k}"][t])
+                assert m.eb_scaling_factor.item() == fx[f"s{k}"][t]
+            else:  # after ATen's update (see above): the table max, hence the scale, within 1e-6
+                np.testing.assert_allclose(y.detach().cpu().numpy(), fx[f"y{k}"][t], rtol=0, atol=1e-6)
+                np.testing.assert_allclose(m.eb_scaling_factor.item(), fx[f"s{k}"][t], rtol=1e-6)
+        torch.autograd.backward(ys, [torch.from_numpy(dy[t]).cuda() for t in range(len(ys))])
+        opt.step()
+    exact = total = 0
+    for t, m in enumerate(mods):
+        rows = fx[f"rows_t{t}"]
+        got = m.embedding_bag.weight.detach().cpu().numpy()[rows]
+        np.testing.assert_allclose(got, fx[f"w_t{t}"], rtol=0, atol=1e-6)
+        exact += int((got == fx[f"w_t{t}"]).sum())
+        total += got.size
+    assert exact > total // 2  # most elements still agree to the bit
+    assert all(m._tset.read_errors() == 0 for m in mods)
 
 
 def test_quant_embedding_bag_two_fused_sgd(dq):
@@ -151,6 +205,83 @@ def test_dp_hooks_single_rank_match_oracle(dq, emb_q, mlp_q):
     for t in range(len(rows)):
         np.testing.assert_array_equal(model.emb_l.table_weight(t).detach().cpu().numpy(), Wo[t])
     assert model.emb_l._tset.read_errors() == 0
+
+
+class ListDLRM(nn.Module):
+    """The unchanged DP driver's model: emb_l = nn.ModuleList of one QuantEmbeddingBagTwo
+    per table (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:380), apply_emb's per-table loop."""
+
+    def __init__(self, rows, D, Ws, **kw):
+        super().__init__()
+        self.emb_l = nn.ModuleList([_qebt(n, D, W, grad_mode="dp", **kw) for n, W in zip(rows, Ws)])
+        self.bot_l = nn.Sequential(nn.Linear(13, D), nn.ReLU()).cuda()
+        self.top_l = nn.Sequential(nn.Linear(D * (len(rows) + 1), 1)).cuda()
+
+    def forward(self, dense, lS_o, lS_i):
+        x = self.bot_l(dense)
+        ly = [e(lS_i[t], lS_o[t]) for t, e in enumerate(self.emb_l)]
+        return self.top_l(torch.cat([x] + ly, dim=1))
+
+
+@pytest.mark.parametrize("emb_q", [True, False])
+def test_dp_hooks_over_module_list_of_26_tables(dq, emb_q):
+    """grad_update / weight_update_parallel_comm over a ModuleList of 26 single-table
+    modules run ONE exchange for all of them (one MultiSetExchange: 2 collectives/step at
+    N>1) and match oracle.dp_step table by table; emb_scaling_factor per module."""
+    from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+
+    rows, D, B = [min(n, 20000) for n in G.KAGGLE_ROWS], 16, 128
+    Ws = G.table_weights(rows, D, 61)
+    torch.manual_seed(0)
+    model = ListDLRM(rows, D, Ws)
+    Wo = [w.copy() for w in Ws]
+    for k in range(2):
+        P = G.pooling_one(rows, B, 62 + k, dist="zipf" if k else "uniform")
+        lS_i = torch.from_numpy(P).cuda()
+        lS_o = torch.arange(B, device="cuda").repeat(len(rows), 1)
+        H.clear_gradients(model)
+        s_fwd = [O.table_scale(w, 4) for w in Wo]
+        model(torch.rand(B, 13, device="cuda"), lS_o, lS_i).pow(2).mean().backward()
+        dy_np = [m._pending[1].detach().cpu().numpy()[0] for m in model.emb_l]
+        H.grad_update_parallel_comm(model, 1, emb_grad_quantized=emb_q, num_bits=8)
+        H.weight_update_parallel_comm(model, 0.1, emb_grad_quantized=emb_q, num_gpus=1)
+        res = O.dp_step(Wo, [[(P[t], np.arange(B)) for t in range(len(rows))]], [dy_np], s_fwd, 0.1,
+                        grad_bits=8 if emb_q else 32)
+        if emb_q:
+            for t, m in enumerate(model.emb_l):
+                assert m.emb_scaling_factor.item() == res[t][0]
+    ex = model._dqrm_emb_exchange[1]
+    assert len(ex.parts) == len(rows)  # one exchange object for all 26 modules
+    assert len({m._tset.err.data_ptr() for m in model.emb_l}) == 1  # one error word, one read per step
+    for t, m in enumerate(model.emb_l):
+        np.testing.assert_array_equal(m.embedding_bag.weight.detach().cpu().numpy(), Wo[t])
+        inc = m._tset.tmax.clone()
+        m._tset.refresh_absmax()
+        assert torch.equal(inc, m._tset.tmax)
+
+
+def test_hooks_and_modules_raise_on_device_errors(dq):
+    """An out-of-range index is flagged by the kernels and surfaces as DQRMError: from
+    weight_update_parallel_comm for grad_mode="dp", from the next training call for the
+    single-GPU modes (ATen raises on such input; nothing trains on silently)."""
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+
+    rows, D, B = [10, 300], 16, 64
+    Ws = G.table_weights(rows, D, 71)
+    model = ListDLRM(rows, D, Ws)
+    P = G.pooling_one(rows, B, 72)
+    P[1, 5] = 300  # one past the end of table 1
+    lS_o = torch.arange(B, device="cuda").repeat(len(rows), 1)
+    model(torch.rand(B, 13, device="cuda"), lS_o, torch.from_numpy(P).cuda()).sum().backward()
+    H.grad_update_parallel_comm(model, 1, num_bits=8)
+    with pytest.raises(L.DQRMError, match="0x1"):
+        H.weight_update_parallel_comm(model, 0.1, num_gpus=1)
+    m = _qebt(rows[1], D, Ws[1], grad_mode="fused_sgd", lr=0.1)
+    x, off = torch.from_numpy(P[1]).cuda(), torch.arange(B, device="cuda")
+    m(x, off).sum().backward()
+    with pytest.raises(L.DQRMError):
+        m(x, off)
 
 
 def test_weight_syncc_single_rank_is_identity(dq):

@@ -103,3 +103,71 @@ def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits):
         for j, (W, b) in enumerate(params):
             np.testing.assert_array_equal(got[f"W{j}"], W)
             np.testing.assert_array_equal(got[f"b{j}"], b)
+
+
+SYNC_ROWS, SYNC_D = [5, 300, 20000], 16
+
+
+def _sync_rank(rank, world, port, out_dir):
+    sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gen_inputs as G
+        from torch import nn
+        from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+        from deep_quantized_recommendation_model_dqrm_amd.quant_modules_not_quantize_grad import (
+            QuantEmbeddingBagCollection)
+
+        torch.cuda.set_device(0)
+        torch.manual_seed(rank)  # each rank starts from its own tables and MLP, as the
+        # reference's ranks do before the first weight_syncc (dp_one_parallel_comm.py:1801)
+        model = nn.Module()
+        Ws = G.table_weights(SYNC_ROWS, SYNC_D, 300 + rank)
+        model.emb_l = QuantEmbeddingBagCollection(SYNC_ROWS, SYNC_D, weights=[torch.from_numpy(w) for w in Ws],
+                                                  grad_mode="dp", use_packed_int4=True)
+        model.emb_l._tset.refresh_scale_and_pack(4)
+        model.bot_l = nn.Sequential(nn.Linear(13, SYNC_D)).cuda()
+        model.top_l = nn.Sequential(nn.Linear(SYNC_D, 1)).cuda()
+        before = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+        H.weight_syncc(model, world)
+        ts = model.emb_l._tset
+        inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+        ts.refresh_absmax()
+        hier_ok = all(torch.equal(a, b) for a, b in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)))
+        after = {n: p.detach().cpu().numpy() for n, p in model.named_parameters()}
+        np.savez(os.path.join(out_dir, f"s{rank}.npz"), hier_ok=np.array(hier_ok), packed=ts.packed.cpu().numpy(),
+                 scale=ts.scale.cpu().numpy(), **{"b_" + k: v for k, v in before.items()},
+                 **{"a_" + k: v for k, v in after.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_weight_syncc_two_ranks_different_tables(tmp_path):
+    """weight_syncc at N=2 with each rank starting from different tables and MLP weights
+    (s_q_g_p_c.py:963-970): every parameter becomes the fp32 rank-ordered mean
+    (all_reduce SUM, then * 1/N) on both ranks, the |W| hierarchy equals a rebuild, and the
+    INT4 rows are repacked with the new table scales."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import oracle as O
+
+    world = 2
+    mp.spawn(_sync_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [dict(np.load(os.path.join(tmp_path, f"s{r}.npz"))) for r in range(world)]
+    names = [k[2:] for k in got[0] if k.startswith("b_")]
+    assert "emb_l.embedding_bag.weight" in names and len(names) >= 5
+    for n in names:
+        mean = ((got[0]["b_" + n] + got[1]["b_" + n]).astype(np.float32) * np.float32(1.0 / world)).astype(np.float32)
+        assert not np.array_equal(got[0]["b_" + n], got[1]["b_" + n]), n  # the ranks really started apart
+        for r in range(world):
+            np.testing.assert_array_equal(got[r]["a_" + n], mean, err_msg=n)
+    W = got[0]["a_emb_l.embedding_bag.weight"]
+    base = np.concatenate([[0], np.cumsum(SYNC_ROWS)])
+    for r in range(world):
+        assert bool(got[r]["hier_ok"])
+        for t in range(len(SYNC_ROWS)):
+            Wt = W[base[t]: base[t + 1]]
+            s = O.table_scale(Wt, 4)
+            assert got[r]["scale"][t] == s
+            np.testing.assert_array_equal(got[r]["packed"][base[t]: base[t + 1]], O.pack_int4(Wt, s))
