@@ -14,8 +14,10 @@ import sys
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
-SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_dense.hip", "dqrm_input.hip")]
+SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_coalesce.hip", "dqrm_dense.hip",
+                                                "dqrm_input.hip")]
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
+INTERNAL_HEADER = os.path.join(CSRC_DIR, "dqrm_internal.h")
 LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
 
 HIPCC_FLAGS = [
@@ -47,7 +49,7 @@ def _stale(out: str, deps) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(LIB_PATH, [*SOURCES, HEADER, __file__])
+    return _stale(LIB_PATH, [*SOURCES, HEADER, INTERNAL_HEADER, __file__])
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -58,7 +60,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     objs = []
     for src in SOURCES:
         obj = _obj(src)
-        if force or _stale(obj, [src, HEADER, __file__]):
+        if force or _stale(obj, [src, HEADER, INTERNAL_HEADER, __file__]):
             tmp = obj + ".tmp.o"
             cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-c", src, "-o", tmp]
             if verbose:

@@ -38,6 +38,8 @@ DQRM_UPD_FP32 = 2
 DQRM_APPLY_AUTO = 0
 DQRM_APPLY_FLAT = 1
 DQRM_APPLY_SLOT = 2
+DQRM_COALESCE_AUTO = 0
+DQRM_COALESCE_GENERAL = 1
 
 DQRM_CRITEO_RECORD_INTS = 40
 DQRM_CRITEO_DENSE = 13
@@ -81,6 +83,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_read_errors",
     "dqrm_last_error",
     "dqrm_set_apply_kernel",
+    "dqrm_set_coalesce_kernel",
     "dqrm_abi_version",
 )
 
@@ -224,6 +227,7 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
         "dqrm_last_error": (C.c_char_p, []),
         "dqrm_set_apply_kernel": (C.c_int, [C.c_int]),
+        "dqrm_set_coalesce_kernel": (C.c_int, [C.c_int]),
         "dqrm_abi_version": (C.c_int, []),
     }
     for name, (res, args) in sig.items():

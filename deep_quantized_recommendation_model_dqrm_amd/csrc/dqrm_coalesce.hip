@@ -1,0 +1,700 @@
+// dqrm_coalesce.hip — K4 coalesce for Criteo-form batches (gfx950).
+//
+//   STE backward        SymmetricQuantFunction.backward   quant_utils.py:349-363
+//   sparse backward     nn.EmbeddingBag(mode="sum", sparse=True), one lookup per bag
+//   grad.coalesce()     + per-table max|grad| for the local scale   s_q_g_p_c.py:859-861
+//
+// One 1024-thread workgroup per (table, row-range slot), exactly the general kernel's
+// workspace contract (include/dqrm.h, dqrm_emb_bwd_coalesce), for batches in the Criteo
+// form (DQRM_BATCH_POOLING_ONE, B <= 4096 lookups per table): bag b is lookup b, so a
+// lookup's dy row is known from its position alone. The kernel is built for latency: at
+// 2048 lookups per table every workgroup does a few hundred keys, so what costs is the
+// chain of dependent steps and the instructions each wave issues, not bandwidth.
+//   1. every thread's lookups (b = tid + 1024 i) are loaded at once; a dimension-split
+//      table (fewer than 8 row blocks: every workgroup sees all lookups and owns D/8 of
+//      the dimensions) also issues its dy slices of ALL lookups right away, so both HBM
+//      round trips overlap;
+//   2. the slot's lookups are compacted in lookup order (ballots + one 64-entry prefix),
+//      keys = (row - r0) << 32 | gather index; a row-split slot issues its dy rows now,
+//      before the sort;
+//   3. sort by row: <= 512 keys one per thread by a bitonic network (shuffles below 64,
+//      LDS above), more by a stable 8-bit LSD radix (ballot digit matching); the keys are
+//      unique and ascend with the lookup index, so either gives the reference's order:
+//      rows ascending, a row's lookups in lookup order;
+//   4. the prefetched values land in a DIMENSION-MAJOR stage at their sorted positions,
+//      and item (segment, dimension) = one lane sums its column strictly in lookup order
+//      (8 LDS reads in flight ahead of the adds), so a hot row's long chain runs at add
+//      latency and short segments cost one read. Slots too large for the stage stream it
+//      in chunks (the same lane carries a segment across chunks).
+// The code is kept small on purpose: each CU runs one workgroup once per launch, so every
+// instruction is fetched cold.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dqrm.h"
+#include "dqrm_internal.h"
+
+namespace {
+
+// Diagnostic build only (-DDQRM_DIAG_CLOCK, tools/diag_coalesce.py): thread 0 of every
+// workgroup stamps the 100 MHz wall clock at phase boundaries.
+#ifdef DQRM_DIAG_CLOCK
+__device__ unsigned long long g_coal_clk[8192 * 16];
+#define CDIAG(k) do { if (threadIdx.x == 0) g_coal_clk[blockIdx.x * 16 + (k)] = wall_clock64(); } while (0)
+#define CDIAG_W(k) do { __builtin_amdgcn_s_waitcnt(0); CDIAG(k); } while (0)
+#else
+#define CDIAG(k) do { } while (0)
+#define CDIAG_W(k) do { } while (0)
+#endif
+
+constexpr int WAVE = 64;
+constexpr int TPB = 1024;
+constexpr int NW = TPB / WAVE;
+constexpr int SPLIT = DQRM_TABLE_SPLIT;
+constexpr int BLK = DQRM_BLOCK_ROWS;
+constexpr int MAXB = (int)dqrm_internal::kCoalesceMaxB;
+constexpr int MAXI = MAXB / TPB;  // lookups per thread
+constexpr int PFR = 6;            // prefetched float4 per thread
+constexpr int DBMAX = 9;          // radix digit bits per pass (one digit per thread in the scan)
+constexpr int FIX_MAX = 64;       // largest bucket the MSD pass finishes by ranking
+constexpr int LDS_BYTES = 156 * 1024;
+// dynamic LDS: keys u64[MAXB] | while sorting: ping-pong u64[MAXB] + digit counters
+// i32[NW << DBMAX]; after it: sorted position of each lookup u16[MAXB] | segment heads
+// u16[MAXB+8] | multi-lookup segments u16[MAXB+8] | output entry of each sorted position
+// i32[MAXB] (-1: part of a multi-lookup segment) | dimension-major stage f32
+constexpr int OFF_SCR = MAXB * 8;
+constexpr int OFF_POS = OFF_SCR;
+constexpr int OFF_HPOS = OFF_POS + MAXB * 2;
+constexpr int OFF_MLIST = OFF_HPOS + (MAXB + 8) * 2;
+constexpr int OFF_SDEST = OFF_MLIST + (MAXB + 8) * 2;
+constexpr int OFF_STAGE = OFF_SDEST + MAXB * 4;
+constexpr int STAGE_FLOATS = (LDS_BYTES - OFF_STAGE) / 4;
+static_assert(OFF_STAGE % 16 == 0, "stage alignment");
+static_assert(OFF_SCR + MAXB * 8 + (NW << DBMAX) * 4 <= LDS_BYTES, "sort scratch");
+static_assert(MAXI * NW <= WAVE, "one prefix lane per (item, wave)");
+// key = (row - r0) << 32 | gather index << 12 | lookup: unique, and gather order = lookup order
+constexpr uint32_t LK_BITS = 12;
+constexpr uint32_t LK_MASK = (1u << LK_BITS) - 1u;
+static_assert(MAXB <= (1 << LK_BITS), "lookup index field");
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << (threadIdx.x % WAVE)) - 1ull; }
+__device__ __forceinline__ uint32_t krow(uint64_t x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ uint32_t kgat(uint64_t x) { return (uint32_t)x >> LK_BITS; }
+__device__ __forceinline__ uint32_t kbag(uint64_t x) { return (uint32_t)x & LK_MASK; }
+__device__ __forceinline__ float abs_max4(float4 v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
+// Items (i, tid), i < ni, in the order i * TPB + tid: the ones whose pred holds get
+// consecutive positions in that order (emit(i, position)); every item also sees the
+// position the next hit would get and whether it hit (all(i, rank, hit)). Returns the count.
+template <class Pred, class Emit, class All>
+__device__ __forceinline__ int ordered_compact(int ni, int* s_cnt, Pred pred, Emit emit, All all) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    uint64_t m[MAXI];
+#pragma unroll
+    for (int i = 0; i < MAXI; ++i) {
+        m[i] = 0;
+        if (i < ni) m[i] = __ballot(pred(i));
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i)
+            if (i < ni) s_cnt[i * NW + w] = (int)__popcll(m[i]);
+    __syncthreads();
+    const int v = lane < ni * NW ? s_cnt[lane] : 0;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int y = __shfl_up(incl, o, WAVE);
+        if (lane >= o) incl += y;
+    }
+    const int excl = incl - v;
+    const int total = __shfl(incl, WAVE - 1, WAVE);
+    const uint64_t lt = lanemask_lt();
+#pragma unroll
+    for (int i = 0; i < MAXI; ++i) {
+        const int base = __shfl(excl, (i * NW + w) & (WAVE - 1), WAVE);
+        const bool hit = (m[i] >> lane) & 1ull;
+        const int rank = base + (int)__popcll(m[i] & lt);
+        if (i < ni) {
+            if (hit) emit(i, rank);
+            all(i, rank, hit);
+        }
+    }
+    return total;
+}
+
+// exclusive prefix of one int per thread over the workgroup; *total = the sum
+__device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const int y = __shfl_up(incl, o, WAVE);
+        if (lane >= o) incl += y;
+    }
+    if (lane == WAVE - 1) s_w[w] = incl;
+    __syncthreads();
+    if (w == 0) {
+        const int x = lane < NW ? s_w[lane] : 0;
+        int y = x;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            const int z = __shfl_up(y, o, WAVE);
+            if (lane >= o) y += z;
+        }
+        if (lane < NW) s_w[lane] = y - x;
+        if (lane == NW - 1) s_w[NW] = y;
+    }
+    __syncthreads();
+    *total = s_w[NW];
+    return s_w[w] + incl - v;
+}
+
+// Stable LSD radix sort of keys[0, n) by the row field (bits [0, nbits)), passes of at
+// most DBMAX bits (a dimension-split table's rows: one pass). Wave w owns keys
+// [w*64*kpl, (w+1)*64*kpl), 64 at a time; same-digit lanes from bit-slice ballots;
+// [digit][wave] counters, one workgroup scan per pass.
+__device__ void radix_sort(uint64_t* keys, uint64_t* tmp, int* hist, int* s_w, int n, int nbits) {
+    const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
+    const int kpl = (n + TPB - 1) / TPB;
+    const int i0 = w * WAVE * kpl + lane;
+    const uint64_t lt = lanemask_lt();
+    const int passes = (nbits + DBMAX - 1) / DBMAX;
+    uint64_t* src = keys;
+    uint64_t* dst = tmp;
+    int sh = 0;
+    for (int ps = 0; ps < passes; ++ps) {
+        const int db = (nbits - sh + (passes - ps) - 1) / (passes - ps);
+        const uint32_t dm = (1u << db) - 1u;
+        const int nd = 1 << db;
+        for (int j = tid; j < (NW << db); j += TPB) hist[j] = 0;
+        __syncthreads();
+        auto peers_of = [&](uint32_t d, bool v) {
+            uint64_t m = __ballot(v);
+            for (int q = 0; q < db; ++q) {
+                const uint64_t bq = __ballot((d >> q) & 1u);
+                m &= ((d >> q) & 1u) ? bq : ~bq;
+            }
+            return m;
+        };
+        for (int kk = 0; kk < kpl; ++kk) {
+            const int i = i0 + kk * WAVE;
+            const bool v = i < n;
+            const uint32_t d = v ? (krow(src[i]) >> sh) & dm : 0u;
+            const uint64_t pm = peers_of(d, v);
+            if (v && (pm & lt) == 0) hist[w * nd + d] += (int)__popcll(pm);
+        }
+        __syncthreads();
+        {  // exclusive scan in (digit, wave) order: thread d owns digit d's NW counters
+            int c[NW];
+            int sum = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                c[q] = tid < nd ? hist[q * nd + tid] : 0;
+                sum += c[q];
+            }
+            int tot;
+            int ex = block_excl_scan(sum, s_w, &tot);
+            if (tid < nd)
+#pragma unroll
+                for (int q = 0; q < NW; ++q) {
+                    hist[q * nd + tid] = ex;
+                    ex += c[q];
+                }
+        }
+        __syncthreads();
+        for (int kk = 0; kk < kpl; ++kk) {
+            const int i = i0 + kk * WAVE;
+            const bool v = i < n;
+            const uint64_t x = v ? src[i] : 0ull;
+            const uint32_t d = (krow(x) >> sh) & dm;
+            const uint64_t pm = peers_of(d, v);
+            if (v) {
+                int* hp = hist + w * nd + d;
+                const int p = *hp + (int)__popcll(pm & lt);
+                dst[p] = x;
+                if ((pm & lt) == 0) *hp = p + (int)__popcll(pm);
+            }
+        }
+        __syncthreads();
+        uint64_t* tt = src;
+        src = dst;
+        dst = tt;
+        sh += db;
+    }
+    if (src != keys) {
+        for (int i = tid; i < n; i += TPB) keys[i] = src[i];
+        __syncthreads();
+    }
+}
+
+// Keys over a row span of more than 8 bits: one counting pass on the top 8 bits of the row
+// into 256 buckets (rank inside a bucket from an LDS atomic: any order), then every key's
+// place inside its bucket = the number of smaller keys there (the keys are unique, so this
+// is THE sorted order; a bucket is read by its own keys only, all reads independent). A
+// bucket above FIX_MAX keys (hot rows) -> radix_sort.
+__device__ void msd_sort(uint64_t* keys, uint64_t* tmp, int* hist, int* s_w, int n, int nbits) {
+    const int tid = threadIdx.x;
+    const int sh = nbits - 8;
+    int* cnt = hist;          // [256]
+    int* start = hist + 256;  // [257]
+    int* flag = hist + 520;
+    if (tid < 256) cnt[tid] = 0;
+    if (tid == 0) *flag = 0;
+    __syncthreads();
+    uint64_t x[MAXI];
+    int d[MAXI], rk[MAXI];
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j) {
+        const int i = tid + TPB * j;
+        d[j] = -1;
+        x[j] = 0;
+        rk[j] = 0;
+        if (i < n) {
+            x[j] = keys[i];
+            d[j] = (int)((krow(x[j]) >> sh) & 255u);
+            rk[j] = atomicAdd(&cnt[d[j]], 1);
+        }
+    }
+    __syncthreads();
+    const int c = tid < 256 ? cnt[tid] : 0;
+    int tot;
+    const int ex = block_excl_scan(c, s_w, &tot);
+    if (tid < 256) {
+        start[tid] = ex;
+        if (c > FIX_MAX) *flag = 1;
+    }
+    if (tid == 0) start[256] = tot;
+    __syncthreads();
+    const bool crowded = *flag != 0;
+    __syncthreads();
+    if (crowded) {
+        radix_sort(keys, tmp, hist, s_w, n, nbits);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j)
+        if (d[j] >= 0) tmp[start[d[j]] + rk[j]] = x[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MAXI; ++j)
+        if (d[j] >= 0) {
+            const int b0 = start[d[j]], b1 = start[d[j] + 1];
+            int below = 0;
+            for (int i = b0; i < b1; ++i) below += tmp[i] < x[j] ? 1 : 0;
+            keys[b0 + below] = x[j];
+        }
+    __syncthreads();
+}
+
+// row-range slot of a row (slot_rows' inverse): the largest s with floor(nblk*s/SPLIT) <= blk
+__device__ __forceinline__ int slot_of_row(int64_t row, int64_t nblk) {
+    const uint32_t blk = (uint32_t)(row >> 8), nb = (uint32_t)nblk;
+    return (int)((SPLIT * (blk + 1) + nb - 1) / nb) - 1;
+}
+
+__device__ __forceinline__ float add8(float acc, float4 x0, float4 x1) {
+    acc = acc + x0.x; acc = acc + x0.y; acc = acc + x0.z; acc = acc + x0.w;
+    acc = acc + x1.x; acc = acc + x1.y; acc = acc + x1.z; acc = acc + x1.w;
+    return acc;
+}
+
+// acc + col[p] + col[p+1] + ... + col[pe-1], strictly in order; 16-B reads, the next 8
+// values in flight while the current 8 are added (col 16-B aligned)
+__device__ __forceinline__ float chain_sum(const float* col, int p, int pe, float acc) {
+    for (; p < pe && (p & 3); ++p) acc = acc + col[p];
+    if (p + 8 <= pe) {
+        float4 x0 = *reinterpret_cast<const float4*>(col + p);
+        float4 x1 = *reinterpret_cast<const float4*>(col + p + 4);
+        p += 8;
+        while (p + 8 <= pe) {
+            const float4 y0 = *reinterpret_cast<const float4*>(col + p);
+            const float4 y1 = *reinterpret_cast<const float4*>(col + p + 4);
+            acc = add8(acc, x0, x1);
+            x0 = y0;
+            x1 = y1;
+            p += 8;
+        }
+        acc = add8(acc, x0, x1);
+    }
+    for (; p < pe; ++p) acc = acc + col[p];
+    return acc;
+}
+
+__global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int s_cnt[MAXI * NW];
+    __shared__ int s_cnt2[MAXI * NW];
+    __shared__ int s_w[NW + 1];
+    __shared__ int64_t s_cb[SPLIT + 1];
+    __shared__ int s_uf[SPLIT + 1];
+    __shared__ int s_ucnt[SPLIT];
+    __shared__ float s_red[NW];
+    uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
+    uint16_t* pos = reinterpret_cast<uint16_t*>(lds + OFF_POS);
+    uint16_t* hpos = reinterpret_cast<uint16_t*>(lds + OFF_HPOS);
+    uint16_t* mlist = reinterpret_cast<uint16_t*>(lds + OFF_MLIST);
+    int* sdest = reinterpret_cast<int*>(lds + OFF_SDEST);
+    float* stage = reinterpret_cast<float*>(lds + OFF_STAGE);
+
+    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
+    const int tid = threadIdx.x, w = tid / WAVE;
+    const int B = (int)a.B;
+    CDIAG(0);
+    // 1. the table's uniform values (scalar loads), then this thread's lookups
+    //    b = tid + TPB*i, all in flight. Every global load below is unconditional (indices
+    //    clamped), so the compiler can count them and wait for exactly the one it needs.
+    const int64_t nrows = a.meta[a.T + t];
+    const float sc = a.scale[t];
+    int64_t cbv[SPLIT + 1];
+#pragma unroll
+    for (int j = 0; j <= SPLIT; ++j) cbv[j] = a.ws_cap_base[t * SPLIT + j];
+    const int ni = (B + TPB - 1) / TPB;
+    int64_t r[MAXI];
+    const int64_t* ti = a.idx + (int64_t)t * a.B;
+#pragma unroll
+    for (int i = 0; i < MAXI; ++i) {
+        const int b = tid + TPB * i;
+        r[i] = ti[b < B ? b : B - 1];
+    }
+    const int64_t nblk = (nrows + BLK - 1) / BLK;
+    const bool dsplit = nblk < SPLIT;
+    const int LPR = a.D / 4;
+    const int DS = LPR < SPLIT ? LPR : SPLIT;
+    const int LG = dsplit ? LPR / DS : LPR;  // float4 of a row this workgroup owns
+    const int lg_sh = __ffs(LG) - 1;
+    const int SW = LG * 4;                   // dimensions this workgroup owns
+    const int sw_sh = lg_sh + 2;
+    const int q0 = dsplit ? s * LG : 0;
+    int64_t r0 = 0, r1 = nrows;
+    if (!dsplit) {
+        r0 = nblk * s / SPLIT * BLK;
+        r1 = nblk * (s + 1) / SPLIT * BLK;
+        r1 = r1 < nrows ? r1 : nrows;
+    }
+    const bool active = dsplit ? s < DS : r0 < r1;
+    const int SP = (STAGE_FLOATS / SW) & ~3;  // column pitch (16-B columns)
+    const int CE = SP - 4;                    // stage entries per chunk
+    const float* dyt = a.dy + (int64_t)t * a.dst_t;
+    auto fetch = [&](int b, int sub) -> float4 {
+        return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
+    };
+    auto finish = [&](float4 g) -> float4 {  // g' = (g * s) / s
+        if (a.ste) {
+            g.x = (g.x * sc) / sc; g.y = (g.y * sc) / sc; g.z = (g.z * sc) / sc; g.w = (g.w * sc) / sc;
+        }
+        return g;
+    };
+    // a dimension-split table: this workgroup's slice of EVERY lookup's dy row, now (other
+    // tables load a dummy address: the loads are issued on every path, so the compiler's
+    // wait counts stay exact and no later wait is for these loads)
+    float4 pfa[PFR], pfb[PFR];
+    const bool pf_early = active && dsplit;
+    {
+        const int nit = pf_early ? B << lg_sh : 1;
+#pragma unroll
+        for (int f = 0; f < PFR; ++f) {
+            int q = tid + TPB * f;
+            q = q < nit ? q : nit - 1;
+            pfa[f] = fetch(q >> lg_sh, q & (LG - 1));
+        }
+    }
+    CDIAG(1);
+    if (!active) {  // a dimension slice beyond D (D < 32): no work; the counts come from slot 0
+        if (tid == 0) a.ws_absmax[k] = 0.0f;
+        return;
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int j = 0; j <= SPLIT; ++j) s_cb[j] = cbv[j];
+    }
+    if (tid < SPLIT) s_ucnt[tid] = 0;
+#pragma unroll
+    for (int i = 0; i < MAXI; ++i)
+        if (tid + TPB * i >= B) r[i] = -1;
+    // 2. the slot's lookups, compacted in lookup order
+    auto none = [](int, int, bool) {};
+    const int n = ordered_compact(
+        ni, s_cnt, [&](int i) { return r[i] >= r0 && r[i] < r1; },
+        [&](int i, int p) {
+            const uint32_t b = tid + TPB * i;
+            const uint32_t g = dsplit ? b : (uint32_t)p;
+            keys[p] = ((uint64_t)(r[i] - r0) << 32) | (g << LK_BITS) | b;
+        },
+        none);
+    if (dsplit ? s == 0 : s == SPLIT - 1) {  // out-of-range indices: flagged once per table
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i)
+            if (tid + TPB * i < B && (r[i] < 0 || r[i] >= nrows)) bad = true;
+        if (bad) atomicOr(a.err, DQRM_ERRF_INDEX);
+    }
+    __syncthreads();
+    // a row-split slot: the dy rows of its lookups, before the sort (same rule: always issued)
+    const bool pf_wide = !dsplit && n > 0;
+    {
+        const int nit = pf_wide ? n << lg_sh : 1;
+#pragma unroll
+        for (int f = 0; f < PFR; ++f) {
+            int q = tid + TPB * f;
+            q = q < nit ? q : nit - 1;
+            pfb[f] = fetch(pf_wide ? kbag(keys[q >> lg_sh]) : 0, q & (LG - 1));
+        }
+    }
+    CDIAG(2);
+    // 3. sort by row
+    {
+        const uint32_t span = (uint32_t)(r1 - r0);
+        const int nbits = span <= 1 ? 0 : 32 - __clz(span - 1);
+        uint64_t* tmp = reinterpret_cast<uint64_t*>(lds + OFF_SCR);
+        int* hist = reinterpret_cast<int*>(lds + OFF_SCR + MAXB * 8);
+        if (nbits > 8)
+            msd_sort(keys, tmp, hist, s_w, n, nbits);
+        else
+            radix_sort(keys, tmp, hist, s_w, n, nbits);
+    }
+    CDIAG(3);
+    for (int p = tid; p < n; p += TPB) pos[kgat(keys[p])] = (uint16_t)p;
+    if (dsplit) {  // invalid lookups have no key: their prefetched slices are dropped
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i)
+            if (tid + TPB * i < B && !(r[i] >= 0 && r[i] < nrows)) pos[tid + TPB * i] = 0xFFFF;
+    }
+    // segment heads (first sorted position of every distinct row) and single-lookup
+    // segments, both prefix-counted in one pass. sdest[p]: a single-lookup segment's output
+    // entry (dimension-split: its segment number, fixed up below), else -(stage index) - 1,
+    // the stage holding only the lookups of multi-lookup segments, in sorted order
+    const int64_t cb_s = cbv[s < SPLIT ? s : 0];
+    int U, NS;
+    {
+        const int lane = tid % WAVE;
+        const int np = (n + TPB - 1) / TPB;
+        uint64_t mh[MAXI], ms[MAXI];
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int p = tid + TPB * i;
+            bool h = false, sg = false;
+            if (i < np && p < n) {
+                const uint32_t rw = krow(keys[p]);
+                h = p == 0 || krow(keys[p - 1]) != rw;
+                sg = h && (p + 1 == n || krow(keys[p + 1]) != rw);
+            }
+            mh[i] = __ballot(h);
+            ms[i] = __ballot(sg);
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i)
+                if (i < np) {
+                    s_cnt[i * NW + w] = (int)__popcll(mh[i]);
+                    s_cnt2[i * NW + w] = (int)__popcll(ms[i]);
+                }
+        __syncthreads();
+        const int vh = lane < np * NW ? s_cnt[lane] : 0, vs = lane < np * NW ? s_cnt2[lane] : 0;
+        int ih = vh, is = vs;
+#pragma unroll
+        for (int o = 1; o < WAVE; o <<= 1) {
+            const int y = __shfl_up(ih, o, WAVE), z = __shfl_up(is, o, WAVE);
+            if (lane >= o) { ih += y; is += z; }
+        }
+        U = __shfl(ih, WAVE - 1, WAVE);
+        NS = __shfl(is, WAVE - 1, WAVE);
+        const int eh = ih - vh, es = is - vs;
+        const uint64_t lt = lanemask_lt();
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int p = tid + TPB * i;
+            const int rh = __shfl(eh, (i * NW + w) & (WAVE - 1), WAVE) + (int)__popcll(mh[i] & lt);
+            const int rs = __shfl(es, (i * NW + w) & (WAVE - 1), WAVE) + (int)__popcll(ms[i] & lt);
+            if (i < np && p < n) {
+                const bool h = (mh[i] >> lane) & 1ull, sg = (ms[i] >> lane) & 1ull;
+                if (h) {
+                    hpos[rh] = (uint16_t)p;
+                    if (dsplit) atomicAdd(&s_ucnt[slot_of_row(krow(keys[p]), nblk)], 1);
+                }
+                const int u = h ? rh : rh - 1;
+                sdest[p] = sg ? (dsplit ? u : (int)(cb_s + u)) : -(p - rs) - 1;
+            }
+        }
+    }
+    if (tid == 0) hpos[U] = (uint16_t)n;
+    __syncthreads();
+    if (dsplit && tid <= SPLIT) {  // first segment of every row-range slot
+        int c = 0;
+        for (int q = 0; q < tid; ++q) c += s_ucnt[q];
+        s_uf[tid] = c;
+    }
+    // segments of more than one lookup (the rest are copied straight from registers)
+    const int M = ordered_compact(
+        (U + TPB - 1) / TPB, s_cnt,
+        [&](int i) {
+            const int u = tid + TPB * i;
+            return u < U && hpos[u + 1] - hpos[u] > 1;
+        },
+        [&](int i, int m) { mlist[m] = (uint16_t)(tid + TPB * i); }, none);
+    if (dsplit) {  // single-lookup segment -> its row-range slot's entry
+        for (int p = tid; p < n; p += TPB) {
+            const int u = sdest[p];
+            if (u >= 0) {
+                const int sl = slot_of_row(krow(keys[p]), nblk);
+                sdest[p] = (int)(s_cb[sl] + (u - s_uf[sl]));
+            }
+        }
+        __syncthreads();
+    }
+    CDIAG(4);
+    float amax = 0.0f;
+    auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
+        const int64_t row = r0 + krow(keys[hpos[u]]);
+        int sl = s;
+        int64_t e = s_cb[s] + u;
+        if (dsplit) {
+            sl = slot_of_row(row, nblk);
+            e = s_cb[sl] + (u - s_uf[sl]);
+        }
+        if (e < s_cb[sl + 1]) {
+            a.ws_vals[e * a.D + q0 * 4 + d] = acc;
+            if (q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
+        }
+        amax = fmaxf(amax, fabsf(acc));
+    };
+    auto put = [&](float* col, float4 v) {
+        col[0] = v.x; col[SP] = v.y; col[2 * SP] = v.z; col[3 * SP] = v.w;
+    };
+    if (n - NS <= CE) {
+        // 4. one chunk. Every value first goes where it belongs -- a single-lookup segment's
+        //    value IS its output row (kept in registers), the others land in the stage at
+        //    their sorted positions -- and only then are the output rows stored, so no wait
+        //    for a load ever waits for a store as well
+        const int nitems = (dsplit ? B : n) << lg_sh;
+        auto land = [&](int q, float4 v) -> int {  // v finished; returns the output entry or -1
+            const int p = pos[q >> lg_sh];
+            if (p == 0xFFFF) return -1;
+            const int e = sdest[p];
+            if (e < 0) put(stage + ((q & (LG - 1)) * 4) * SP + (-e - 1), v);
+            return e;
+        };
+        auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
+            if (e < 0 || e >= s_cb[SPLIT]) return;
+            reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D)[q0 + (q & (LG - 1))] = v;
+            if (q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
+            amax = fmaxf(amax, abs_max4(v));
+        };
+        int q = tid;
+        if (pf_early || pf_wide) {
+            int de[PFR];
+#pragma unroll
+            for (int f = 0; f < PFR; ++f) {
+                de[f] = -1;
+                if (q + TPB * f < nitems) {  // the STE division only where a value exists
+                    pfb[f] = finish(dsplit ? pfa[f] : pfb[f]);
+                    de[f] = land(q + TPB * f, pfb[f]);
+                }
+            }
+#pragma unroll
+            for (int f = 0; f < PFR; ++f) store(q + TPB * f, de[f], pfb[f]);
+            q += TPB * PFR;
+        }
+        for (; q < nitems; q += TPB) {  // beyond the register budget (or no prefetch)
+            const int p = pos[q >> lg_sh];
+            if (p == 0xFFFF) continue;
+            const float4 v = finish(fetch(kbag(keys[p]), q & (LG - 1)));
+            store(q, land(q, v), v);
+        }
+        __syncthreads();
+        CDIAG(5);
+        for (int i = tid; i < (M << sw_sh); i += TPB) {
+            const int u = mlist[i >> sw_sh], d = i & (SW - 1);
+            const int h = hpos[u], len = hpos[u + 1] - h;
+            const int st = -sdest[h] - 1;  // the segment's first stage entry
+            const float* col = stage + d * SP;
+            emit(u, d, chain_sum(col, st + 1, st + len, col[st]));
+        }
+    } else {
+        // a slot larger than the stage: chunks of CE sorted lookups, loaded after the sort;
+        // item (u, d) belongs to thread (u*SW + d) % TPB in every chunk, so the segment that
+        // crosses a chunk boundary continues in the same lane (carry)
+        float carry = 0.0f;
+        for (int c0 = 0; c0 < n; c0 += CE) {
+            const int ce = n - c0 < CE ? n - c0 : CE;
+            for (int q = tid; q < (ce << lg_sh); q += TPB) {
+                const int p = c0 + (q >> lg_sh), sub = q & (LG - 1);
+                put(stage + (sub * 4) * SP + (p - c0), finish(fetch(kbag(keys[p]), sub)));
+            }
+            __syncthreads();
+            auto seg_of = [&](int p) {  // segment holding sorted position p
+                int lo = 0, hi = U - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((int)hpos[mid] <= p) lo = mid; else hi = mid - 1;
+                }
+                return lo;
+            };
+            const int ua = seg_of(c0), ub = seg_of(c0 + ce - 1);
+            const int first = ua << sw_sh;
+            for (int i = first + ((tid - first) % TPB + TPB) % TPB; i < ((ub + 1) << sw_sh); i += TPB) {
+                const int u = i >> sw_sh, d = i & (SW - 1);
+                const int h = hpos[u], e1 = hpos[u + 1];
+                const float* col = stage + d * SP - c0;
+                const int pe = e1 < c0 + ce ? e1 : c0 + ce;
+                const float acc = h >= c0 ? chain_sum(col, h + 1, pe, col[h]) : chain_sum(col, c0, pe, carry);
+                if (e1 > c0 + ce) {
+                    carry = acc;
+                    continue;
+                }
+                emit(u, d, acc);
+            }
+            __syncthreads();
+        }
+    }
+    CDIAG_W(6);
+    // the workgroup's max|grad| (dimension-split: its slice's) and the slot counts
+    for (int o = WAVE / 2; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, WAVE));
+    if (tid % WAVE == 0) s_red[w] = amax;
+    __syncthreads();
+    if (tid == 0) {
+        float m = 0.0f;
+        for (int q = 0; q < NW; ++q) m = fmaxf(m, s_red[q]);
+        a.ws_absmax[k] = m;
+    }
+    if (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT)) {
+        const int sl = dsplit ? tid : s;
+        int c = dsplit ? s_ucnt[sl] : U;
+        const int64_t cap = s_cb[sl + 1] - s_cb[sl];
+        if (c > cap) {
+            atomicOr(a.err, DQRM_ERRF_OVERFLOW);
+            c = (int)cap;
+        }
+        a.ws_ucount[t * SPLIT + sl] = c;
+    }
+    CDIAG_W(7);
+}
+
+}  // namespace
+
+namespace dqrm_internal {
+
+int launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream) {
+    static bool lds_set = false;  // the attribute is per function, process-wide
+    if (!lds_set) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
+            return DQRM_E_HIP;
+        lds_set = true;
+    }
+    hipLaunchKernelGGL(k_coalesce_p1, dim3(a.T * SPLIT), dim3(TPB), LDS_BYTES, stream, a);
+    return hipGetLastError() == hipSuccess ? DQRM_OK : DQRM_E_HIP;
+}
+
+}  // namespace dqrm_internal
+
+#ifdef DQRM_DIAG_CLOCK
+extern "C" int dqrm_diag_coal_read(unsigned long long* host, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return DQRM_E_HIP;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_coal_clk), (size_t)n * sizeof(unsigned long long)) != hipSuccess)
+        return DQRM_E_HIP;
+    return DQRM_OK;
+}
+#endif

@@ -25,6 +25,7 @@
 #include <atomic>
 
 #include "../../include/dqrm.h"
+#include "dqrm_internal.h"
 
 #define DQRM_INLINE __device__ __forceinline__
 
@@ -44,6 +45,13 @@ __device__ unsigned long long g_diag_clk[8192 * 16];
 #define DIAG_W(k) do { __builtin_amdgcn_s_waitcnt(0); DIAG_T(k); } while (0)
 #else
 #define DIAG_W(k) do { } while (0)
+#endif
+// diagnostic shader-cycle stamp (s_memtime): with the wall stamps, the in-kernel clock
+#ifdef DQRM_DIAG_CLOCK
+#define DIAG_C(k) \
+    do { if (threadIdx.x == 0) g_diag_clk[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define DIAG_C(k) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------------------------
@@ -2963,6 +2971,7 @@ __global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
     __shared__ float s_red[FB_TPB / WAVE];
     const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
     DIAG_T(0);
+    DIAG_C(7);
     // Criteo form with <= 8 bags per thread: the thread's indices are loaded right away, in
     // parallel with the table metadata (no dependent round trip before the gather)
     int64_t pre[8];
@@ -2972,6 +2981,7 @@ __global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) pre[j] = (j < per && (int64_t)threadIdx.x * per + j < a.B) ? ti[j] : -1;
     }
+    DIAG_W(8);
     const Meta m = make_meta(a.meta, a.T);
     const int64_t nrows = m.num_rows[t];
     const int64_t nblk = ceil_div(nrows, BLK);
@@ -3010,6 +3020,7 @@ __global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
         }
     }
     DIAG_W(5);
+    DIAG_C(15);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3316,6 +3327,9 @@ int allow_lds(K kernel, size_t bytes) {
     return DQRM_OK;
 }
 
+// dqrm_emb_bwd_coalesce's kernel choice (dqrm_set_coalesce_kernel)
+std::atomic<int> g_coalesce_kernel{DQRM_COALESCE_AUTO};
+
 // dqrm_apply_sparse_update's kernel choice: -1 = not yet read from DQRM_APPLY
 std::atomic<int> g_apply_kernel{-1};
 
@@ -3406,6 +3420,12 @@ const char* dqrm_last_error(void) { return g_last_error; }
 __attribute__((visibility("hidden"))) int dqrm_internal_set_error(int code, const char* msg) {
     return set_error(code, "%s", msg);
 }
+int dqrm_set_coalesce_kernel(int kind) {
+    if (kind != DQRM_COALESCE_AUTO && kind != DQRM_COALESCE_GENERAL)
+        return set_error(DQRM_E_INVALID, "dqrm_set_coalesce_kernel: unknown kind %d", kind);
+    return g_coalesce_kernel.exchange(kind);
+}
+
 int dqrm_set_apply_kernel(int kind) {
     if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_SLOT)
         return set_error(DQRM_E_INVALID, "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat) or 2 (slot)");
@@ -3639,6 +3659,18 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
     c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
     c.ws_cap_base = ws_cap_base; c.ws_rows = ws_rows; c.ws_vals = ws_vals; c.ws_ucount = ws_ucount;
     c.ws_absmax = ws_absmax; c.ws = workspace; c.ws_bytes = workspace_bytes;
+    if (g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && (batch->flags & DQRM_BATCH_POOLING_ONE) &&
+        batch->num_bags <= dqrm_internal::kCoalesceMaxB && batch->max_lookups >= batch->num_bags &&
+        set->total_rows <= 0xffffffffll) {
+        dqrm_internal::CoalesceArgs ca{};
+        ca.meta = set->meta; ca.T = set->num_tables; ca.D = set->dim; ca.B = batch->num_bags; ca.idx = batch->idx;
+        ca.dy = dy; ca.dst_t = dy_stride_t; ca.dst_b = dy_stride_b; ca.scale = set->scale; ca.ste = ste;
+        ca.err = set->err; ca.ws_cap_base = ws_cap_base; ca.ws_rows = ws_rows; ca.ws_vals = ws_vals;
+        ca.ws_ucount = ws_ucount; ca.ws_absmax = ws_absmax;
+        if (dqrm_internal::launch_coalesce_pool1(ca, (hipStream_t)stream) != DQRM_OK)
+            return set_error(DQRM_E_HIP, "dqrm_emb_bwd_coalesce: launch failed: %s", hipGetErrorString(hipGetLastError()));
+        return DQRM_OK;
+    }
     return launch_bwd<1>(c, (hipStream_t)stream, "dqrm_emb_bwd_coalesce");
 }
 

@@ -184,7 +184,8 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
  *   ws_rows     i32 [WCAP]            local row ids
  *   ws_vals     f32 [WCAP][D]         coalesced sums
  *   ws_ucount   i32 [T*S]             entries used per slot
- *   ws_absmax   f32 [T*S]             max |vals| per slot (the local scale's input)
+ *   ws_absmax   f32 [T*S]             partial maxima of |vals|: the max over table t's S
+ *                                     entries is max |vals_t| (the local scale's input)
  * dqrm_coalesce_slot_caps() gives the slot capacities (host).
  * ------------------------------------------------------------------------------ */
 
@@ -322,6 +323,16 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
 #define DQRM_APPLY_FLAT 1
 #define DQRM_APPLY_SLOT 2
 int dqrm_set_apply_kernel(int kind);
+
+/* Which kernel dqrm_emb_bwd_coalesce launches (process-wide; returns the previous choice,
+ * or DQRM_E_INVALID). AUTO (default): batches in the Criteo form (DQRM_BATCH_POOLING_ONE)
+ * with num_bags <= 4096 and max_lookups >= num_bags take the Criteo-form kernel
+ * (dqrm_coalesce.hip), everything else the general one; GENERAL: always the general
+ * kernel. Both give bit-identical workspaces (rows, values, counts; the max over a table's
+ * DQRM_TABLE_SPLIT ws_absmax entries). */
+#define DQRM_COALESCE_AUTO 0
+#define DQRM_COALESCE_GENERAL 1
+int dqrm_set_coalesce_kernel(int kind);
 
 /* ---------------------------------------------------------------------------------
  * Dense (MLP) layer gradients, data-parallel:

@@ -699,3 +699,66 @@ def test_terabyte_full_size_773m_rows(dq):
     finally:
         del ts, ex
         torch.cuda.empty_cache()
+
+
+COAL_ROWS = [3, 62, 971, 1435, 1792, 1793, 2208, 7112, 300000, 20_000_000]
+
+
+@pytest.fixture
+def general_coalesce(dq):
+    """Force dqrm_emb_bwd_coalesce onto the general kernel for the duration of a block."""
+    L = dq._lib
+    lib = L.load()
+
+    class _Ctx:
+        def __enter__(self):
+            self.prev = lib.dqrm_set_coalesce_kernel(L.DQRM_COALESCE_GENERAL)
+
+        def __exit__(self, *exc):
+            lib.dqrm_set_coalesce_kernel(self.prev)
+
+    return _Ctx()
+
+
+@pytest.mark.parametrize("D,B,dist", [(64, 2048, "uniform"), (64, 2048, "zipf"), (16, 2048, "uniform"),
+                                      (16, 4096, "zipf"), (128, 2048, "uniform"), (32, 128, "uniform"),
+                                      (64, 1, "uniform"), (4, 3000, "zipf"), (256, 700, "zipf")])
+def test_criteo_form_coalesce_bitexact(dq, general_coalesce, D, B, dist):
+    """The Criteo-form coalesce kernel (dqrm_coalesce.hip: dimension-split tables of < 8
+    row blocks incl. the 1792/1793-row boundary, row-split slots by bitonic (<= 512 keys) or
+    radix sort, chunked stages for slots larger than LDS) writes exactly the oracle's
+    coalesced rows and values, the same counts as the general kernel, and per-table maxima
+    equal to max|vals|; out-of-range indices are flagged and left out."""
+    rows = COAL_ROWS
+    T = len(rows)
+    rng = np.random.default_rng(B * 7 + D)
+    P = G.pooling_one(rows, B, 61 + D, dist=dist)
+    if B > 8:
+        P[0, 5] = 3          # out of range on the 3-row table
+        P[2, 7] = -1         # negative on the 971-row table
+    dy = G.upstream_grad(T, B, D, 62 + D)
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=5)
+    scale = torch.from_numpy(rng.uniform(0.01, 0.1, size=T).astype(f32)).cuda()
+    ts.scale.copy_(scale)
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+    dyt = torch.from_numpy(dy).cuda()
+    ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+    ts.backward_coalesce(b, dyt, ws)
+    err = ts.read_errors()
+    ws_g = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+    with general_coalesce:
+        ts.backward_coalesce(b, dyt, ws_g)
+    assert ts.read_errors() == err
+    if B > 8:
+        assert err & dq._lib.DQRM_ERRF_INDEX
+    s = scale.cpu().numpy()
+    ar = np.arange(B, dtype=np.int64)
+    assert torch.equal(ws.ucount, ws_g.ucount)
+    for t in range(T):
+        r_o, v_o, _ = O.emb_bwd_coalesce(rows[t], P[t], ar, dy[t], s[t])
+        r_n, v_n = _table_slots(ws, t)
+        np.testing.assert_array_equal(r_n, r_o)
+        np.testing.assert_array_equal(v_n, v_o)
+        am = ws.absmax.view(T, -1)[t].max().item()
+        assert am == (np.abs(v_o).max() if v_o.size else 0.0)
+        assert am == ws_g.absmax.view(T, -1)[t].max().item()

@@ -1,0 +1,51 @@
+"""Per-phase wall-clock breakdown of the Criteo-form coalesce kernel (k_coalesce_p1) on the
+diagnostic build (tools/build_diag_coal.sh). Stamps: 0 start, 1 indices landed, 2 slot
+compacted, 3 sorted, 4 heads, 5 stage landed, 6 segments done (stores issued), 7 end.
+usage: python tools/diag_coalesce.py [terabyte|terabyte_ref|kaggle] [B]"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("DQRM_LIB_PATH", os.path.join(ROOT, "tools", "diag_build", "libdqrm_clock.so"))
+import deep_quantized_recommendation_model_dqrm_amd as dq  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd import _lib as L  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd.workloads import CONFIGS  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "terabyte"
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
+rows, D = CONFIGS[cfg]
+T = len(rows)
+lib = L.load()
+lib.dqrm_diag_coal_read.argtypes = [C.c_void_p, C.c_int]
+ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
+g = torch.Generator(device="cuda").manual_seed(5)
+P = torch.stack([torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows])
+b = dq.LookupBatch.pooling_one(P)
+dy = torch.randn(T, B, D, device="cuda", generator=g) * 0.05
+ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+ts.forward(b)
+for _ in range(20):
+    ts.backward_coalesce(b, dy, ws)
+torch.cuda.synchronize()
+buf = np.zeros(T * 8 * 16, dtype=np.uint64)
+ts.backward_coalesce(b, dy, ws)
+lib.dqrm_diag_coal_read(buf.ctypes.data, buf.size)
+c = buf.reshape(T, 8, 16).astype(np.int64)
+k0 = c[:, :, 0].min()
+print(f"{cfg} B={B} D={D}: span {(c[:, :, 7].max() - k0) / 100:.1f} us")
+print("per table, slowest slot (us): start | idx | compact | sort | heads | land | segs | tail || end")
+order = np.argsort(-c[:, :, 7].max(axis=1))
+for t in order:
+    s = int(np.argmax(c[t, :, 7]))
+    p = c[t, s]
+    if p[2] == 0:
+        print(f"t{t:2d} n={rows[t]:>10d} slot{s}: inactive end {(p[7] - k0) / 100:.1f}")
+        continue
+    ph = [p[0] - k0] + [p[i + 1] - p[i] for i in range(7)]
+    print(f"t{t:2d} n={rows[t]:>10d} slot{s}: " + " ".join(f"{x / 100:5.1f}" for x in ph) + f" || {(p[7] - k0) / 100:5.1f}")
+print("errors", ts.read_errors())
