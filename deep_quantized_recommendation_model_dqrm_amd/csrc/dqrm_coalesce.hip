@@ -357,7 +357,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 #pragma unroll
     for (int i = 0; i < MAXI; ++i) {
         const int b = tid + TPB * i;
-        r[i] = ti[b < B ? b : B - 1];
+        r[i] = -1;
+        if (i < ni) r[i] = ti[b < B ? b : B - 1];
     }
     const int64_t nblk = (nrows + BLK - 1) / BLK;
     const bool dsplit = nblk < SPLIT;
@@ -387,20 +388,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         }
         return g;
     };
-    // a dimension-split table: this workgroup's slice of EVERY lookup's dy row, now (other
-    // tables load a dummy address: the loads are issued on every path, so the compiler's
-    // wait counts stay exact and no later wait is for these loads)
-    float4 pfa[PFR], pfb[PFR];
-    const bool pf_early = active && dsplit;
-    {
-        const int nit = pf_early ? B << lg_sh : 1;
-#pragma unroll
-        for (int f = 0; f < PFR; ++f) {
-            int q = tid + TPB * f;
-            q = q < nit ? q : nit - 1;
-            pfa[f] = fetch(q >> lg_sh, q & (LG - 1));
-        }
-    }
     CDIAG(1);
     if (!active) {  // a dimension slice beyond D (D < 32): no work; the counts come from slot 0
         if (tid == 0) a.ws_absmax[k] = 0.0f;
@@ -414,6 +401,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 #pragma unroll
     for (int i = 0; i < MAXI; ++i)
         if (tid + TPB * i >= B) r[i] = -1;
+    CDIAG(8);
     // 2. the slot's lookups, compacted in lookup order
     auto none = [](int, int, bool) {};
     const int n = ordered_compact(
@@ -424,6 +412,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             keys[p] = ((uint64_t)(r[i] - r0) << 32) | (g << LK_BITS) | b;
         },
         none);
+    CDIAG(9);
     if (dsplit ? s == 0 : s == SPLIT - 1) {  // out-of-range indices: flagged once per table
         bool bad = false;
 #pragma unroll
@@ -432,16 +421,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         if (bad) atomicOr(a.err, DQRM_ERRF_INDEX);
     }
     __syncthreads();
-    // a row-split slot: the dy rows of its lookups, before the sort (same rule: always issued)
-    const bool pf_wide = !dsplit && n > 0;
-    {
-        const int nit = pf_wide ? n << lg_sh : 1;
+    CDIAG(10);
+    // the dy values this workgroup will combine, in flight across the sort (a dimension-
+    // split table: its slice of every lookup; a row split: its lookups' rows). Nothing
+    // between here and their use waits for global memory.
+    float4 pf[PFR];
+    const int npf = (dsplit ? B : n) << lg_sh;
 #pragma unroll
-        for (int f = 0; f < PFR; ++f) {
-            int q = tid + TPB * f;
-            q = q < nit ? q : nit - 1;
-            pfb[f] = fetch(pf_wide ? kbag(keys[q >> lg_sh]) : 0, q & (LG - 1));
-        }
+    for (int f = 0; f < PFR; ++f) {
+        const int q = tid + TPB * f;
+        if (q < npf) pf[f] = fetch(dsplit ? q >> lg_sh : (int)kbag(keys[q >> lg_sh]), q & (LG - 1));
     }
     CDIAG(2);
     // 3. sort by row
@@ -583,18 +572,18 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             amax = fmaxf(amax, abs_max4(v));
         };
         int q = tid;
-        if (pf_early || pf_wide) {
+        {
             int de[PFR];
 #pragma unroll
             for (int f = 0; f < PFR; ++f) {
                 de[f] = -1;
                 if (q + TPB * f < nitems) {  // the STE division only where a value exists
-                    pfb[f] = finish(dsplit ? pfa[f] : pfb[f]);
-                    de[f] = land(q + TPB * f, pfb[f]);
+                    pf[f] = finish(pf[f]);
+                    de[f] = land(q + TPB * f, pf[f]);
                 }
             }
 #pragma unroll
-            for (int f = 0; f < PFR; ++f) store(q + TPB * f, de[f], pfb[f]);
+            for (int f = 0; f < PFR; ++f) store(q + TPB * f, de[f], pf[f]);
             q += TPB * PFR;
         }
         for (; q < nitems; q += TPB) {  // beyond the register budget (or no prefetch)

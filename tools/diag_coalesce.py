@@ -48,4 +48,9 @@ for t in order:
         continue
     ph = [p[0] - k0] + [p[i + 1] - p[i] for i in range(7)]
     print(f"t{t:2d} n={rows[t]:>10d} slot{s}: " + " ".join(f"{x / 100:5.1f}" for x in ph) + f" || {(p[7] - k0) / 100:5.1f}")
+sub = [(c[t, s, 8] - c[t, s, 1], c[t, s, 9] - c[t, s, 8], c[t, s, 10] - c[t, s, 9], c[t, s, 2] - c[t, s, 10])
+       for t in range(T) for s in range(8) if c[t, s, 2] > 0]
+sub = np.array(sub) / 100
+print("compact split (median us): idx-wait %.2f  compaction %.2f  report+barrier %.2f  prefetch-issue %.2f" %
+      tuple(np.median(sub, axis=0)))
 print("errors", ts.read_errors())
