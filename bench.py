@@ -96,7 +96,7 @@ PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "kaggle": "kaggle"}
 KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
     "emb_fwd": "k_emb_fwd<{lpr},",
     "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
-    "bwd_coalesce": "k_bwd_fused<{lpr}, 1>",
+    "bwd_coalesce": ("k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),  # Criteo-form batches / general
     "bwd_sgd": "k_bwd_fused<{lpr}, 0>",
     "grad_quant_pack": "k_quant_pack<{lpr}>",
     "apply_sparse_update": "k_apply_flat<{lpr}>",
@@ -109,9 +109,10 @@ def pmc_traffic(path, phase, D):
     (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
     if not path or not os.path.exists(path) or phase not in KERNEL_SYMBOL:
         return None
-    prefix = KERNEL_SYMBOL[phase].format(lpr=D // 4)
+    sym = KERNEL_SYMBOL[phase]
+    prefixes = tuple(p.format(lpr=D // 4) for p in (sym if isinstance(sym, tuple) else (sym,)))
     for name, v in json.load(open(path))["kernels"].items():
-        if name.startswith(prefix) and v.get("hbm_bytes_per_launch") is not None:
+        if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
             return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
                     "source": os.path.relpath(path, ROOT)}
     return None

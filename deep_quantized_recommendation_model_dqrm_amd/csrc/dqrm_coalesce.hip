@@ -51,6 +51,7 @@ constexpr int WAVE = 64;
 constexpr int TPB = 1024;
 constexpr int NW = TPB / WAVE;
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
+static_assert(SPLIT == 8, "the XCD-aware block map puts a table's SPLIT slots on one XCD");
 constexpr int BLK = DQRM_BLOCK_ROWS;
 constexpr int MAXB = (int)dqrm_internal::kCoalesceMaxB;
 constexpr int MAXI = MAXB / TPB;  // lookups per thread
@@ -339,7 +340,12 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     int* sdest = reinterpret_cast<int*>(lds + OFF_SDEST);
     float* stage = reinterpret_cast<float*>(lds + OFF_STAGE);
 
-    const int k = blockIdx.x, t = k / SPLIT, s = k % SPLIT;
+    // XCD-aware placement: blocks b and b + 8 share an XCD (and its L2), so table t's 8 slots
+    // are blocks (t/8)*64 + s*8 + t%8. A dimension-split table's slots read 32-B slices of
+    // the same dy lines; on one XCD a line is fetched from HBM once, not once per slot.
+    const int t = (int)(blockIdx.x >> 6) * 8 + (int)(blockIdx.x & 7), s = (int)(blockIdx.x >> 3) & 7;
+    if (t >= a.T) return;
+    const int k = t * SPLIT + s;
     const int tid = threadIdx.x, w = tid / WAVE;
     const int B = (int)a.B;
     CDIAG(0);
@@ -673,7 +679,7 @@ int launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream) {
             return DQRM_E_HIP;
         lds_set = true;
     }
-    hipLaunchKernelGGL(k_coalesce_p1, dim3(a.T * SPLIT), dim3(TPB), LDS_BYTES, stream, a);
+    hipLaunchKernelGGL(k_coalesce_p1, dim3((a.T + 7) / 8 * 64), dim3(TPB), LDS_BYTES, stream, a);
     return hipGetLastError() == hipSuccess ? DQRM_OK : DQRM_E_HIP;
 }
 

@@ -50,6 +50,9 @@ def test_pmc_traffic_lookup(bench, tmp_path):
     assert bench.pmc_traffic(str(path), "emb_fwd", 16) is None  # no PMC pass for it
     assert bench.pmc_traffic(str(tmp_path / "missing.json"), "bwd_coalesce", 64) is None
     assert bench.pmc_traffic(None, "bwd_coalesce", 64) is None
+    summ["kernels"]["k_coalesce_p1(CoalesceArgs)"] = {"avg_us": 23.6, "hbm_bytes_per_launch": 2.3e7}
+    path.write_text(json.dumps(summ))  # the Criteo-form coalesce kernel is found first
+    assert bench.pmc_traffic(str(path), "bwd_coalesce", 64)["bytes"] == 23_000_000
     for name in sorted(os.listdir(os.path.join(ROOT, "profiles"))):  # committed summaries parse
         if name.startswith("r2_") and name.endswith("_summary.json"):
             for ph in bench.KERNEL_SYMBOL:
