@@ -111,7 +111,8 @@ def pmc_traffic(path, phase, D):
         return None
     sym = KERNEL_SYMBOL[phase]
     prefixes = tuple(p.format(lpr=D // 4) for p in (sym if isinstance(sym, tuple) else (sym,)))
-    for name, v in json.load(open(path))["kernels"].items():
+    kernels = json.load(open(path))["kernels"]
+    for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
         if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
             return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
                     "source": os.path.relpath(path, ROOT)}
