@@ -40,24 +40,36 @@ namespace {
 // workgroup stamps the 100 MHz wall clock at phase boundaries.
 #ifdef DQRM_DIAG_CLOCK
 __device__ unsigned long long g_coal_clk[8192 * 16];
-#define CDIAG(k) do { if (threadIdx.x == 0) g_coal_clk[blockIdx.x * 16 + (k)] = wall_clock64(); } while (0)
-#define CDIAG_W(k) do { __builtin_amdgcn_s_waitcnt(0); CDIAG(k); } while (0)
+#define CDIAG(ph) do { if (threadIdx.x == 0) g_coal_clk[k * 16 + (ph)] = wall_clock64(); } while (0)
+#define CDIAG_W(ph) do { __builtin_amdgcn_s_waitcnt(0); CDIAG(ph); } while (0)
 #else
 #define CDIAG(k) do { } while (0)
 #define CDIAG_W(k) do { } while (0)
 #endif
 
 constexpr int WAVE = 64;
-constexpr int TPB = 1024;
+#ifndef DQRM_COAL_TPB
+#define DQRM_COAL_TPB 1024
+#endif
+#ifndef DQRM_COAL_PFR
+#define DQRM_COAL_PFR 6
+#endif
+constexpr int TPB = DQRM_COAL_TPB;
 constexpr int NW = TPB / WAVE;
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
 static_assert(SPLIT == 8, "the XCD-aware block map puts a table's SPLIT slots on one XCD");
 constexpr int BLK = DQRM_BLOCK_ROWS;
 constexpr int MAXB = (int)dqrm_internal::kCoalesceMaxB;
 constexpr int MAXI = MAXB / TPB;  // lookups per thread
-constexpr int PFR = 6;            // prefetched float4 per thread
-constexpr int DBMAX = 9;          // radix digit bits per pass (one digit per thread in the scan)
+constexpr int PFR = DQRM_COAL_PFR;  // prefetched float4 per thread
+constexpr int DBMAX = TPB >= 512 ? 9 : 8;  // radix digit bits per pass (one digit per thread in the scan)
+static_assert(TPB >= 256, "the MSD pass gives each of its 256 buckets a thread");
 constexpr int FIX_MAX = 64;       // largest bucket the MSD pass finishes by ranking
+#ifndef DQRM_COAL_CSPAN
+#define DQRM_COAL_CSPAN 4096
+#endif
+constexpr int CSPAN = DQRM_COAL_CSPAN;  // largest row span sorted by counting rows (0: never)
+constexpr int RPT = CSPAN > 0 ? (CSPAN + TPB - 1) / TPB : 1;  // rows per thread in the row scan
 constexpr int LDS_BYTES = 156 * 1024;
 // dynamic LDS: keys u64[MAXB] | while sorting: ping-pong u64[MAXB] + digit counters
 // i32[NW << DBMAX]; after it: sorted position of each lookup u16[MAXB] | segment heads
@@ -71,6 +83,12 @@ constexpr int OFF_SDEST = OFF_MLIST + (MAXB + 8) * 2;
 constexpr int OFF_STAGE = OFF_SDEST + MAXB * 4;
 constexpr int STAGE_FLOATS = (LDS_BYTES - OFF_STAGE) / 4;
 static_assert(OFF_STAGE % 16 == 0, "stage alignment");
+// counting path: per-row packed prefix (lookups | distinct rows << 16) and multi-lookup
+// prefix, [CSPAN + 1] each, at the start of the stage (which is filled only after them)
+constexpr int OFF_INFO = OFF_STAGE;
+constexpr int OFF_MINFO = OFF_INFO + (CSPAN + 4) * 4;
+static_assert(OFF_MINFO + (CSPAN + 4) * 4 <= LDS_BYTES, "row counters");
+static_assert(MAXB < 65536 && CSPAN < 65536, "16-bit packed row prefixes");
 static_assert(OFF_SCR + MAXB * 8 + (NW << DBMAX) * 4 <= LDS_BYTES, "sort scratch");
 static_assert(MAXI * NW <= WAVE, "one prefix lane per (item, wave)");
 // key = (row - r0) << 32 | gather index << 12 | lookup: unique, and gather order = lookup order
@@ -79,6 +97,20 @@ constexpr uint32_t LK_MASK = (1u << LK_BITS) - 1u;
 static_assert(MAXB <= (1 << LK_BITS), "lookup index field");
 
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << (threadIdx.x % WAVE)) - 1ull; }
+// the wave index as a scalar (uniform) value, for v_readlane broadcasts
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE)); }
+__device__ __forceinline__ int lane_of(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+// inclusive prefix sum over the 64 lanes by DPP row shifts and row broadcasts (no LDS
+// permutes); every lane must be active
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
 __device__ __forceinline__ uint32_t krow(uint64_t x) { return (uint32_t)(x >> 32); }
 __device__ __forceinline__ uint32_t kgat(uint64_t x) { return (uint32_t)x >> LK_BITS; }
 __device__ __forceinline__ uint32_t kbag(uint64_t x) { return (uint32_t)x & LK_MASK; }
@@ -91,7 +123,7 @@ __device__ __forceinline__ float abs_max4(float4 v) {
 // position the next hit would get and whether it hit (all(i, rank, hit)). Returns the count.
 template <class Pred, class Emit, class All>
 __device__ __forceinline__ int ordered_compact(int ni, int* s_cnt, Pred pred, Emit emit, All all) {
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    const int lane = threadIdx.x % WAVE, w = wave_id();
     uint64_t m[MAXI];
 #pragma unroll
     for (int i = 0; i < MAXI; ++i) {
@@ -104,18 +136,13 @@ __device__ __forceinline__ int ordered_compact(int ni, int* s_cnt, Pred pred, Em
             if (i < ni) s_cnt[i * NW + w] = (int)__popcll(m[i]);
     __syncthreads();
     const int v = lane < ni * NW ? s_cnt[lane] : 0;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int y = __shfl_up(incl, o, WAVE);
-        if (lane >= o) incl += y;
-    }
+    const int incl = wave_incl_scan(v);
     const int excl = incl - v;
-    const int total = __shfl(incl, WAVE - 1, WAVE);
+    const int total = lane_of(incl, WAVE - 1);
     const uint64_t lt = lanemask_lt();
 #pragma unroll
     for (int i = 0; i < MAXI; ++i) {
-        const int base = __shfl(excl, (i * NW + w) & (WAVE - 1), WAVE);
+        const int base = lane_of(excl, (i * NW + w) & (WAVE - 1));
         const bool hit = (m[i] >> lane) & 1ull;
         const int rank = base + (int)__popcll(m[i] & lt);
         if (i < ni) {
@@ -128,29 +155,39 @@ __device__ __forceinline__ int ordered_compact(int ni, int* s_cnt, Pred pred, Em
 
 // exclusive prefix of one int per thread over the workgroup; *total = the sum
 __device__ __forceinline__ int block_excl_scan(int v, int* s_w, int* total) {
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
-    int incl = v;
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const int y = __shfl_up(incl, o, WAVE);
-        if (lane >= o) incl += y;
-    }
+    const int lane = threadIdx.x % WAVE, w = wave_id();
+    const int incl = wave_incl_scan(v);
     if (lane == WAVE - 1) s_w[w] = incl;
     __syncthreads();
     if (w == 0) {
         const int x = lane < NW ? s_w[lane] : 0;
-        int y = x;
-#pragma unroll
-        for (int o = 1; o < NW; o <<= 1) {
-            const int z = __shfl_up(y, o, WAVE);
-            if (lane >= o) y += z;
-        }
+        const int y = wave_incl_scan(x);
         if (lane < NW) s_w[lane] = y - x;
         if (lane == NW - 1) s_w[NW] = y;
     }
     __syncthreads();
     *total = s_w[NW];
     return s_w[w] + incl - v;
+}
+
+// block_excl_scan of two ints at once (shared barriers)
+__device__ __forceinline__ void block_excl_scan2(int v1, int v2, int* s_w, int* s_w2, int& e1, int& e2,
+                                                 int& t1, int& t2) {
+    const int lane = threadIdx.x % WAVE, w = wave_id();
+    const int i1 = wave_incl_scan(v1), i2 = wave_incl_scan(v2);
+    if (lane == WAVE - 1) { s_w[w] = i1; s_w2[w] = i2; }
+    __syncthreads();
+    if (w == 0) {
+        const int x1 = lane < NW ? s_w[lane] : 0, x2 = lane < NW ? s_w2[lane] : 0;
+        const int y1 = wave_incl_scan(x1), y2 = wave_incl_scan(x2);
+        if (lane < NW) { s_w[lane] = y1 - x1; s_w2[lane] = y2 - x2; }
+        if (lane == NW - 1) { s_w[NW] = y1; s_w2[NW] = y2; }
+    }
+    __syncthreads();
+    t1 = s_w[NW];
+    t2 = s_w2[NW];
+    e1 = s_w[w] + i1 - v1;
+    e2 = s_w2[w] + i2 - v2;
 }
 
 // Stable LSD radix sort of keys[0, n) by the row field (bits [0, nbits)), passes of at
@@ -302,10 +339,25 @@ __device__ __forceinline__ float add8(float acc, float4 x0, float4 x1) {
     return acc;
 }
 
-// acc + col[p] + col[p+1] + ... + col[pe-1], strictly in order; 16-B reads, the next 8
-// values in flight while the current 8 are added (col 16-B aligned)
+// acc + col[p] + col[p+1] + ... + col[pe-1], strictly in order; 16-B reads, the next 16
+// values in flight while the current 16 are added (col 16-B aligned)
 __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, float acc) {
     for (; p < pe && (p & 3); ++p) acc = acc + col[p];
+    if (p + 16 <= pe) {
+        const float4* c4 = reinterpret_cast<const float4*>(col + p);
+        float4 x0 = c4[0], x1 = c4[1], x2 = c4[2], x3 = c4[3];
+        p += 16;
+        while (p + 16 <= pe) {
+            c4 = reinterpret_cast<const float4*>(col + p);
+            const float4 y0 = c4[0], y1 = c4[1], y2 = c4[2], y3 = c4[3];
+            acc = add8(acc, x0, x1);
+            acc = add8(acc, x2, x3);
+            x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+            p += 16;
+        }
+        acc = add8(acc, x0, x1);
+        acc = add8(acc, x2, x3);
+    }
     if (p + 8 <= pe) {
         float4 x0 = *reinterpret_cast<const float4*>(col + p);
         float4 x1 = *reinterpret_cast<const float4*>(col + p + 4);
@@ -329,6 +381,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_cnt[MAXI * NW];
     __shared__ int s_cnt2[MAXI * NW];
     __shared__ int s_w[NW + 1];
+    __shared__ int s_w2[NW + 1];
+    __shared__ int s_crowd;
     __shared__ int64_t s_cb[SPLIT + 1];
     __shared__ int s_uf[SPLIT + 1];
     __shared__ int s_ucnt[SPLIT];
@@ -408,14 +462,39 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     for (int i = 0; i < MAXI; ++i)
         if (tid + TPB * i >= B) r[i] = -1;
     CDIAG(8);
-    // 2. the slot's lookups, compacted in lookup order
+    // Row spans of at most CSPAN rows are sorted by counting rows: the per-row counts give
+    // every segment's start, number and kind directly (no comparison sort, no head pass).
+    // A lookup's place among its row's lookups (lookup order) comes from
+    //   ranked (span <= 256): per-wave row counters + same-row lanes by ballots, as one
+    //     stable radix pass does;
+    //   atomic (256 < span <= CSPAN): the row counter's arrival rank, then re-ranked inside
+    //     its bucket by lookup order (a bucket above FIX_MAX -> the comparison sort)
+    const uint32_t span = (uint32_t)(r1 - r0);
+    const int nbits = span <= 1 ? 0 : 32 - __clz(span - 1);
+    const bool ranked = CSPAN > 0 && nbits <= 8;
+    const bool atomic_mode = nbits > 8 && span <= (uint32_t)CSPAN;
+    int* info = reinterpret_cast<int*>(lds + OFF_INFO);
+    int* minfo = reinterpret_cast<int*>(lds + OFF_MINFO);
+    int* whist = reinterpret_cast<int*>(lds + OFF_SCR);  // ranked: [NW][span] row counters
+    if (atomic_mode) {
+        for (int q = tid; q < (int)span; q += TPB) info[q] = 0;
+        if (tid == 0) s_crowd = 0;
+    }
+    if (ranked)
+        for (int q = tid; q < NW * (int)span; q += TPB) whist[q] = 0;
+    // 2. the slot's lookups, compacted in lookup order (counting path: each one's arrival
+    //    rank in its row's counter, in any order)
     auto none = [](int, int, bool) {};
+    uint64_t kx[MAXI];
+    int krk[MAXI];
     const int n = ordered_compact(
         ni, s_cnt, [&](int i) { return r[i] >= r0 && r[i] < r1; },
         [&](int i, int p) {
             const uint32_t b = tid + TPB * i;
             const uint32_t g = dsplit ? b : (uint32_t)p;
-            keys[p] = ((uint64_t)(r[i] - r0) << 32) | (g << LK_BITS) | b;
+            kx[i] = ((uint64_t)(r[i] - r0) << 32) | (g << LK_BITS) | b;
+            keys[p] = kx[i];
+            if (atomic_mode) krk[i] = atomicAdd(&info[r[i] - r0], 1);
         },
         none);
     CDIAG(9);
@@ -439,11 +518,171 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         if (q < npf) pf[f] = fetch(dsplit ? q >> lg_sh : (int)kbag(keys[q >> lg_sh]), q & (LG - 1));
     }
     CDIAG(2);
+    const int64_t cb_s = cbv[s < SPLIT ? s : 0];
+    uint64_t* tmp = reinterpret_cast<uint64_t*>(lds + OFF_SCR);
+    int U, NS, M;
+    bool counted = false;
+    int ta = 0, tm = 0;
+    if (ranked) {
+        // 3a'. wave w ranks keys [w*64*kpl, (w+1)*64*kpl) in order: same-row lanes by
+        //      bit-slice ballots, earlier keys of the wave by its row counters
+        const int lane = tid % WAVE, wu = wave_id();
+        const int kpl = (n + TPB - 1) / TPB;
+        const int i0 = wu * WAVE * kpl + lane;
+        const uint64_t lt = lanemask_lt();
+        uint64_t xr[MAXI];
+        int wr[MAXI];
+#pragma unroll
+        for (int kk = 0; kk < MAXI; ++kk) {
+            if (kk >= kpl) break;
+            const int i = i0 + kk * WAVE;
+            const bool v = i < n;
+            xr[kk] = v ? keys[i] : 0ull;
+            const uint32_t d = krow(xr[kk]);
+            uint64_t pm = __ballot(v);
+            for (int q = 0; q < nbits; ++q) {
+                const uint64_t bq = __ballot((d >> q) & 1u);
+                pm &= ((d >> q) & 1u) ? bq : ~bq;
+            }
+            int* hc = whist + wu * (int)span + d;
+            wr[kk] = v ? *hc + (int)__popcll(pm & lt) : 0;
+            if (v && (pm & lt) == 0) *hc += (int)__popcll(pm);
+        }
+        __syncthreads();
+        // 3b'. per row (thread = row): its count over the waves, the row prefixes, and each
+        //      wave's first place in the row's bucket
+        int cw[NW];
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            cw[q] = tid < (int)span ? whist[q * (int)span + tid] : 0;
+            c += cw[q];
+        }
+        int ea, em;
+        block_excl_scan2(c | (c > 0 ? 1 << 16 : 0), c > 1 ? 1 : 0, s_w, s_w2, ea, em, ta, tm);
+        if (tid < (int)span) {
+            info[tid] = ea;
+            minfo[tid] = em;
+            int o = ea & 0xFFFF;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                whist[q * (int)span + tid] = o;
+                o += cw[q];
+            }
+        }
+        if (tid == 0) {
+            info[span] = ta;
+            minfo[span] = tm;
+        }
+        __syncthreads();
+        // 3c'. every key to its place (each place written once; all keys are in registers)
+#pragma unroll
+        for (int kk = 0; kk < MAXI; ++kk) {
+            if (kk >= kpl) break;
+            if (i0 + kk * WAVE < n) keys[whist[wu * (int)span + krow(xr[kk])] + wr[kk]] = xr[kk];
+        }
+        __syncthreads();
+        counted = true;
+    } else if (atomic_mode) {
+        // 3a. row scan: per row, the lookups and distinct rows before it (packed) and the
+        //     multi-lookup rows before it; thread tid owns rows [tid*RPT, tid*RPT + RPT)
+        int c[RPT];
+        int va = 0, vm = 0;
+        bool crowd = false;
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+            const int q = tid * RPT + j;
+            c[j] = q < (int)span ? info[q] : 0;
+            va += c[j] | (c[j] > 0 ? 1 << 16 : 0);
+            vm += c[j] > 1 ? 1 : 0;
+            crowd |= c[j] > FIX_MAX;
+        }
+        if (crowd) s_crowd = 1;
+        int ea, em;
+        block_excl_scan2(va, vm, s_w, s_w2, ea, em, ta, tm);
+        if (s_crowd == 0) {
+#pragma unroll
+            for (int j = 0; j < RPT; ++j) {
+                const int q = tid * RPT + j;
+                if (q < (int)span) {
+                    info[q] = ea;
+                    minfo[q] = em;
+                }
+                ea += c[j] | (c[j] > 0 ? 1 << 16 : 0);
+                em += c[j] > 1 ? 1 : 0;
+            }
+            if (tid == 0) {
+                info[span] = ta;
+                minfo[span] = tm;
+            }
+            __syncthreads();
+            // 3b. every lookup to its row's bucket (arrival order), 3c. then to its place in
+            //     the bucket = the number of the bucket's keys before it in lookup order
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i)
+                if (i < ni && r[i] >= r0 && r[i] < r1) tmp[(info[r[i] - r0] & 0xFFFF) + krk[i]] = kx[i];
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i)
+                if (i < ni && r[i] >= r0 && r[i] < r1) {
+                    const int q = (int)(r[i] - r0);
+                    const int st = info[q] & 0xFFFF, len = (info[q + 1] & 0xFFFF) - st;
+                    int below = 0;
+                    for (int j = st; j < st + len && len > 1; ++j) below += tmp[j] < kx[i] ? 1 : 0;
+                    keys[st + below] = kx[i];
+                }
+            __syncthreads();
+            counted = true;
+        }
+    }
+    if (counted) {
+            CDIAG(3);
+            // 3d. per sorted position: gather -> position map, segment heads, multi-lookup
+            //     segment list and output entries, all from the row prefixes
+            for (int p = tid; p < n; p += TPB) {
+                const uint64_t x = keys[p];
+                const int q = (int)krow(x);
+                const int inf = info[q], st = inf & 0xFFFF, u = inf >> 16;
+                const int len = (info[q + 1] & 0xFFFF) - st, mp = minfo[q];
+                pos[kgat(x)] = (uint16_t)p;
+                if (p == st) {
+                    hpos[u] = (uint16_t)p;
+                    if (len > 1) mlist[mp] = (uint16_t)u;
+                }
+                int e = -(p - (u - mp)) - 1;
+                if (len == 1) {
+                    if (dsplit) {
+                        const int sl = slot_of_row(q, nblk);
+                        const int rs = (int)(nblk * sl / SPLIT * BLK);
+                        e = (int)(s_cb[sl] + (u - (info[rs] >> 16)));
+                    } else {
+                        e = (int)(cb_s + u);
+                    }
+                }
+                sdest[p] = e;
+            }
+            U = ta >> 16;
+            M = tm;
+            NS = U - M;
+            if (tid == 0) hpos[U] = (uint16_t)n;
+            if (dsplit && tid <= SPLIT) {  // first segment of every row-range slot, and counts
+                auto uf = [&](int sl) {
+                    const int64_t rs = nblk * sl / SPLIT * BLK;
+                    return rs < (int64_t)span ? info[rs] >> 16 : U;
+                };
+                s_uf[tid] = uf(tid);
+                if (tid < SPLIT) s_ucnt[tid] = uf(tid + 1) - uf(tid);
+            }
+    }
+    if (dsplit) {  // invalid lookups have no key: their prefetched slices are dropped
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i)
+            if (tid + TPB * i < B && !(r[i] >= 0 && r[i] < nrows)) pos[tid + TPB * i] = 0xFFFF;
+    }
+    if (counted) __syncthreads();
+    else {
     // 3. sort by row
     {
-        const uint32_t span = (uint32_t)(r1 - r0);
-        const int nbits = span <= 1 ? 0 : 32 - __clz(span - 1);
-        uint64_t* tmp = reinterpret_cast<uint64_t*>(lds + OFF_SCR);
         int* hist = reinterpret_cast<int*>(lds + OFF_SCR + MAXB * 8);
         if (nbits > 8)
             msd_sort(keys, tmp, hist, s_w, n, nbits);
@@ -461,8 +700,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // segments, both prefix-counted in one pass. sdest[p]: a single-lookup segment's output
     // entry (dimension-split: its segment number, fixed up below), else -(stage index) - 1,
     // the stage holding only the lookups of multi-lookup segments, in sorted order
-    const int64_t cb_s = cbv[s < SPLIT ? s : 0];
-    int U, NS;
     {
         const int lane = tid % WAVE;
         const int np = (n + TPB - 1) / TPB;
@@ -488,21 +725,17 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 }
         __syncthreads();
         const int vh = lane < np * NW ? s_cnt[lane] : 0, vs = lane < np * NW ? s_cnt2[lane] : 0;
-        int ih = vh, is = vs;
-#pragma unroll
-        for (int o = 1; o < WAVE; o <<= 1) {
-            const int y = __shfl_up(ih, o, WAVE), z = __shfl_up(is, o, WAVE);
-            if (lane >= o) { ih += y; is += z; }
-        }
-        U = __shfl(ih, WAVE - 1, WAVE);
-        NS = __shfl(is, WAVE - 1, WAVE);
+        const int ih = wave_incl_scan(vh), is = wave_incl_scan(vs);
+        U = lane_of(ih, WAVE - 1);
+        NS = lane_of(is, WAVE - 1);
         const int eh = ih - vh, es = is - vs;
         const uint64_t lt = lanemask_lt();
+        const int wu = wave_id();
 #pragma unroll
         for (int i = 0; i < MAXI; ++i) {
             const int p = tid + TPB * i;
-            const int rh = __shfl(eh, (i * NW + w) & (WAVE - 1), WAVE) + (int)__popcll(mh[i] & lt);
-            const int rs = __shfl(es, (i * NW + w) & (WAVE - 1), WAVE) + (int)__popcll(ms[i] & lt);
+            const int rh = lane_of(eh, (i * NW + wu) & (WAVE - 1)) + (int)__popcll(mh[i] & lt);
+            const int rs = lane_of(es, (i * NW + wu) & (WAVE - 1)) + (int)__popcll(ms[i] & lt);
             if (i < np && p < n) {
                 const bool h = (mh[i] >> lane) & 1ull, sg = (ms[i] >> lane) & 1ull;
                 if (h) {
@@ -522,7 +755,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         s_uf[tid] = c;
     }
     // segments of more than one lookup (the rest are copied straight from registers)
-    const int M = ordered_compact(
+    M = ordered_compact(
         (U + TPB - 1) / TPB, s_cnt,
         [&](int i) {
             const int u = tid + TPB * i;
@@ -539,6 +772,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         }
         __syncthreads();
     }
+    }  // comparison sort
     CDIAG(4);
     float amax = 0.0f;
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
