@@ -333,44 +333,39 @@ __device__ __forceinline__ int slot_of_row(int64_t row, int64_t nblk) {
     return (int)((SPLIT * (blk + 1) + nb - 1) / nb) - 1;
 }
 
-__device__ __forceinline__ float add8(float acc, float4 x0, float4 x1) {
-    acc = acc + x0.x; acc = acc + x0.y; acc = acc + x0.z; acc = acc + x0.w;
-    acc = acc + x1.x; acc = acc + x1.y; acc = acc + x1.z; acc = acc + x1.w;
-    return acc;
-}
+#ifndef DQRM_COAL_CH
+#define DQRM_COAL_CH 16
+#endif
+constexpr int CH4 = DQRM_COAL_CH / 4;  // float4 of an ordered chain in flight
 
-// acc + col[p] + col[p+1] + ... + col[pe-1], strictly in order; 16-B reads, the next 16
-// values in flight while the current 16 are added (col 16-B aligned)
+// acc + col[p] + col[p+1] + ... + col[pe-1], strictly in order; 16-B reads, the next
+// 4*CH4 values in flight while the current 4*CH4 are added (col 16-B aligned)
 __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, float acc) {
     for (; p < pe && (p & 3); ++p) acc = acc + col[p];
-    if (p + 16 <= pe) {
-        const float4* c4 = reinterpret_cast<const float4*>(col + p);
-        float4 x0 = c4[0], x1 = c4[1], x2 = c4[2], x3 = c4[3];
-        p += 16;
-        while (p + 16 <= pe) {
-            c4 = reinterpret_cast<const float4*>(col + p);
-            const float4 y0 = c4[0], y1 = c4[1], y2 = c4[2], y3 = c4[3];
-            acc = add8(acc, x0, x1);
-            acc = add8(acc, x2, x3);
-            x0 = y0; x1 = y1; x2 = y2; x3 = y3;
-            p += 16;
+    if (p + 4 * CH4 <= pe) {
+        float4 x[CH4];
+#pragma unroll
+        for (int j = 0; j < CH4; ++j) x[j] = reinterpret_cast<const float4*>(col + p)[j];
+        p += 4 * CH4;
+        while (p + 4 * CH4 <= pe) {
+            float4 y[CH4];
+#pragma unroll
+            for (int j = 0; j < CH4; ++j) y[j] = reinterpret_cast<const float4*>(col + p)[j];
+#pragma unroll
+            for (int j = 0; j < CH4; ++j) {
+                acc = acc + x[j].x; acc = acc + x[j].y; acc = acc + x[j].z; acc = acc + x[j].w;
+                x[j] = y[j];
+            }
+            p += 4 * CH4;
         }
-        acc = add8(acc, x0, x1);
-        acc = add8(acc, x2, x3);
+#pragma unroll
+        for (int j = 0; j < CH4; ++j) {
+            acc = acc + x[j].x; acc = acc + x[j].y; acc = acc + x[j].z; acc = acc + x[j].w;
+        }
     }
-    if (p + 8 <= pe) {
-        float4 x0 = *reinterpret_cast<const float4*>(col + p);
-        float4 x1 = *reinterpret_cast<const float4*>(col + p + 4);
-        p += 8;
-        while (p + 8 <= pe) {
-            const float4 y0 = *reinterpret_cast<const float4*>(col + p);
-            const float4 y1 = *reinterpret_cast<const float4*>(col + p + 4);
-            acc = add8(acc, x0, x1);
-            x0 = y0;
-            x1 = y1;
-            p += 8;
-        }
-        acc = add8(acc, x0, x1);
+    for (; p + 4 <= pe; p += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(col + p);
+        acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
     }
     for (; p < pe; ++p) acc = acc + col[p];
     return acc;

@@ -9,10 +9,10 @@ O=$R/tools/diag_build; C=$R/deep_quantized_recommendation_model_dqrm_amd/csrc
 mkdir -p $O
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I $R/include"
 for v in $1; do
-  IFS=: read tpb pfr csp <<< "$v"; n=t${tpb}p${pfr}c${csp}
-  ( /opt/rocm/bin/hipcc $F -DDQRM_COAL_TPB=$tpb -DDQRM_COAL_PFR=$pfr -DDQRM_COAL_CSPAN=$csp -c $C/dqrm_coalesce.hip -o $O/c_$n.o 2>/dev/null &&
+  IFS=: read tpb pfr csp ch <<< "$v"; n=t${tpb}p${pfr}c${csp}h${ch}
+  ( /opt/rocm/bin/hipcc $F -DDQRM_COAL_TPB=$tpb -DDQRM_COAL_PFR=$pfr -DDQRM_COAL_CSPAN=$csp -DDQRM_COAL_CH=$ch -c $C/dqrm_coalesce.hip -o $O/c_$n.o 2>/dev/null &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $C/dqrm_kernels.o $O/c_$n.o $C/dqrm_dense.o $C/dqrm_input.o -o $O/libdqrm_$n.so ) &
-  ( /opt/rocm/bin/hipcc $F -DDQRM_DIAG_CLOCK -DDQRM_COAL_TPB=$tpb -DDQRM_COAL_PFR=$pfr -DDQRM_COAL_CSPAN=$csp -c $C/dqrm_coalesce.hip -o $O/cc_$n.o 2>/dev/null &&
+  ( /opt/rocm/bin/hipcc $F -DDQRM_DIAG_CLOCK -DDQRM_COAL_TPB=$tpb -DDQRM_COAL_PFR=$pfr -DDQRM_COAL_CSPAN=$csp -DDQRM_COAL_CH=$ch -c $C/dqrm_coalesce.hip -o $O/cc_$n.o 2>/dev/null &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $C/dqrm_kernels.o $O/cc_$n.o $C/dqrm_dense.o $C/dqrm_input.o -o $O/libdqrm_${n}_clock.so ) &
 done
 wait
