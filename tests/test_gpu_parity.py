@@ -701,7 +701,7 @@ def test_terabyte_full_size_773m_rows(dq):
         torch.cuda.empty_cache()
 
 
-COAL_ROWS = [3, 62, 971, 1435, 1792, 1793, 2208, 7112, 300000, 20_000_000]
+COAL_ROWS = [3, 62, 971, 1435, 1792, 1793, 2208, 7112, 32768, 300000, 20_000_000]
 
 
 @pytest.fixture
@@ -725,8 +725,10 @@ def general_coalesce(dq):
                                       (64, 1, "uniform"), (4, 3000, "zipf"), (256, 700, "zipf")])
 def test_criteo_form_coalesce_bitexact(dq, general_coalesce, D, B, dist):
     """The Criteo-form coalesce kernel (dqrm_coalesce.hip: dimension-split tables of < 8
-    row blocks incl. the 1792/1793-row boundary, row-split slots by bitonic (<= 512 keys) or
-    radix sort, chunked stages for slots larger than LDS) writes exactly the oracle's
+    row blocks incl. the 1792/1793-row boundary; row spans <= 256 by ballot-ranked row
+    counting, spans up to 4096 rows (32768-row table: exactly 4096) by atomic row counting
+    with the comparison sort as the crowded (Zipf) fallback, wider spans by the MSD sort;
+    chunked stages for slots larger than LDS) writes exactly the oracle's
     coalesced rows and values, the same counts as the general kernel, and per-table maxima
     equal to max|vals|; out-of-range indices are flagged and left out."""
     rows = COAL_ROWS
