@@ -69,7 +69,10 @@ def parse(argv=None):
                    help="refresh the table scales every P steps (q_m_n_q_g.py:303-315); 0 = every step")
     p.add_argument("--use-packed", action="store_true",
                    help="with --scale-period: gather INT4 rows between refreshes, repack touched rows")
-    p.add_argument("--graph", action="store_true", help="replay each step from a captured HIP graph (N=1)")
+    p.add_argument("--graph", action="store_true", help="replay the steps from captured HIP graphs (N=1)")
+    p.add_argument("--graph-steps", type=int, default=8,
+                   help="consecutive steps (one per resident batch) captured in each HIP graph: one "
+                        "graph launch per that many steps (must divide --steps, else 1)")
     p.add_argument("--index-dist", default="uniform", choices=["uniform", "zipf"])
     p.add_argument("--num-batches", type=int, default=8, help="distinct resident batches cycled")
     p.add_argument("--gather-batch", type=int, default=65536,
@@ -291,15 +294,22 @@ def main():
     dj = names.index(dom)
 
     graphs = None
-    if a.graph:  # one captured step per resident batch; periodic refresh steps stay eager
+    gs = 1
+    if a.graph:
+        # gs consecutive steps (batches k .. k+gs-1) per captured graph, one graph per window of
+        # the resident batches; a graph launch costs more than a B=128 step, so it is paid once
+        # per gs steps. Periodic-refresh runs keep one step per graph (refresh steps run eager).
+        gs = a.graph_steps if (a.scale_period <= 1 and a.graph_steps > 1 and a.steps % a.graph_steps == 0
+                               and (a.warmup + a.steps) % a.graph_steps == 0) else 1
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         graphs = []
         with torch.cuda.stream(s):
-            for k in range(len(batches)):
+            for k in range(0, max(len(batches), gs), gs):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
-                    step(k, refresh=a.scale_period <= 0)
+                    for j in range(gs):
+                        step(k + j, refresh=a.scale_period <= 0)
                 graphs.append(g)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -307,8 +317,8 @@ def main():
     def run(i, ev=None):
         if graphs is None or (a.scale_period > 1 and i % a.scale_period == 0):
             step(i, ev, only=dj)
-        else:
-            graphs[i % len(graphs)].replay()
+        elif i % gs == 0:  # steps i .. i+gs-1 (batches (i+j) % len(batches), as the eager run)
+            graphs[(i % max(len(batches), gs)) // gs].replay()
 
     # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
     # it runs on) on every sample_every-th step, so the events barely perturb the timing
@@ -398,7 +408,8 @@ def main():
                 "batch_per_gpu": B, "global_batch": B_global, "pooling": 1,
                 "grad_bits": a.grad_bits if a.mode == "dp" else None,
                 "scale_period": max(a.scale_period, 1), "packed_int4_forward": a.use_packed,
-                "hip_graph": a.graph, "parallelism": f"dp{world} (tables replicated)",
+                "hip_graph": a.graph, "graph_steps": gs if a.graph else None,
+                "parallelism": f"dp{world} (tables replicated)",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -10,24 +10,27 @@
 // lookup's dy row is known from its position alone. The kernel is built for latency: at
 // 2048 lookups per table every workgroup does a few hundred keys, so what costs is the
 // chain of dependent steps and the instructions each wave issues, not bandwidth.
-//   1. every thread's lookups (b = tid + 1024 i) are loaded at once; a dimension-split
-//      table (fewer than 8 row blocks: every workgroup sees all lookups and owns D/8 of
-//      the dimensions) also issues its dy slices of ALL lookups right away, so both HBM
-//      round trips overlap;
-//   2. the slot's lookups are compacted in lookup order (ballots + one 64-entry prefix),
-//      keys = (row - r0) << 32 | gather index; a row-split slot issues its dy rows now,
-//      before the sort;
-//   3. sort by row: <= 512 keys one per thread by a bitonic network (shuffles below 64,
-//      LDS above), more by a stable 8-bit LSD radix (ballot digit matching); the keys are
-//      unique and ascend with the lookup index, so either gives the reference's order:
-//      rows ascending, a row's lookups in lookup order;
-//   4. the prefetched values land in a DIMENSION-MAJOR stage at their sorted positions,
-//      and item (segment, dimension) = one lane sums its column strictly in lookup order
-//      (8 LDS reads in flight ahead of the adds), so a hot row's long chain runs at add
-//      latency and short segments cost one read. Slots too large for the stage stream it
-//      in chunks (the same lane carries a segment across chunks).
-// The code is kept small on purpose: each CU runs one workgroup once per launch, so every
-// instruction is fetched cold.
+//   1. every thread's lookups (b = tid + 1024 i) are loaded at once;
+//   2. the slot's lookups are compacted in lookup order (ballots + a DPP scan), keys =
+//      (row - r0) << 32 | gather index << 12 | lookup; the dy values this workgroup combines
+//      (a dimension-split table -- fewer than 8 row blocks, every workgroup sees all lookups
+//      and owns D/8 of the dimensions -- its slice of every lookup; a row split: its
+//      lookups' rows) are issued now and stay in flight across the sort;
+//   3. rows are COUNTED, not compared, for row spans up to CSPAN rows: spans <= 256 by
+//      per-wave row counters + bit-sliced same-row ballots (a stable radix pass), larger
+//      ones by LDS row counters (arrival rank) re-ranked inside each row's bucket by lookup
+//      order; one block scan of the per-row (lookups, distinct rows, multi-lookup rows)
+//      prefixes then gives every segment's start, output entry and stage place directly.
+//      Wider spans: an MSD bucket sort; a crowded bucket (hot row) falls back to the stable
+//      LSD radix sort. Either way the order is the reference's: rows ascending, a row's
+//      lookups in lookup order;
+//   4. single-lookup segments are stored straight from registers; the others land in a
+//      DIMENSION-MAJOR stage at their sorted positions and item (segment, dimension) = one
+//      lane sums its column strictly in lookup order (16 LDS values in flight ahead of the
+//      adds). Slots too large for the stage stream it in chunks (the same lane carries a
+//      segment across chunks).
+// A table's 8 slots run on one XCD (block map below), so dy lines shared by the slices of a
+// dimension-split table come from one L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -437,12 +440,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     auto fetch = [&](int b, int sub) -> float4 {
         return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
     };
-    auto finish = [&](float4 g) -> float4 {  // g' = (g * s) / s
-        if (a.ste) {
-            g.x = (g.x * sc) / sc; g.y = (g.y * sc) / sc; g.z = (g.z * sc) / sc; g.w = (g.w * sc) / sc;
-        }
-        return g;
-    };
+    const dqrm_internal::SteDiv ste_div(sc);
+    auto finish = [&](float4 g) -> float4 { return a.ste ? ste_div(g) : g; };  // g' = (g * s) / s
     CDIAG(1);
     if (!active) {  // a dimension slice beyond D (D < 32): no work; the counts come from slot 0
         if (tid == 0) a.ws_absmax[k] = 0.0f;

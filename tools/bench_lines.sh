@@ -11,9 +11,9 @@ declare -A LINES=(
   [tb_unfused]="--steps 20 --warmup 5 --unfused-local --gather-batch 0 --mlp-iters 0 --cpu-baseline 0"
   [kaggle_dp]="--config kaggle --steps 50 --warmup 5 --gather-batch 0 --mlp-iters 0"
   [kaggle_fwd128]="--config kaggle --mode fwd --batch-per-gpu 128 --steps 200 --warmup 20 --gather-batch 0 --mlp-iters 0"
-  [kaggle_fwd128_graph]="--config kaggle --mode fwd --batch-per-gpu 128 --steps 200 --warmup 20 --graph --gather-batch 0 --mlp-iters 0 --cpu-baseline 0"
+  [kaggle_fwd128_graph]="--config kaggle --mode fwd --batch-per-gpu 128 --steps 200 --warmup 24 --graph --gather-batch 0 --mlp-iters 0 --cpu-baseline 0"
   [kaggle_sgd128]="--config kaggle --mode sgd --batch-per-gpu 128 --steps 200 --warmup 20 --gather-batch 0 --mlp-iters 0"
-  [kaggle_sgd128_graph]="--config kaggle --mode sgd --batch-per-gpu 128 --steps 200 --warmup 20 --graph --gather-batch 0 --mlp-iters 0 --cpu-baseline 0"
+  [kaggle_sgd128_graph]="--config kaggle --mode sgd --batch-per-gpu 128 --steps 200 --warmup 24 --graph --gather-batch 0 --mlp-iters 0 --cpu-baseline 0"
 )
 ORDER="tb tb_periodic tb_unfused kaggle_dp kaggle_fwd128 kaggle_fwd128_graph kaggle_sgd128 kaggle_sgd128_graph"
 NAMES=${*:-$ORDER}
