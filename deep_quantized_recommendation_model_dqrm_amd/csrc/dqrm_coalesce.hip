@@ -440,8 +440,12 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     auto fetch = [&](int b, int sub) -> float4 {
         return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
     };
-    const dqrm_internal::SteDiv ste_div(sc);
-    auto finish = [&](float4 g) -> float4 { return a.ste ? ste_div(g) : g; };  // g' = (g * s) / s
+    auto finish = [&](float4 g) -> float4 {  // g' = (g * s) / s
+        if (a.ste) {
+            g.x = (g.x * sc) / sc; g.y = (g.y * sc) / sc; g.z = (g.z * sc) / sc; g.w = (g.w * sc) / sc;
+        }
+        return g;
+    };
     CDIAG(1);
     if (!active) {  // a dimension slice beyond D (D < 32): no work; the counts come from slot 0
         if (tid == 0) a.ws_absmax[k] = 0.0f;

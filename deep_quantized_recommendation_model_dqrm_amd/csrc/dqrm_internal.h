@@ -34,35 +34,4 @@ constexpr int64_t kCoalesceMaxB = 4096;
 // launches k_coalesce_p1 (dqrm_coalesce.hip); returns a DQRM_E_* code
 int launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream);
 
-// STE backward g' = (g * s) / s (quant_utils.py:349-363) without the IEEE division
-// sequence, bit-identical to it: y = RN(1/s) once per table; q0 = RN(x*y) lies within 2 ulp
-// of x/s, one residual correction (fma: the product is exact) makes it faithful, and
-// Markstein's step with the correctly rounded y then gives exactly RN(x/s). Valid while
-// nothing under- or overflows: s in [2^-60, 2^60] (checked per table) and |x| in
-// [2^-60, 2^60]; a zero keeps its sign through x*y; anything else (tiny, huge, non-finite
-// values, s = 0) takes the IEEE division.
-struct SteDiv {
-    float s, y;
-    bool ok;
-    __device__ __forceinline__ explicit SteDiv(float s_) : s(s_) {
-        const float as = fabsf(s_);
-        ok = as >= 0x1p-60f && as <= 0x1p60f;
-        y = ok ? 1.0f / s_ : 0.0f;
-    }
-    __device__ __forceinline__ float operator()(float g) const {
-        const float x = g * s;
-        const float ax = fabsf(x);
-        if (!ok || !(ax <= 0x1p60f && (ax >= 0x1p-60f || ax == 0.0f))) return x / s;
-        float q = x * y;
-        float r = fmaf(-s, q, x);
-        q = fmaf(r, y, q);
-        r = fmaf(-s, q, x);
-        q = fmaf(r, y, q);
-        return ax == 0.0f ? x * y : q;
-    }
-    __device__ __forceinline__ float4 operator()(float4 g) const {
-        return make_float4((*this)(g.x), (*this)(g.y), (*this)(g.z), (*this)(g.w));
-    }
-};
-
 }  // namespace dqrm_internal

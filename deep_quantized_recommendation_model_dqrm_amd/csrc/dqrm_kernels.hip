@@ -1405,8 +1405,12 @@ struct DySource {
     DQRM_INLINE float4 fetch(uint32_t bag, int sub) const {
         return reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[off4 + sub];
     }
-    dqrm_internal::SteDiv sd;
-    DQRM_INLINE float4 finish(float4 g) const { return ste ? sd(g) : g; }
+    DQRM_INLINE float4 finish(float4 g) const {
+        if (ste) {
+            g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
+        }
+        return g;
+    }
     DQRM_INLINE float4 load(uint32_t bag, int sub) const { return finish(fetch(bag, sub)); }
 };
 
@@ -2816,8 +2820,7 @@ DQRM_INLINE void fused_slot(const FArgs& a, unsigned char* lds, int k, int t, in
     DIAG_T(1);
     // 2. prefetch this workgroup's slice of every gathered lookup's dy row into registers:
     //    the loads stay in flight across the sort (barriers wait for LDS traffic only)
-    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, dsplit ? z * LG : 0,
-                       dqrm_internal::SteDiv(a.scale[t])};
+    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, dsplit ? z * LG : 0};
     float4 pfv[FB_PFR];
     if (pf) {
 #pragma unroll
@@ -3264,7 +3267,6 @@ __global__ void __launch_bounds__(256) k_lookup_grad(LgArgs a) {
     const int lane = threadIdx.x % LPR, grp = threadIdx.x / LPR;
     const int D = LPR * 4;
     const float s = a.scale[t];
-    const dqrm_internal::SteDiv ste_div(s);
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
     const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
     const int64_t B = a.B;
@@ -3280,7 +3282,7 @@ __global__ void __launch_bounds__(256) k_lookup_grad(LgArgs a) {
         }
         if (s1 == s0) continue;
         float4 g = reinterpret_cast<const float4*>(a.dy + (int64_t)t * a.dst_t + b * a.dst_b)[lane];
-        if (a.ste) g = ste_div(g);
+        if (a.ste) { g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s; }
         for (int64_t j = s0; j < s1; ++j) {
             int64_t r = a.idx[ibase + j];
             float4 v = g;
