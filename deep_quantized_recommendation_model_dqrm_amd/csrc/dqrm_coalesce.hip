@@ -11,11 +11,12 @@
 // 2048 lookups per table every workgroup does a few hundred keys, so what costs is the
 // chain of dependent steps and the instructions each wave issues, not bandwidth.
 //   1. every thread's lookups (b = tid + 1024 i) are loaded at once;
-//   2. the slot's lookups are compacted in lookup order (ballots + a DPP scan), keys =
-//      (row - r0) << 32 | gather index << 12 | lookup; the dy values this workgroup combines
-//      (a dimension-split table -- fewer than 8 row blocks, every workgroup sees all lookups
-//      and owns D/8 of the dimensions -- its slice of every lookup; a row split: its
-//      lookups' rows) are issued now and stay in flight across the sort;
+//   2. a dimension-split table (fewer than 8 row blocks: every workgroup sees all lookups
+//      and owns D/8 of the dimensions) issues its dy slice of every lookup right behind the
+//      index loads (a row-split slot issues as many placeholder loads, so the compiler waits
+//      for the index loads alone); the slot's lookups are compacted in lookup order (ballots
+//      + a DPP scan), keys = (row - r0) << 32 | gather index << 12 | lookup; a row-split
+//      slot then issues its lookups' dy rows, in flight across the sort;
 //   3. rows are COUNTED, not compared, for row spans up to CSPAN rows: spans <= 256 by
 //      per-wave row counters + bit-sliced same-row ballots (a stable radix pass), larger
 //      ones by LDS row counters (arrival rank) re-ranked inside each row's bucket by lookup
@@ -451,6 +452,23 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         if (tid == 0) a.ws_absmax[k] = 0.0f;
         return;
     }
+    // A dimension-split table combines its slice of EVERY lookup: those dy loads depend on
+    // nothing and go out now, in flight with the index loads and across the compaction and
+    // sort. A row-split slot issues the same number of placeholder loads (one hot 16-B line,
+    // overwritten after the compaction), so on both paths the compiler waits for the index
+    // loads alone.
+    float4 pf[PFR];
+    {
+        const int lim = B > 0 ? (B << lg_sh) - 1 : 0;
+#pragma unroll
+        for (int f = 0; f < PFR; ++f) {
+            const int q = min(tid + TPB * f, lim);
+            const float4* src = dsplit && B > 0
+                                    ? reinterpret_cast<const float4*>(dyt + (int64_t)(q >> lg_sh) * a.dst_b) + q0 + (q & (LG - 1))
+                                    : reinterpret_cast<const float4*>(a.ws_cap_base);
+            pf[f] = *src;
+        }
+    }
     if (tid == 0) {
 #pragma unroll
         for (int j = 0; j <= SPLIT; ++j) s_cb[j] = cbv[j];
@@ -508,12 +526,12 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // the dy values this workgroup will combine, in flight across the sort (a dimension-
     // split table: its slice of every lookup; a row split: its lookups' rows). Nothing
     // between here and their use waits for global memory.
-    float4 pf[PFR];
-    const int npf = (dsplit ? B : n) << lg_sh;
+    if (!dsplit) {
 #pragma unroll
-    for (int f = 0; f < PFR; ++f) {
-        const int q = tid + TPB * f;
-        if (q < npf) pf[f] = fetch(dsplit ? q >> lg_sh : (int)kbag(keys[q >> lg_sh]), q & (LG - 1));
+        for (int f = 0; f < PFR; ++f) {
+            const int q = tid + TPB * f;
+            if (q < (n << lg_sh)) pf[f] = fetch((int)kbag(keys[q >> lg_sh]), q & (LG - 1));
+        }
     }
     CDIAG(2);
     const int64_t cb_s = cbv[s < SPLIT ? s : 0];
