@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -56,8 +57,18 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="terabyte", choices=sorted(CONFIGS))
-    p.add_argument("--mode", default="dp", choices=["dp", "fwd", "sgd"],
-                   help="dp: data-parallel QAT step; fwd: forward only; sgd: forward + fused sparse SGD")
+    p.add_argument("--mode", default="dp", choices=["dp", "fwd", "sgd", "dropin-sgd", "dropin-dp"],
+                   help="dp: data-parallel QAT step; fwd: forward only; sgd: forward + fused sparse SGD; "
+                        "dropin-sgd / dropin-dp: the reference drivers' call pattern through the drop-in "
+                        "modules and hooks (see dropin_main)")
+    p.add_argument("--dropin-form", default="list", choices=["list", "collection"],
+                   help="drop-in modes: the unchanged drivers' ModuleList of per-table QuantEmbeddingBagTwo, "
+                        "or one QuantEmbeddingBagCollection replacing apply_emb's loop")
+    p.add_argument("--grad-mode", default="sparse", choices=["sparse", "fused_sgd"],
+                   help="dropin-sgd: module grad_mode (sparse = torch.optim.SGD on the per-lookup COO)")
+    p.add_argument("--sync-every", type=int, default=0,
+                   help="dp mode: weight_syncc every K steps inside the timed region (the DP driver's "
+                        "replica averaging, every 200 iterations, dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1924-1936)")
     p.add_argument("--batch-per-gpu", type=int, default=2048,
                    help="samples per rank per step (weak scaling; reference TB mini-batch 2048)")
     p.add_argument("--global-batch", type=int, default=0,
@@ -100,10 +111,10 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "emb_fwd": "k_emb_fwd<{lpr},",
     "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
     "bwd_coalesce": ("k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),  # Criteo-form batches / general
-    "bwd_sgd": "k_bwd_fused<{lpr}, 0>",
+    "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "grad_quant_pack": "k_quant_pack<{lpr}>",
-    "apply_sparse_update": "k_apply_flat<{lpr}>",
-    "apply_local": "k_apply_local<{lpr}>",
+    "apply_sparse_update": "k_apply_flat<{lpr},",
+    "apply_local": "k_apply_local<{lpr},",
 }
 
 
@@ -118,8 +129,18 @@ def pmc_traffic(path, phase, D):
     for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
         if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
             return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
+                    "profiled_median_us": round(v["median_us"], 2) if v.get("median_us") else None,
                     "source": os.path.relpath(path, ROOT)}
     return None
+
+
+def latest_profile(tag):
+    """The newest round's committed rocprofv3 summary for a config (profiles/rN_<tag>_summary.json)."""
+    import glob
+
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{tag}_summary.json")),
+                   key=lambda p: int(re.match(r"r(\d+)_", os.path.basename(p)).group(1)))
+    return cands[-1] if cands else None
 
 
 def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
@@ -192,6 +213,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:  # gloo: functional rehearsal of the N>1 path (e.g. several ranks on one GPU)
             dist.init_process_group("gloo")
+    if a.mode.startswith("dropin"):
+        dropin_main(a, world, rank, dev)
+        return
     cfg = CONFIGS[a.config]
     rows, D = cfg["rows"], cfg["dim"]
     T = len(rows)
@@ -314,11 +338,28 @@ def main():
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
+    sync_every = a.sync_every if a.mode == "dp" else 0
+    if sync_every and a.graph:
+        print("--sync-every runs eager (no --graph)", file=sys.stderr)
+        sys.exit(2)
+    from deep_quantized_recommendation_model_dqrm_amd.sgd_quantized_gradients_parallel_comm import sync_table_set
+
     def run(i, ev=None):
         if graphs is None or (a.scale_period > 1 and i % a.scale_period == 0):
             step(i, ev, only=dj)
         elif i % gs == 0:  # steps i .. i+gs-1 (batches (i+j) % len(batches), as the eager run)
             graphs[(i % max(len(batches), gs)) // gs].replay()
+        if sync_every and (i + 1) % sync_every == 0:  # weight_syncc (checksum gate + local ring mean)
+            sync_table_set(ts, world)
+
+    sync_ms = None
+    if sync_every:  # the sync alone, outside the timed region (a few calls)
+        torch.cuda.synchronize()
+        t0s = time.perf_counter()
+        for _ in range(3):
+            sync_table_set(ts, world)
+        torch.cuda.synchronize()
+        sync_ms = (time.perf_counter() - t0s) / 3 * 1e3
 
     # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
     # it runs on) on every sample_every-th step, so the events barely perturb the timing
@@ -370,7 +411,7 @@ def main():
         replicas_match = all(torch.equal(allcs[0], c) for c in allcs)
     else:
         replicas_match = True
-    prof = a.traffic_profile or os.path.join(ROOT, "profiles", f"r2_{PROFILE_TAG[a.config]}_summary.json")
+    prof = a.traffic_profile or latest_profile(PROFILE_TAG[a.config])
     traffic = pmc_traffic(prof, dom, D)
     if rank == 0:
         value = B_global * a.steps / elapsed
@@ -420,6 +461,9 @@ def main():
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events "
                                "(apply_local and bwd_sgd include the |W| hierarchy finalize launch)",
+            "weight_syncc": ({"every": sync_every, "ms_per_call": round(sync_ms, 3),
+                              "amortized_us_per_step": round(sync_ms * 1e3 / sync_every, 2),
+                              "in_timed_region": True} if sync_every else None),
             "scale_refresh_ms": round(refresh_ms, 4) if refresh_ms is not None else None,
             "scale_refresh_note": ("full INT4 repack of all tables (worst case: every scale moved), once per "
                                    f"{a.scale_period} steps" if refresh_ms is not None else None),
@@ -441,6 +485,153 @@ def main():
     if err:  # a step that dropped or mis-indexed lookups is not a measurement
         print(f"device error flags 0x{err:x}", file=sys.stderr)
         sys.exit(3)
+
+
+def count_launches(fn, steps=3):
+    """Device kernels launched per call of fn (torch.profiler over `steps` calls; None when the
+    profiler cannot trace the device here)."""
+    try:
+        from torch.profiler import ProfilerActivity, profile
+
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for _ in range(steps):
+                fn()
+            torch.cuda.synchronize()
+        n = sum(1 for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA)
+        return round(n / steps, 1) if n else None
+    except Exception:  # noqa: BLE001 -- a measurement aid only
+        return None
+
+
+def dropin_main(a, world, rank, dev):
+    """The reference drivers' own call pattern through the drop-in (BASELINE configs 3-4),
+    timed as a whole step with its host work (module calls, autograd, optimizer, hooks):
+
+    dropin-sgd  dlrm_s_pytorch_single_gpu.py:609-674,1943-1950 -- apply_emb's per-table loop
+                over 26 QuantEmbeddingBagTwo (--dropin-form list) or one
+                QuantEmbeddingBagCollection (collection), backward from a fixed dL/dy, then
+                torch.optim.SGD.step() (grad_mode sparse: the per-lookup COO) or nothing
+                (fused_sgd: the update ran in the backward kernel);
+    dropin-dp   dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1888-1904 -- clear_gradients,
+                forward, backward, grad_update_parallel_comm(..., 8 bits),
+                weight_update_parallel_comm; a ModuleList is consolidated into one table set
+                by the hooks on first use.
+    The line also carries the direct-API step (EmbeddingTableSet / SparseGradExchange) at
+    the same shape, and the device launches per step."""
+    from torch import nn
+
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+    from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+
+    cfg = CONFIGS[a.config]
+    rows, D = cfg["rows"], cfg["dim"]
+    T = len(rows)
+    B_global = a.global_batch if a.global_batch > 0 else a.batch_per_gpu * world
+    B = B_global // world
+    dp = a.mode == "dropin-dp"
+    gm = "dp" if dp else a.grad_mode
+    Q.set_pooling_one_inputs(True)  # Criteo-form inputs (offsets = arange), as the drivers feed
+    t0 = time.time()
+    if a.dropin_form == "list":
+        emb = nn.ModuleList([Q.QuantEmbeddingBagTwo(n, D, 4, embedding_id=i, init="device", grad_mode=gm, lr=a.lr,
+                                                    device=dev) for i, n in enumerate(rows)])
+    else:
+        emb = Q.QuantEmbeddingBagCollection(rows, D, 4, init="device", grad_mode=gm, lr=a.lr, device=dev)
+    model = nn.Module()
+    model.emb_l, model.bot_l, model.top_l = emb, nn.ModuleList(), nn.ModuleList()
+    params = [p for p in model.parameters()]
+    opt = torch.optim.SGD(params, lr=a.lr) if (not dp and gm == "sparse") else None
+    batches = make_batches(rows, B_global, rank, world, a.num_batches, a.seed, a.index_dist, dev)
+    lS_o = torch.arange(B, dtype=torch.int64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(a.seed + rank)
+    dys = [torch.randn(B, D, device=dev, generator=g) * 0.05 for _ in range(T)]
+    setup_s = time.time() - t0
+
+    def step(i):
+        P = batches[i % len(batches)].idx.view(T, B)
+        if dp:
+            H.clear_gradients(model)
+        if a.dropin_form == "list":
+            ly = [emb[t](P[t], lS_o) for t in range(T)]
+        else:
+            ly = emb(lS_o.expand(T, B), P)
+        torch.autograd.backward(ly, dys)
+        if dp:
+            H.grad_update_parallel_comm(model, world, True, a.grad_bits)
+            H.weight_update_parallel_comm(model, a.lr, num_gpus=world)
+        elif opt is not None:
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+
+    for i in range(a.warmup):
+        step(i)
+    launches = count_launches(lambda: step(0))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tst = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - tst
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    errs = (emb[0]._tset if a.dropin_form == "list" else emb._tset).read_errors()
+    del model, emb, opt
+    torch.cuda.empty_cache()
+
+    # the direct-API step at the same shape, for comparison (same process, fresh tables)
+    ts = dq.EmbeddingTableSet(rows, D, device=dev, init="uniform", seed=a.seed)
+    ex = dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits) if dp else None
+    dyt = torch.stack(dys)
+
+    def direct(i):
+        b = batches[i % len(batches)]
+        ts.forward(b, bits=4)
+        if dp:
+            ex.step(b, dyt, a.lr)
+        else:
+            ts.backward_sgd(b, dyt, a.lr)
+
+    for i in range(a.warmup):
+        direct(i)
+    direct_launches = count_launches(lambda: direct(0))
+    torch.cuda.synchronize()
+    tdt = time.perf_counter()
+    for i in range(a.steps):
+        direct(a.warmup + i)
+    torch.cuda.synchronize()
+    direct_s = time.perf_counter() - tdt
+    if rank == 0:
+        us = elapsed / a.steps * 1e6
+        dus = direct_s / a.steps * 1e6
+        line = {
+            "metric": ("drop-in DP QAT-step samples/sec (ModuleList/collection + the four grad-comm hooks)" if dp else
+                       "drop-in single-GPU QAT-step samples/sec (modules + " +
+                       ("torch.optim.SGD)" if gm == "sparse" else "fused SGD in the backward)")),
+            "value": round(B_global * a.steps / elapsed, 1) if errs == 0 else None,
+            "unit": "samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(us / 1e3, 4), "us_per_step": round(us, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32 (int4 fake-quant activations)",
+            "data": "synthetic (uniform-random Criteo-form indices, device-initialised U(+-sqrt(1/n)) tables)",
+            "config": {"workload": f"criteo-{a.config} embedding {a.mode} ({a.dropin_form})", "tables": T,
+                       "total_rows": sum(rows), "emb_dim": D, "batch_per_gpu": B, "global_batch": B_global,
+                       "grad_mode": gm, "grad_bits": a.grad_bits if dp else None, "pooling": 1,
+                       "parallelism": f"dp{world} (tables replicated)"},
+            "launches_per_step": launches,
+            "direct_api": {"us_per_step": round(dus, 2), "launches_per_step": direct_launches,
+                           "dropin_over_direct": round(us / dus, 2)},
+            "device_errors": errs, "setup_s": round(setup_s, 1),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def gather_phase(a, ts, rows, T, D, dev):

@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_coalesce.hip", "dqrm_dense.hip",
-                                                "dqrm_input.hip")]
+                                                "dqrm_input.hip", "dqrm_sync.hip")]
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
 INTERNAL_HEADER = os.path.join(CSRC_DIR, "dqrm_internal.h")
 LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
@@ -57,17 +57,24 @@ def build(force: bool = False, verbose: bool = True) -> str:
     libdqrm.so next to this file."""
     if not force and not needs_build():
         return LIB_PATH
-    objs = []
-    for src in SOURCES:
+    objs, jobs = [], []
+    for src in SOURCES:  # translation units compile in parallel (one hipcc each)
         obj = _obj(src)
         if force or _stale(obj, [src, HEADER, INTERNAL_HEADER, __file__]):
             tmp = obj + ".tmp.o"
             cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-c", src, "-o", tmp]
             if verbose:
                 print("[dqrm] " + " ".join(cmd), file=sys.stderr)
-            subprocess.run(cmd, check=True)
-            os.replace(tmp, obj)
+            jobs.append((subprocess.Popen(cmd), cmd, tmp, obj))
         objs.append(obj)
+    failed = None
+    for proc, cmd, tmp, obj in jobs:
+        if proc.wait() != 0:
+            failed = failed or subprocess.CalledProcessError(proc.returncode, cmd)
+        elif failed is None:
+            os.replace(tmp, obj)
+    if failed is not None:
+        raise failed
     tmp = LIB_PATH + ".tmp"
     cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:

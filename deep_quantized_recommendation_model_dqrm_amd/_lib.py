@@ -25,6 +25,7 @@ DQRM_ERRF_OVERFLOW = 4
 DQRM_BLOCK_ROWS = 256
 DQRM_SBLOCK_ROWS = 65536
 DQRM_TABLE_SPLIT = 8
+DQRM_SYNC_STRIDE = 64
 DQRM_SLOT_KEYS = 8192
 
 DQRM_FWD_REFRESH_SCALE = 1
@@ -49,7 +50,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 3  # include/dqrm.h
+DQRM_ABI_VERSION = 4  # include/dqrm.h
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
@@ -80,6 +81,8 @@ EXPORTED_SYMBOLS = (
     "dqrm_rowwise_prepack",
     "dqrm_rowwise_bag",
     "dqrm_init_uniform",
+    "dqrm_checksum64",
+    "dqrm_replica_mean",
     "dqrm_read_errors",
     "dqrm_last_error",
     "dqrm_set_apply_kernel",
@@ -112,6 +115,7 @@ class TableSet(C.Structure):
         ("tflags", C.c_void_p),
         ("sdirty", C.c_void_p),
         ("bdirty", C.c_void_p),
+        ("sync", C.c_void_p),
     ]
 
 
@@ -224,6 +228,8 @@ def load(path: str | None = None) -> C.CDLL:
             [C.c_int, P, C.c_int64, C.c_int, P, C.c_int64, P, C.c_int64, C.c_int, P, P, P, P],
         ),
         "dqrm_init_uniform": (C.c_int, [TS, C.c_uint64, P]),
+        "dqrm_checksum64": (C.c_int, [P, C.c_int64, P, P]),
+        "dqrm_replica_mean": (C.c_int, [P, C.c_int64, C.c_int, C.c_float, P]),
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
         "dqrm_last_error": (C.c_char_p, []),
         "dqrm_set_apply_kernel": (C.c_int, [C.c_int]),

@@ -357,11 +357,56 @@ class MultiSetExchange:
         return self.absmax.numel() * 4, self.payload.numel()
 
 
+class ConsolidatedExchange:
+    """The exchange of a ModuleList of per-table modules whose tables live in ONE
+    consolidated set (quant_modules_not_quantize_grad.consolidate_tables): the modules'
+    pending (batch, dy) pairs are concatenated on the device (one copy each for the
+    indices, offsets and dy) and the step runs as ONE coalesce, ONE quantize-pack and ONE
+    apply for all tables (two collectives at N > 1) -- the launch count of a single
+    26-table set. At world size 1 with quantized gradients quantize-pack and apply run
+    fused at apply time (dqrm_apply_local), which also produces the averaged scales."""
+
+    def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None):
+        self.tables = tables
+        self.grad_bits = grad_bits
+        self.max_lookups = [int(max_lookups)] * tables.T
+        self.inner = SparseGradExchange(tables, max_lookups, grad_bits=grad_bits, group=group)
+        self.world = self.inner.world
+        self.fused = self.world == 1 and 2 <= grad_bits <= 16
+        self.scales = [self.inner.s_avg[t: t + 1] for t in range(tables.T)]
+        self._args = None
+
+    def exchange(self, items) -> list[torch.Tensor]:
+        batch = LookupBatch.concat([it[0] for it in items])
+        dy = torch.cat([it[1].reshape(1, batch.num_bags, -1) for it in items], dim=0)
+        ste, layout = items[0][2], items[0][3]
+        if any(it[2] != ste for it in items):
+            raise ValueError("modules differ in full_precision (STE) within one step")
+        if self.fused:
+            self.inner.kernels.coalesce(batch, dy, self.inner.ws, ste, "tbd")
+            self._args = (batch, dy)  # keep the inputs alive until the update
+        else:
+            self.inner.exchange(batch, dy, ste=ste, layout="tbd")
+        return self.scales
+
+    def apply(self, lr: float, mode: int | None = None, repack=False) -> None:
+        rp = any(repack) if isinstance(repack, (list, tuple)) else bool(repack)
+        if self.fused and (mode is None or mode == L.DQRM_UPD_DP):
+            self.inner.kernels.apply_local(self.inner.ws, self.grad_bits, self.inner.s_avg, lr, rp)
+        else:
+            self.inner.apply(lr, mode=mode, repack=rp)
+        self._args = None
+
+    @property
+    def scales_ready_after_apply(self) -> bool:
+        return self.fused
+
+
 def get_my_slice(n: int, my_size: int, my_rank: int) -> slice:
     """Contiguous per-rank batch slice (dlrm_s_pytorch_single_gpu.py:989-993)."""
     k, m = divmod(n, my_size)
     return slice(my_rank * k + min(my_rank, m), (my_rank + 1) * k + min(my_rank + 1, m), 1)
 
 
-__all__ = ["SparseGradExchange", "MultiSetExchange", "HipExchangeKernels", "payload_bytes", "get_my_slice",
-           "all_gather_into"]
+__all__ = ["SparseGradExchange", "MultiSetExchange", "ConsolidatedExchange", "HipExchangeKernels", "payload_bytes",
+           "get_my_slice", "all_gather_into"]

@@ -33,6 +33,8 @@
 // A table's 8 slots run on one XCD (block map below), so dy lines shared by the slices of a
 // dimension-split table come from one L2.
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 #include "../../include/dqrm.h"
@@ -921,16 +923,17 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 
 namespace dqrm_internal {
 
-int launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream) {
-    static bool lds_set = false;  // the attribute is per function, process-wide
-    if (!lds_set) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
-            return DQRM_E_HIP;
-        lds_set = true;
-    }
+hipError_t launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream) {
+    // the attribute is per function, process-wide: set once (thread-safe), re-checked each call
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    });
+    if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(k_coalesce_p1, dim3((a.T + 7) / 8 * 64), dim3(TPB), LDS_BYTES, stream, a);
-    return hipGetLastError() == hipSuccess ? DQRM_OK : DQRM_E_HIP;
+    return hipGetLastError();
 }
 
 }  // namespace dqrm_internal

@@ -31,7 +31,7 @@ struct CoalesceArgs {
 // largest B the Criteo-form coalesce kernel takes (larger batches use the general kernel)
 constexpr int64_t kCoalesceMaxB = 4096;
 
-// launches k_coalesce_p1 (dqrm_coalesce.hip); returns a DQRM_E_* code
-int launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream);
+// launches k_coalesce_p1 (dqrm_coalesce.hip); returns the HIP error of the launch
+hipError_t launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream);
 
 }  // namespace dqrm_internal

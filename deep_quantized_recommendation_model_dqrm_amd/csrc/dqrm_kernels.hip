@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <mutex>
 
 #include "../../include/dqrm.h"
 #include "dqrm_internal.h"
@@ -148,6 +149,82 @@ DQRM_INLINE uint16_t pack4_int4(float q0, float q1, float q2, float q3) {
 }
 
 DQRM_INLINE void flag_error(uint32_t* err, uint32_t f) { atomicOr(err, f); }
+
+// ------------------------------------------------------------------------------------
+// In-launch hand-off of the |W| hierarchy to a table's last workgroup (no finalize launch).
+// MI355X_MICROARCH.md "inter-workgroup visibility", hand-off row 1: every byte the last
+// workgroup reads was stored write-through (sc1 stores, or device-scope atomics), every
+// storing wave waits vmcnt(0), a workgroup barrier, then ONE lane adds to the table's
+// arrival counter; the workgroup whose add returns expected-1 reads with sc1 loads only.
+// No L2 write-back (release fence) and no L1 invalidate (acquire) on either side.
+// ------------------------------------------------------------------------------------
+DQRM_INLINE void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DQRM_INLINE float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DQRM_INLINE uint32_t ld_wt(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-B write-through store (global_store_dwordx4 ... sc1)
+DQRM_INLINE void st4_wt(float4* p, float4 v) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+}
+// W stores of a narrow table (<= 256 rows: finalize rebuilds its maxima from W) go write-through
+DQRM_INLINE void st4_w(float4* p, float4 v, bool wt) {
+    if (wt) st4_wt(p, v); else *p = v;
+}
+DQRM_INLINE void st_w(float* p, float v, bool wt) {
+    if (wt) st_wt(p, v); else *p = v;
+}
+
+// dirty flags (u8 arrays sdirty / bdirty) are set / cleared by device-scope atomics on their
+// aligned 32-bit word and read with sc1 word loads (the arrays are padded to whole words)
+DQRM_INLINE uint32_t* flag_word(const uint8_t* f, int64_t i, int* sh) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(f + i);
+    *sh = (int)(a & 3u) * 8;
+    return reinterpret_cast<uint32_t*>(a & ~(uintptr_t)3u);
+}
+DQRM_INLINE void flag_set(uint8_t* f, int64_t i) {
+    int sh;
+    uint32_t* w = flag_word(f, i, &sh);
+    atomicOr(w, 1u << sh);
+}
+DQRM_INLINE void flag_clear(uint8_t* f, int64_t i) {
+    int sh;
+    uint32_t* w = flag_word(f, i, &sh);
+    atomicAnd(w, ~(0xFFu << sh));
+}
+DQRM_INLINE bool flag_get(const uint8_t* f, int64_t i) {
+    int sh;
+    const uint32_t* w = flag_word(f, i, &sh);
+    return ((ld_wt(w) >> sh) & 0xFFu) != 0u;
+}
+
+// loads of the finalize: sc1 inside the updating launch (WT), plain in a launch of its own
+template <bool WT> DQRM_INLINE float ld_h(const float* p) { if constexpr (WT) return ld_wt(p); else return *p; }
+template <bool WT> DQRM_INLINE uint32_t ld_h(const uint32_t* p) { if constexpr (WT) return ld_wt(p); else return *p; }
+template <bool WT> DQRM_INLINE bool flag_get_h(const uint8_t* f, int64_t i) {
+    int sh;
+    const uint32_t* w = flag_word(f, i, &sh);
+    return ((ld_h<WT>(w) >> sh) & 0xFFu) != 0u;
+}
+
+// All threads of the workgroup call this after their last store for table t; returns
+// (uniformly) whether this is the last of the `expected` arriving workgroups. The last one
+// re-arms the counter for the next launch.
+DQRM_INLINE bool arrive_last(uint32_t* cnt, uint32_t expected) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics have landed
+    __syncthreads();                                   // ... and every other wave's
+    if (threadIdx.x == 0) {
+        const uint32_t old = atomicAdd(cnt, 1u);
+        const bool last = old + 1u == expected;
+        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = last ? 1 : 0;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
 
 // ------------------------------------------------------------------------------------
 // K0: synthetic init, U(-sqrt(1/n), sqrt(1/n)) per table (q_m_n_q_g.py:273-275 distribution)
@@ -1121,7 +1198,7 @@ DQRM_INLINE void staged_long_segments(const SlotLds& L, int U, int n, const uint
 // ------------------------------------------------------------------------------------
 DQRM_INLINE void update_superblock(float* sblkmax, uint8_t* sdirty, int64_t sb, float old_blk, float nb) {
     const float old_sb = sblkmax[sb];
-    if (old_blk == old_sb && nb < old_blk) sdirty[sb] = 1;
+    if (old_blk == old_sb && nb < old_blk) flag_set(sdirty, sb);
     if (nb > old_sb) atomicMax(reinterpret_cast<unsigned int*>(sblkmax) + sb, __float_as_uint(nb));
 }
 
@@ -1158,7 +1235,7 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
             continue;
         }
         const float nb = fmaxf(old_blk, cand);
-        blkmax[bb + blk] = nb;
+        st_wt(blkmax + bb + blk, nb);
         update_superblock(sblkmax, sdirty, sbb + (blk >> 8), old_blk, nb);
     }
     __syncthreads();
@@ -1176,7 +1253,7 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
         v = wave_max(v);
         if (lane == 0) {
             const float old_blk = blkmax[bb + blk];
-            blkmax[bb + blk] = v;
+            st_wt(blkmax + bb + blk, v);
             update_superblock(sblkmax, sdirty, sbb + (blk >> 8), old_blk, v);
         }
     }
@@ -1185,18 +1262,32 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
 // Per table, after its slot workgroups: re-reduce flagged superblocks, then tmax over all
 // superblocks. Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their
 // rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats).
+template <bool WT>
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
                                int D, bool tracked) {
+    // Every load below is an sc1 (write-through) load: this runs either as its own launch or
+    // in the table's last workgroup of the updating kernel (arrive_last), whose producers
+    // stored the hierarchy write-through.
     __shared__ float red[16];
     __shared__ int s_rescan;
     if (m.num_rows[t] <= BLK) {
         const int64_t grow = m.row_base[t] + threadIdx.x;
         float v = 0.0f;
         if (threadIdx.x < m.num_rows[t]) {
-            const float4* wr = reinterpret_cast<const float4*>(W + grow * D);
-            for (int k = 0; k < D / 4; ++k) v = fmaxf(v, abs_max4(wr[k]));
+            const float* wr = W + grow * D;
+            if constexpr (WT) {
+                for (int k0 = 0; k0 < D; k0 += 16) {  // 16 loads in flight
+                    float x[16];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) x[j] = k0 + j < D ? ld_h<WT>(wr + k0 + j) : 0.0f;
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) v = fmaxf(v, fabsf(x[j]));
+                }
+            } else {
+                for (int k = 0; k < D / 4; ++k) v = fmaxf(v, abs_max4(reinterpret_cast<const float4*>(wr)[k]));
+            }
             rowmax[grow] = v;
         }
         v = wave_max(v);
@@ -1207,8 +1298,8 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) r = fmaxf(r, red[k]);
             blkmax[m.blk_base[t]] = r;
             sblkmax[m.sblk_base[t]] = r;
-            sdirty[m.sblk_base[t]] = 0;
-            bdirty[m.blk_base[t]] = 0;
+            if (flag_get_h<WT>(sdirty, m.sblk_base[t])) flag_clear(sdirty, m.sblk_base[t]);
+            if (flag_get_h<WT>(bdirty, m.blk_base[t])) flag_clear(bdirty, m.blk_base[t]);
             tmax[t] = r;
         }
         return;
@@ -1220,80 +1311,108 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     constexpr int U4 = 4;  // loads in flight per thread
     // tracked (flat apply kernels): tmax already holds every grown row max (atomicMax), so
     // the table-wide rescan is needed only if a rescanned superblock held the table max
-    const float tmax0 = tracked ? tmax[t] : 0.0f;
+    const float tmax0 = tracked ? ld_h<WT>(tmax + t) : 0.0f;
     if (threadIdx.x == 0) s_rescan = tracked ? 0 : 1;
     __syncthreads();
-    for (int64_t k0 = (int64_t)w * WAVE * U4; k0 < ns; k0 += (int64_t)nw * WAVE * U4) {
-        bool d[U4];
+    // the table's superblock flags, 4 per 32-bit word (word 0 holds superblock 0 at byte sh0)
+    int sh0;
+    const uint32_t* sdw = flag_word(sdirty, sbb, &sh0);
+    sh0 /= 8;
+    const int64_t nwords = (ns + sh0 + 3) / 4;
+    // one superblock whose max holder shrank, by one wave: re-reduce its flagged blocks' 256
+    // rowmax (the owning lane keeps the new block max in a register), then the superblock
+    auto fix_superblock = [&](int64_t sb) {
+        const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+        float nv[SBLK_BLOCKS / WAVE];
+        bool dq[SBLK_BLOCKS / WAVE];
+        const float old_sb = ld_h<WT>(sblkmax + sbb + sb);  // with the flags and block maxima: one round trip
 #pragma unroll
-        for (int j = 0; j < U4; ++j) {
-            const int64_t k = k0 + j * WAVE + lane;
-            d[j] = k < ns && sdirty[sbb + k];
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+            const int64_t b = b0 + lane + q * WAVE;
+            dq[q] = b < b1 && flag_get_h<WT>(bdirty, bb + b);
+            nv[q] = b < b1 ? ld_h<WT>(blkmax + bb + b) : 0.0f;
         }
 #pragma unroll
-        for (int j = 0; j < U4; ++j) {
-            uint64_t msk = __ballot(d[j]);
-            while (msk) {  // rare: a superblock's max holder shrank
-                const int l = __ffsll((long long)msk) - 1;
-                msk &= msk - 1;
-                const int64_t sb = k0 + j * WAVE + l;
-                const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-                // blocks the flat apply flagged (a max holder shrank): re-reduce their 256 rowmax
-                // (wave-cooperative; the owning lane keeps the new value in a register)
-                // the superblock's dirty flags, block maxima and old max in one round trip
-                float nv[SBLK_BLOCKS / WAVE];
-                bool dq[SBLK_BLOCKS / WAVE];
-                const float old_sb = sblkmax[sbb + sb];
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+            uint64_t dm = __ballot(dq[q]);
+            while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
+                constexpr int DB = 8;
+                int dl[DB];
+                float x[DB];
 #pragma unroll
-                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-                    const int64_t b = b0 + lane + q * WAVE;
-                    dq[q] = b < b1 && bdirty[bb + b];
-                    nv[q] = b < b1 ? blkmax[bb + b] : 0.0f;
+                for (int i = 0; i < DB; ++i) {
+                    dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
+                    dm &= dm ? dm - 1 : 0;
                 }
 #pragma unroll
-                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-                    uint64_t dm = __ballot(dq[q]);
-                    while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
-                        constexpr int DB = 8;
-                        int dl[DB];
-                        float x[DB];
+                for (int i = 0; i < DB; ++i) {
+                    x[i] = 0.0f;
+                    if (dl[i] < 0) continue;
+                    const int64_t blk = b0 + q * WAVE + dl[i];
 #pragma unroll
-                        for (int i = 0; i < DB; ++i) {
-                            dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
-                            dm &= dm ? dm - 1 : 0;
-                        }
-#pragma unroll
-                        for (int i = 0; i < DB; ++i) {
-                            x[i] = 0.0f;
-                            if (dl[i] < 0) continue;
-                            const int64_t blk = b0 + q * WAVE + dl[i];
-#pragma unroll
-                            for (int k = 0; k < BLK / WAVE; ++k) {
-                                const int64_t rr = blk * BLK + lane + k * WAVE;
-                                if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], rowmax[m.row_base[t] + rr]);
-                            }
-                        }
-#pragma unroll
-                        for (int i = 0; i < DB; ++i) {
-                            if (dl[i] < 0) continue;
-                            const float y = wave_max(x[i]);
-                            if (lane == dl[i]) nv[q] = y;
-                        }
+                    for (int k = 0; k < BLK / WAVE; ++k) {
+                        const int64_t rr = blk * BLK + lane + k * WAVE;
+                        if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], ld_h<WT>(rowmax + m.row_base[t] + rr));
                     }
-                    if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; bdirty[b0 + lane + q * WAVE + bb] = 0; }
                 }
-                float v = 0.0f;
 #pragma unroll
-                for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
-                v = wave_max(v);
-                if (lane == 0) {
-                    sblkmax[sbb + sb] = v;
-                    sdirty[sbb + sb] = 0;
-                    if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
+                for (int i = 0; i < DB; ++i) {
+                    if (dl[i] < 0) continue;
+                    const float y = wave_max(x[i]);
+                    if (lane == dl[i]) nv[q] = y;
+                }
+            }
+            if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; flag_clear(bdirty, b0 + lane + q * WAVE + bb); }
+        }
+        float v = 0.0f;
+#pragma unroll
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
+        v = wave_max(v);
+        if (lane == 0) {
+            sblkmax[sbb + sb] = v;
+            flag_clear(sdirty, sbb + sb);
+            if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
+        }
+    };
+    // 1. list the flagged superblocks in LDS (one scan of the flag words); 2. one wave per
+    // listed superblock. A list that overflows is finished by another scan (the fixed
+    // superblocks' flags are clear by then).
+    constexpr int FIN_LIST = 128;
+    __shared__ int s_dl[FIN_LIST];
+    __shared__ int s_dn;
+    for (;;) {
+        if (threadIdx.x == 0) s_dn = 0;
+        __syncthreads();
+        for (int64_t k0 = (int64_t)threadIdx.x; k0 < nwords; k0 += (int64_t)blockDim.x * U4) {
+            uint32_t fw[U4];
+#pragma unroll
+            for (int j = 0; j < U4; ++j) {
+                const int64_t k = k0 + (int64_t)j * blockDim.x;
+                uint32_t x = k < nwords ? ld_h<WT>(sdw + k) : 0u;
+                if (k == 0) x &= 0xFFFFFFFFu << (8 * sh0);            // bytes before superblock 0
+                const int64_t nb = ns + sh0 - k * 4;                   // valid bytes in this word
+                if (nb < 4) x &= nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u);
+                fw[j] = x;
+            }
+#pragma unroll
+            for (int j = 0; j < U4; ++j) {
+                uint32_t x = fw[j];
+                while (x) {  // rare: a superblock's max holder shrank
+                    const int by = (__ffs((int)x) - 1) / 8;
+                    x &= ~(0xFFu << (8 * by));
+                    const int p = atomicAdd(&s_dn, 1);
+                    if (p < FIN_LIST) s_dl[p] = (int)((k0 + (int64_t)j * blockDim.x) * 4 + by - sh0);
                 }
             }
         }
+        __syncthreads();
+        const int nd = s_dn;
+        for (int i = w; i < nd && i < FIN_LIST; i += nw) fix_superblock(s_dl[i]);
+        if (nd <= FIN_LIST) break;  // uniform
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cleared flags land before the next scan
+        __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new superblock maxima reach L2 first
     __syncthreads();
     if (!s_rescan) return;  // uniform: tmax is exact already
     float v = 0.0f;
@@ -1302,7 +1421,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < U4; ++j) {
             const int64_t k = k0 + (int64_t)j * blockDim.x;
-            x[j] = k < ns ? sblkmax[sbb + k] : 0.0f;
+            x[j] = k < ns ? ld_h<WT>(sblkmax + sbb + k) : 0.0f;
         }
 #pragma unroll
         for (int j = 0; j < U4; ++j) v = fmaxf(v, x[j]);
@@ -1327,7 +1446,7 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
                                                          const int64_t* __restrict__ meta, int T, int D,
                                                          int tracked) {
     const Meta m = make_meta(meta, T);
-    finalize_table(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0);
+    finalize_table<false>(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -1369,7 +1488,7 @@ DQRM_INLINE void visit_slot_lookups(const int64_t* off, const int64_t* idx, int6
         for (int k = 0; k < GB; ++k) {  // validate, then the first index of every bag in flight
             const int64_t b = bs + k;
             int64_t s0 = o[k], s1 = o[k + 1];
-            if (b < b1 && (s0 < 0 || s1 > L || s1 < s0)) {
+            if (b < b1 && (s0 < 0 || s1 > L || s1 < s0 || (b == 0 && s0 != 0))) {  // off[0] must be 0
                 if (report) flag_error(err, DQRM_ERRF_OFFSET);
                 s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
                 s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
@@ -1590,6 +1709,9 @@ struct ApplyArgs {
     uint8_t* sdirty;
     uint8_t* bdirty;
     float* tmax;
+    uint32_t* sync;
+    int fin_launch;    // 1: the |W| hierarchy is finalized by a separate k_table_finalize launch
+    int wt;            // rowmax / narrow-table W stores write-through (needed by the in-launch finalize)
     const float* pscale;
     const int64_t* meta;
     uint32_t* err;
@@ -1684,13 +1806,13 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
         float4 w = st.w;
         w.x = update(w.x, st.acc.x); w.y = update(w.y, st.acc.y);
         w.z = update(w.z, st.acc.z); w.w = update(w.w, st.acc.w);
-        reinterpret_cast<float4*>(a.W + grow * D)[off4 + sub] = w;
+        st4_w(reinterpret_cast<float4*>(a.W + grow * D) + off4 + sub, w, dsplit);
         if (a.repack) pack4_row(w, a.packed + grow * (D / 2), off4 + sub, r_pack);
         if (!dsplit) {
             const float old_rm = group_max<LPRS>(abs_max4(st.w));
             const float rm = group_max<LPRS>(abs_max4(w));
             if (sub == 0) {
-                a.rowmax[grow] = rm;
+                st_wt(a.rowmax + grow, rm);
                 keys[i] = with_lo(keys[i], row_record(rm, old_rm, st.blk));
             }
         }
@@ -1712,12 +1834,12 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
 #pragma unroll
         for (int d = 0; d < DL::NDL; ++d) w[d] = update(w[d], acc[d]);
 #pragma unroll
-        for (int d = 0; d < DL::NDL; ++d) a.W[grow * D + off4 * 4 + lig + DL::GD * d] = w[d];
+        for (int d = 0; d < DL::NDL; ++d) st_w(a.W + grow * D + off4 * 4 + lig + DL::GD * d, w[d], dsplit);
         if (a.repack) dl_pack_int4<LPRS>(w, a.packed + grow * (D / 2), off4 * 4, lig, r_pack);
         if (!dsplit) {
             const float rm = dl_absmax<LPRS>(w);
             if (lig == 0) {
-                a.rowmax[grow] = rm;
+                st_wt(a.rowmax + grow, rm);
                 keys[i] = with_lo(keys[i], row_record(rm, old_rm, old_blk));
             }
         }
@@ -1725,15 +1847,24 @@ DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t*
     const int nlong = compact_long(heads, U, n, s_long, s_wsum);
     DIAG_T(3);
     staged_long_segments<LPRS, OP_SUM>(sl, U, n, s_long, nlong, s_wsum, src, 0.0f, fbegin, fend);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rowmax stores land before maintain_blocks reads them
     __syncthreads();
     DIAG_T(4);
     if (!dsplit) maintain_blocks(m, t, sl, U, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, s_wsum + TWG / WAVE + 2);
 }
 
 DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x);
+// a workgroup's queue of shrunk block-max holders whose blocks it owns (k_apply_local)
+struct OwnQueue {
+    int* cnt;
+    uint32_t* blk;
+    float* old;
+};
+constexpr int OWN_QCAP = 64;
 template <int LPR>
 DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
-                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub);
+                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub,
+                                 bool owned = false, const OwnQueue* oq = nullptr);
 
 // A slot whose merged entries exceed SLOT_KEYS (LDS sort capacity): k_apply_flat's method
 // restricted to the slot. Every rank's slot rows are ascending, so the entry of row x in
@@ -1802,6 +1933,9 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     const int T = a.T;
     const int D = LPR * 4;
     Meta m = make_meta(a.meta, T);
+    // the slot's work; then all SPLIT workgroups of the table arrive and the last one
+    // finalizes the table's |W| hierarchy (untracked: block-level maintenance, tmax rescan)
+    [&]() {
     const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
     DIAG_T(0);
     const int64_t cap = a.cap_base[t + 1] - a.cap_base[t];
@@ -1870,6 +2004,9 @@ __global__ void __launch_bounds__(TWG) k_table_apply(ApplyArgs a) {
     else
         apply_segments<LPR, LPR>(a, sl, s_long, s_wsum, m, t, U, n, 0, false, pl);
     DIAG_T(5);
+    }();
+    if (!a.fin_launch && arrive_last(a.sync + (int64_t)t * DQRM_SYNC_STRIDE, SPLIT))
+        finalize_table<true>(m, t, a.W, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, a.bdirty, a.tmax, D, false);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1914,7 +2051,8 @@ constexpr int FLAT_TPB = 256;
 // read it (then the block max is that grower's current value) or the holder is flagged.
 template <int LPR>
 DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
-                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub) {
+                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub,
+                                 bool owned, const OwnQueue* oq) {
     constexpr int D = LPR * 4;
     const int64_t blk = x >> 8;
     const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
@@ -1922,13 +2060,14 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
     float4 w;
     w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
     w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
-    reinterpret_cast<float4*>(a.W + grow * D)[sub] = w;
+    // narrow tables are rebuilt from W by finalize (write-through: it may run in this launch)
+    st4_w(reinterpret_cast<float4*>(a.W + grow * D) + sub, w, nrows <= BLK && a.wt);
     if (a.repack) pack4_row(w, a.packed + grow * (D / 2), sub, r_pack);
     const float old_rm = group_max<LPR>(abs_max4(w0));
     const float rm = group_max<LPR>(abs_max4(w));
     if (sub == 0) {
-        a.rowmax[grow] = rm;
-        if (nrows > BLK) {  // narrow tables are rebuilt from W by finalize
+        st_w(a.rowmax + grow, rm, a.wt);
+        if (nrows > BLK) {
             const int64_t sb = sbb + (blk >> 8);
             if (rm > old_blk) {
                 atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
@@ -1938,8 +2077,15 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
                 }
             }
             if (old_rm == old_blk && rm < old_rm) {
-                a.bdirty[bb + blk] = 1;
-                a.sdirty[sb] = 1;
+                int p = OWN_QCAP;
+                if (owned && oq) {  // the workgroup holds every touched row of this block: it re-reduces it
+                    p = atomicAdd(oq->cnt, 1);
+                    if (p < OWN_QCAP) { oq->blk[p] = (uint32_t)blk; oq->old[p] = old_blk; }
+                }
+                if (p >= OWN_QCAP) {  // the finalize launch re-reduces the block
+                    flag_set(a.bdirty, bb + blk);
+                    flag_set(a.sdirty, sb);
+                }
             }
         }
     }
@@ -1951,7 +2097,7 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
 // quantizes its coalesced entries with k_quant_pack's rounding and applies them with
 // k_apply_flat's update: the same values the payload round trip produces, without
 // writing and re-reading the payload.
-template <int LPR>
+template <int LPR, bool FIN>  // FIN: the table's last working workgroup finalizes its |W| hierarchy
 __global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int64_t* __restrict__ ws_cap_base,
                                                           const int32_t* __restrict__ ws_rows,
                                                           const float* __restrict__ ws_vals,
@@ -1961,9 +2107,26 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int
     constexpr int D = LPR * 4;
     constexpr int G = FLAT_TPB / LPR;
     const int k = blockIdx.y, t = k / SPLIT;
-    const int64_t cap = ws_cap_base[k + 1] - ws_cap_base[k];
-    int cnt = ws_ucount[k];
-    cnt = cnt < 0 ? 0 : (cnt > cap ? (int)cap : cnt);
+    // the table's slot counts: this slot's work, and how many workgroups of the table work
+    // (each arrives once; the last one finalizes the table's |W| hierarchy)
+    int cnt = 0;
+    uint32_t expected = 0;
+    if constexpr (FIN) {
+#pragma unroll
+        for (int ss = 0; ss < SPLIT; ++ss) {
+            const int kk = t * SPLIT + ss;
+            const int64_t cp = ws_cap_base[kk + 1] - ws_cap_base[kk];
+            int c = ws_ucount[kk];
+            c = c < 0 ? 0 : (c > cp ? (int)cp : c);
+            if (kk == k) cnt = c;
+            const uint32_t wgs = (uint32_t)((c + G - 1) / G);
+            expected += wgs < gridDim.x ? wgs : gridDim.x;
+        }
+    } else {
+        const int64_t cp = ws_cap_base[k + 1] - ws_cap_base[k];
+        cnt = ws_ucount[k];
+        cnt = cnt < 0 ? 0 : (cnt > cp ? (int)cp : cnt);
+    }
     const bool writer = blockIdx.x == 0 && k % SPLIT == 0;  // s_avg[t], even for an empty slot
     if ((int64_t)blockIdx.x * G >= cnt && !writer) return;
     float am = 0.0f;
@@ -1979,9 +2142,23 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int
     const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
     const int64_t src0 = ws_cap_base[k];
     const int sub = threadIdx.x % LPR;
+    // FIN = false: a block whose entries all fall in this workgroup's chunk is OWNED here (the
+    // slot's rows are ascending, so another entry of the block would be the chunk's neighbour
+    // entry): a shrunk holder of such a block is re-reduced below instead of being flagged
+    __shared__ int s_oq_n;
+    __shared__ uint32_t s_oq_blk[OWN_QCAP];
+    __shared__ float s_oq_old[OWN_QCAP];
+    const OwnQueue oq{&s_oq_n, s_oq_blk, s_oq_old};
+    if (!FIN) {
+        if (threadIdx.x == 0) s_oq_n = 0;
+        __syncthreads();
+    }
     for (int e = blockIdx.x * G + threadIdx.x / LPR; e < cnt; e += gridDim.x * G) {
         const int32_t x = ws_rows[src0 + e];
         const float4 v = reinterpret_cast<const float4*>(ws_vals + (src0 + e) * D)[sub];
+        const int c0 = e - (int)(threadIdx.x / LPR);  // the chunk's first entry
+        const int32_t xlo = (!FIN && c0 > 0) ? ws_rows[src0 + c0 - 1] : -1;
+        const int32_t xhi = (!FIN && c0 + G < cnt) ? ws_rows[src0 + c0 + G] : -1;
         if (x < 0 || x >= nrows) {  // cannot happen for a workspace this library coalesced
             if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
             continue;
@@ -1989,11 +2166,40 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int
         float4 acc;  // + 0.0f: the payload's integer round trip turns -0 into +0
         acc.x = fake_quant(v.x, rr, qlo, qhi) + 0.0f; acc.y = fake_quant(v.y, rr, qlo, qhi) + 0.0f;
         acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
-        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
+        const bool owned = !FIN && (xlo < 0 || (xlo >> 8) != (x >> 8)) && (xhi < 0 || (xhi >> 8) != (x >> 8));
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub, owned, FIN ? nullptr : &oq);
+    }
+    if constexpr (!FIN) {  // owned blocks whose max holder shrank: re-reduce their 256 row maxima
+        __syncthreads();
+        const int nq = s_oq_n < OWN_QCAP ? s_oq_n : OWN_QCAP;
+        if (nq > 0) {  // uniform; rare
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's row maxima have landed
+            __syncthreads();
+            const int lane = threadIdx.x % WAVE;
+            for (int q = threadIdx.x / WAVE; q < nq; q += FLAT_TPB / WAVE) {
+                const int64_t blk = s_oq_blk[q];
+                float mv = 0.0f;
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) {
+                    const int64_t r = blk * BLK + lane + i * WAVE;
+                    if (r < nrows) mv = fmaxf(mv, ld_wt(a.rowmax + rb + r));  // sc1: past any stale L1 line
+                }
+                mv = wave_max(mv);
+                if (lane == 0) {
+                    a.blkmax[bb + blk] = mv;
+                    const int64_t sb = sbb + (blk >> 8);
+                    if (mv < s_oq_old[q] && s_oq_old[q] == a.sblkmax[sb]) flag_set(a.sdirty, sb);  // held the superblock max
+                }
+            }
+        }
+    }
+    if constexpr (FIN) {
+        if (arrive_last(a.sync + (int64_t)t * DQRM_SYNC_STRIDE, expected))
+            finalize_table<true>(m, t, a.W, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, a.bdirty, a.tmax, D, true);
     }
 }
 
-template <int LPR>
+template <int LPR, bool FIN>
 __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     constexpr int D = LPR * 4;
     constexpr int G = FLAT_TPB / LPR;               // entries per workgroup pass
@@ -2007,6 +2213,14 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     const unsigned char* pr = a.payloads + (int64_t)r * a.payload_bytes;
     const int cnt_r = table_entry_count(pr, t, cap);
     if ((int64_t)blockIdx.x * G >= cnt_r) return;
+    // workgroups of table t that work, over all ranks' payloads (each arrives once)
+    uint32_t expected = 0;
+    if (FIN)
+    for (int j = 0; j < N; ++j) {
+        const uint32_t wgs =
+            (uint32_t)((table_entry_count(a.payloads + (int64_t)j * a.payload_bytes, t, cap) + G - 1) / G);
+        expected += wgs < gridDim.x ? wgs : gridDim.x;
+    }
     const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
     const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
     const ApplyUpdate update{a.mode, (float)(1.0 / (double)N), sc, (float)((double)sc / (double)N), a.nlr};
@@ -2047,6 +2261,10 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
             }
         }
         flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
+    }
+    if constexpr (FIN) {
+        if (arrive_last(a.sync + (int64_t)t * DQRM_SYNC_STRIDE, expected))
+            finalize_table<true>(m, t, a.W, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, a.bdirty, a.tmax, D, true);
     }
 }
 
@@ -2377,6 +2595,8 @@ struct FArgs {
     float* tmax;
     uint8_t* sdirty;
     uint8_t* bdirty;
+    uint32_t* sync;
+    int fin_launch;
     const float* scale;
     const float* pscale;
     const int64_t* meta;
@@ -2443,7 +2663,7 @@ DQRM_INLINE float4 seg_op4(float4 acc, float4 v, float nlr) {
 // |W| hierarchy upkeep of one updated row of a wide table (see flat_row_update)
 DQRM_INLINE void fused_row_upkeep(const FArgs& a, int t, int64_t grow, uint32_t x, int64_t bb, int64_t sbb,
                                   float old_rm, float rm, float old_blk) {
-    a.rowmax[grow] = rm;
+    st_wt(a.rowmax + grow, rm);
     const int64_t blk = x >> 8;
     const int64_t sb = sbb + (blk >> 8);
     if (rm > old_blk) {
@@ -2454,8 +2674,8 @@ DQRM_INLINE void fused_row_upkeep(const FArgs& a, int t, int64_t grow, uint32_t 
         }
     }
     if (old_rm == old_blk && rm < old_rm) {
-        a.bdirty[bb + blk] = 1;
-        a.sdirty[sb] = 1;
+        flag_set(a.bdirty, bb + blk);
+        flag_set(a.sdirty, sb);
     }
 }
 
@@ -2492,14 +2712,15 @@ DQRM_INLINE void fused_write(const FArgs& a, const FOut& o, int u, uint32_t x, f
         }
         amax = fmaxf(amax, abs_max4(acc));
     } else {
-        reinterpret_cast<float4*>(a.W + grow * D)[o.q0 + lane] = acc;
+        // narrow (dim-split) tables: write-through, the table's last workgroup rebuilds from W
+        st4_w(reinterpret_cast<float4*>(a.W + grow * D) + o.q0 + lane, acc, !o.wide_upkeep);
         if (a.repack) pack4_row(acc, a.packed + grow * (D / 2), o.q0 + lane, o.r_pack);
         if (o.wide_upkeep) {
             const float old_rm = group_max<LG>(abs_max4(wold));
             const float rm = group_max<LG>(abs_max4(acc));
             if (lane == 0) {
                 if (o.bgrow) {
-                    a.rowmax[grow] = rm;
+                    st_wt(a.rowmax + grow, rm);
                     const int jb = (int)((x >> 8) - o.b0s);
                     atomicMax(&o.bgrow[jb], __float_as_uint(rm));
                     if (old_rm == oblk && rm < old_rm) o.bshr[jb] = 1u;
@@ -2749,7 +2970,7 @@ DQRM_INLINE void fused_segments_staged(const FArgs& a, const FOut& o, const uint
                 for (int d = 0; d < NDL; ++d) amax = fmaxf(amax, fabsf(acc[d]));
             } else {
 #pragma unroll
-                for (int d = 0; d < NDL; ++d) a.W[grow * D + dim0 + lig + GL * d] = acc[d];
+                for (int d = 0; d < NDL; ++d) st_w(a.W + grow * D + dim0 + lig + GL * d, acc[d], !o.wide_upkeep);
                 if (a.repack) {  // even lanes pack their nibble with the odd neighbour's
 #pragma unroll
                     for (int d = 0; d < NDL; ++d) {
@@ -2766,7 +2987,7 @@ DQRM_INLINE void fused_segments_staged(const FArgs& a, const FOut& o, const uint
                     const float rm = group_max<GL>(mx);
                     if (lig == 0) {
                         if (o.bgrow) {
-                            a.rowmax[grow] = rm;
+                            st_wt(a.rowmax + grow, rm);
                             const int jb = (int)((x >> 8) - o.b0s);
                             atomicMax(&o.bgrow[jb], __float_as_uint(rm));
                             if (orm == oblk && rm < orm) o.bshr[jb] = 1u;
@@ -2944,15 +3165,15 @@ DQRM_INLINE void fused_slot(const FArgs& a, unsigned char* lds, int k, int t, in
             const float old_blk = a.blkmax[o.bb + blk];
             const int64_t sb = o.sbb + (blk >> 8);
             if (cand > old_blk) {
-                a.blkmax[o.bb + blk] = cand;
+                st_wt(a.blkmax + o.bb + blk, cand);
                 if (cand > a.sblkmax[sb]) {
                     atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(cand));
                     if (cand > a.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(cand));
                 }
             }
             if (s_bshr[threadIdx.x]) {
-                a.bdirty[o.bb + blk] = 1;
-                a.sdirty[sb] = 1;
+                flag_set(a.bdirty, o.bb + blk);
+                flag_set(a.sdirty, sb);
             }
         }
     }
@@ -3021,6 +3242,278 @@ __global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
     }
     DIAG_W(5);
     DIAG_C(15);
+    // SGD / local update: the table's last slot workgroup finalizes its |W| hierarchy
+    if (MODE != 1 && !a.fin_launch && arrive_last(a.sync + (int64_t)t * DQRM_SYNC_STRIDE, SPLIT))
+        finalize_table<true>(m, t, a.W, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, a.bdirty, a.tmax, LPR * 4, true);
+}
+
+// ------------------------------------------------------------------------------------
+// K4 SGD for small batches (BASELINE config 3: Kaggle, B = 128): ONE workgroup per table
+// owns all of the table's lookups, so duplicate rows, the ordered update chains and the
+// |W| hierarchy are resolved inside the workgroup -- no sort, no workspace, no hand-off,
+// no finalize. dqrm_emb_bwd_sgd takes it when max_lookups <= min(SG_MAXL, 64 * D/4) and
+// B * D <= SG_DY_FLOATS. Same arithmetic and order as k_bwd_fused<LPR, 0>: per row, in
+// ascending lookup position j,  W = fma((dy[bag(j)] * s) / s, -lr, W).
+//   1. one round trip: the table's indices, every bag's dy slice (STE applied, staged in
+//      LDS), the offsets (bag form) and, for a narrow table, its rows' |W| maxima;
+//   2. one lane group (LPR lanes) per lookup i: the group's lanes compare x_i with
+//      disjoint position ranges (one 64-bit match mask each); i owns its row iff no earlier
+//      position matches;
+//   3. owners load their W row and the old block / superblock / table maxima (one round
+//      trip), walk the matches in position order out of LDS, store W (+ INT4 repack);
+//   4. |W| hierarchy: growth by atomicMax; a shrunk block-max holder queues its block,
+//      re-reduced from rowmax once the workgroup's stores have landed, then (rarely) its
+//      superblock, then (more rarely) the table maximum; a narrow table reduces its row
+//      maxima in LDS.
+// ------------------------------------------------------------------------------------
+constexpr int SG_TPB = 512;
+constexpr int SG_MAXL = 512;           // lookups per table: at most one per thread
+constexpr int SG_DY_FLOATS = 16384;    // dy staging, dynamic LDS (64 KiB)
+// lookups per table k_sgd_small takes: one per thread, 64 positions per lane's match mask,
+// at most 8 lookups per lane group
+__host__ __device__ constexpr int sg_maxl(int lpr) {
+    return SG_MAXL < 64 * lpr ? (SG_MAXL < 8 * (SG_TPB / lpr) ? SG_MAXL : 8 * (SG_TPB / lpr))
+                              : (64 * lpr < 8 * (SG_TPB / lpr) ? 64 * lpr : 8 * (SG_TPB / lpr));
+}
+
+template <int LPR>
+__global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
+    constexpr int D = LPR * 4;
+    constexpr int G = SG_TPB / LPR;                              // lane groups
+    constexpr int MAXL = sg_maxl(LPR);
+    constexpr int NPG = (MAXL + G - 1) / G;                      // lookups per lane group (<= 8)
+    static_assert(NPG <= 8 && MAXL <= 64 * LPR, "k_sgd_small geometry");
+    constexpr int DYF = SG_DY_FLOATS / 4 / SG_TPB;               // dy float4 per thread
+    constexpr int NW = SG_TPB / WAVE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* s_dy = reinterpret_cast<float4*>(lds);               // [B][LPR], STE applied
+    __shared__ int32_t s_row[SG_MAXL];                           // local row of lookup j, -1 invalid
+    __shared__ int32_t s_bag[SG_MAXL];                           // bag of lookup j (offsets form)
+    __shared__ float s_rm[BLK];                                  // narrow table: row maxima
+    __shared__ int32_t s_q[SG_MAXL];                             // offsets, then queued blocks
+    __shared__ float s_qo[SG_MAXL], s_qso[SG_MAXL];              // their old block / superblock max
+    __shared__ int32_t s_sq[SG_MAXL];                            // queued superblocks
+    __shared__ float s_sqo[SG_MAXL];                             // ... their old max
+    __shared__ float s_red[NW];
+    __shared__ int s_n[3];                                       // queue lengths, rescan flag
+    const int t = blockIdx.x;
+    const Meta m = make_meta(a.meta, a.T);
+    const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    const bool narrow = nrows <= BLK;
+    const int B = (int)a.B;
+    const bool p1 = a.pool1 != 0;
+    const int64_t ib = p1 ? (int64_t)t * B : a.idx_base[t];
+    const int L = p1 ? B : (int)(a.idx_base[t + 1] - ib);
+    if (L > a.Lc || L > MAXL) {  // more lookups than the caller planned for: skipped, flagged
+        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        return;
+    }
+    const float s = a.scale[t];
+    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int gbase = (threadIdx.x % WAVE) - sub;
+    const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
+    // 1. every independent load of the table in flight together: each lane group's lookups
+    //    (its LPR lanes load the same index), the bags' dy slices, offsets, narrow row maxima
+    int64_t xr[NPG];
+#pragma unroll
+    for (int k = 0; k < NPG; ++k) {
+        const int i = grp + k * G;
+        xr[k] = i < L ? a.idx[ib + i] : -1;
+    }
+    const int64_t o0 = (!p1 && (int)threadIdx.x < B) ? a.off[(int64_t)t * B + threadIdx.x] : 0;
+    const float* dyt = a.dy + (int64_t)t * a.dst_t;
+    float4 gv[DYF];
+#pragma unroll
+    for (int f = 0; f < DYF; ++f) {
+        const int q = threadIdx.x + f * SG_TPB;
+        if (q < B * LPR) gv[f] = reinterpret_cast<const float4*>(dyt + (int64_t)(q / LPR) * a.dst_b)[q % LPR];
+    }
+    const float rmv = (narrow && threadIdx.x < nrows) ? a.rowmax[rb + threadIdx.x] : 0.0f;
+    const float otm = narrow ? 0.0f : a.tmax[t];
+    // 2. as soon as the indices land: every lookup's W row slice and old block / superblock
+    //    maxima (speculatively, owner or not), in flight across the LDS staging and the scan
+    int32_t xk[NPG];
+    float4 w0[NPG];
+    float ob[NPG], osb[NPG];
+#pragma unroll
+    for (int k = 0; k < NPG; ++k) {
+        const int i = grp + k * G;
+        const bool ok = xr[k] >= 0 && xr[k] < nrows;
+        if (i < L && !ok && sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+        xk[k] = (i < L && ok) ? (int32_t)xr[k] : -1;
+        ob[k] = 0.0f; osb[k] = 0.0f;
+        if (xk[k] >= 0) {
+            w0[k] = reinterpret_cast<const float4*>(a.W + (rb + xk[k]) * D)[sub];
+            if (!narrow) {
+                ob[k] = a.blkmax[bb + (xk[k] >> 8)];
+                osb[k] = a.sblkmax[sbb + (xk[k] >> 16)];
+            }
+        }
+        if (i < L && sub == 0) s_row[i] = xk[k];
+    }
+#pragma unroll
+    for (int f = 0; f < DYF; ++f) {
+        const int q = threadIdx.x + f * SG_TPB;
+        if (q < B * LPR) {
+            float4 g = gv[f];
+            if (a.ste) { g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s; }
+            s_dy[q] = g;
+        }
+    }
+    if (narrow && threadIdx.x < nrows) s_rm[threadIdx.x] = rmv;
+    if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+    if (!p1 && (int)threadIdx.x < B) s_q[threadIdx.x] = o0 < 0 ? -1 : (o0 > L ? L + 1 : (int32_t)o0);
+    if (!p1)
+        for (int j = threadIdx.x; j < L; j += SG_TPB) s_bag[j] = -1;
+    __syncthreads();
+    if (!p1 && (int)threadIdx.x < B) {  // bag b = lookups [off[b], off[b+1]) (the last ends at L)
+        const int b = threadIdx.x;
+        int s0 = s_q[b], s1 = b + 1 < B ? s_q[b + 1] : L;
+        if (s0 < 0 || s1 > L || s1 < s0 || (b == 0 && s0 != 0)) {  // as visit_slot_lookups; off[0] must be 0
+            flag_error(a.err, DQRM_ERRF_OFFSET);
+            s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
+            s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+        }
+        for (int j = s0; j < s1; ++j) s_bag[j] = b;
+    }
+    if (!p1) __syncthreads();
+    // 3. duplicate scan: lane `sub` of a group compares positions [sub*ch, sub*ch + ch)
+    const int ch = (L + LPR - 1) / LPR;  // <= 64
+    const int j0 = sub * ch, j1 = j0 + ch < L ? j0 + ch : L;
+    uint64_t mk[NPG];
+#pragma unroll
+    for (int k = 0; k < NPG; ++k) mk[k] = 0ull;
+    for (int j = j0; j < j1; ++j) {
+        const int32_t v = s_row[j];
+#pragma unroll
+        for (int k = 0; k < NPG; ++k) mk[k] |= (uint64_t)(v == xk[k] && v >= 0) << (j - j0);
+    }
+    bool own[NPG];
+#pragma unroll
+    for (int k = 0; k < NPG; ++k) {
+        const int i = grp + k * G;
+        const int lo = i - j0;  // positions of this lane's range that precede i
+        const uint64_t earlier = lo <= 0 ? 0ull : (lo >= 64 ? mk[k] : (mk[k] & ((1ull << lo) - 1ull)));
+        own[k] = i < L && xk[k] >= 0 && !(__ballot(earlier != 0ull) & gmask);
+    }
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < NPG; ++k) {
+        if (!own[k]) continue;  // group-uniform
+        float4 acc = w0[k];
+        for (int l = 0; l < LPR; ++l) {  // the row's positions, ascending
+            const uint32_t lo32 = (uint32_t)__shfl((int)(uint32_t)mk[k], gbase + l, WAVE);
+            const uint32_t hi32 = (uint32_t)__shfl((int)(uint32_t)(mk[k] >> 32), gbase + l, WAVE);
+            uint64_t ml = ((uint64_t)hi32 << 32) | lo32;
+            while (ml) {
+                const int j = l * ch + __ffsll((long long)ml) - 1;
+                ml &= ml - 1;
+                const int bag = p1 ? j : s_bag[j];
+                if (bag < 0) continue;  // a lookup outside every bag (flagged offsets)
+                acc = seg_op4<OP_FMA>(acc, s_dy[bag * LPR + sub], a.nlr);
+            }
+        }
+        const int64_t grow = rb + xk[k];
+        reinterpret_cast<float4*>(a.W + grow * D)[sub] = acc;
+        if (a.repack) pack4_row(acc, a.packed + grow * (D / 2), sub, r_pack);
+        const float orm = group_max<LPR>(abs_max4(w0[k]));
+        const float rm = group_max<LPR>(abs_max4(acc));
+        if (sub == 0) {
+            if (narrow) {
+                a.rowmax[grow] = rm;
+                s_rm[xk[k]] = rm;
+            } else {
+                st_wt(a.rowmax + grow, rm);
+                const int64_t blk = xk[k] >> 8, sb = blk >> 8;
+                if (rm > ob[k]) {
+                    atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
+                    if (rm > osb[k]) {
+                        atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sbb + sb, __float_as_uint(rm));
+                        if (rm > otm) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
+                    }
+                }
+                if (orm == ob[k] && rm < orm) {  // held its block's max and shrank
+                    const int q = atomicAdd(&s_n[0], 1);
+                    s_q[q] = (int32_t)blk;
+                    s_qo[q] = ob[k];
+                    s_qso[q] = osb[k];
+                }
+            }
+        }
+    }
+    // 4. the table's maxima (LDS work first; a store round trip only when a block needs its
+    //    row maxima re-read)
+    __syncthreads();
+    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
+    if (narrow) {
+        float v = threadIdx.x < nrows ? s_rm[threadIdx.x] : 0.0f;
+        v = wave_max(v);
+        if (lane == 0) s_red[w] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float r = 0.0f;
+            for (int q = 0; q < NW; ++q) r = fmaxf(r, s_red[q]);
+            a.blkmax[bb] = r;
+            a.sblkmax[sbb] = r;
+            a.tmax[t] = r;
+        }
+        return;
+    }
+    const int64_t nblk = ceil_div(nrows, BLK);
+    const int nq = s_n[0];
+    if (nq == 0) return;  // uniform: no block max holder shrank (the common case)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the workgroup's row maxima have landed
+    __syncthreads();
+    for (int q = w; q < nq; q += NW) {  // a wave per shrunk block: its 256 row maxima
+        const int64_t blk = s_q[q];
+        float v = 0.0f;
+#pragma unroll
+        for (int i = 0; i < BLK / WAVE; ++i) {
+            const int64_t r = blk * BLK + lane + i * WAVE;
+            if (r < nrows) v = fmaxf(v, ld_wt(a.rowmax + rb + r));
+        }
+        v = wave_max(v);
+        if (lane == 0) {
+            st_wt(a.blkmax + bb + blk, v);
+            if (s_qo[q] == s_qso[q] && v < s_qo[q]) {  // it held its superblock's max
+                const int p = atomicAdd(&s_n[1], 1);
+                s_sq[p] = (int32_t)(blk >> 8);
+                s_sqo[p] = s_qso[q];
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nsq = s_n[1];
+    for (int q = w; q < nsq; q += NW) {  // a wave per shrunk superblock: its 256 block maxima
+        const int64_t sb = s_sq[q];
+        float v = 0.0f;
+#pragma unroll
+        for (int i = 0; i < SBLK_BLOCKS / WAVE; ++i) {
+            const int64_t b = sb * SBLK_BLOCKS + lane + i * WAVE;
+            if (b < nblk) v = fmaxf(v, ld_wt(a.blkmax + bb + b));
+        }
+        v = wave_max(v);
+        if (lane == 0) {
+            st_wt(a.sblkmax + sbb + sb, v);
+            if (s_sqo[q] == otm && v < otm) s_n[2] = 1;  // it held the table max
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (s_n[2]) {  // uniform: rescan the table's superblock maxima
+        const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
+        float v = 0.0f;
+        for (int64_t k = threadIdx.x; k < ns; k += SG_TPB) v = fmaxf(v, ld_wt(a.sblkmax + sbb + k));
+        v = wave_max(v);
+        if (lane == 0) s_red[w] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float r = 0.0f;
+            for (int q = 0; q < NW; ++q) r = fmaxf(r, s_red[q]);
+            a.tmax[t] = r;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -3174,7 +3667,7 @@ int check_set(const dqrm_table_set* s) {
     if (D < 4 || D > 256 || (D & 3) || ((D / 4) & (D / 4 - 1)))
         return set_error(DQRM_E_INVALID, "dqrm: dim must be 4*2^k <= 256 (got %d)", D);
     if (!s->W || !s->rowmax || !s->blkmax || !s->sblkmax || !s->tmax || !s->scale || !s->pscale ||
-        !s->meta || !s->err || !s->tflags || !s->sdirty || !s->bdirty)
+        !s->meta || !s->err || !s->tflags || !s->sdirty || !s->bdirty || !s->sync)
         return set_error(DQRM_E_INVALID, "dqrm: null state pointer");
     if (((uintptr_t)s->W) & 15)
         return set_error(DQRM_E_INVALID, "dqrm: W must be 16-byte aligned");
@@ -3229,8 +3722,8 @@ __global__ void __launch_bounds__(256) k_rows_changed(const float* __restrict__ 
         if (packed) pack_row_int4<LPR>(w, packed, g, lane, 1.0f / pscale[t]);
         if (lane == 0) {
             rowmax[g] = v;
-            bdirty[m.blk_base[t] + r / BLK] = 1;
-            sdirty[m.sblk_base[t] + r / ((int64_t)BLK * SBLK_BLOCKS)] = 1;
+            flag_set(bdirty, m.blk_base[t] + r / BLK);
+            flag_set(sdirty, m.sblk_base[t] + r / ((int64_t)BLK * SBLK_BLOCKS));
         }
     }
 }
@@ -3275,10 +3768,15 @@ __global__ void __launch_bounds__(256) k_lookup_grad(LgArgs a) {
     for (int64_t b = (int64_t)blockIdx.x * G + grp; b < B; b += (int64_t)gridDim.x * G) {
         int64_t s0 = p1 ? b : off[b];
         int64_t s1 = p1 ? b + 1 : ((b + 1 < B) ? off[b + 1] : L);
-        if (s0 < 0 || s1 > L || s1 < s0) {
+        if (s0 < 0 || s1 > L || s1 < s0 || (b == 0 && s0 != 0)) {  // nn.EmbeddingBag needs off[0] == 0
             if (lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
             s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
             s1 = s1 < s0 ? s0 : (s1 > L ? L : s1);
+            if (b == 0)  // lookups before the first bag: zero rows on the table's row 0, never garbage
+                for (int64_t j = 0; j < s0; ++j) {
+                    if (lane == 0) a.rows[ibase + j] = rowbase;
+                    reinterpret_cast<float4*>(a.vals + (ibase + j) * D)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
         }
         if (s1 == s0) continue;
         float4 g = reinterpret_cast<const float4*>(a.dy + (int64_t)t * a.dst_t + b * a.dst_b)[lane];
@@ -3316,6 +3814,8 @@ int allow_lds(K kernel, size_t bytes) {
     // re-setting it on every call costs host time on the launch path)
     // (keyed by the kernel's address: several kernels share one function-pointer type)
     if (bytes <= 65536) return DQRM_OK;
+    static std::mutex mu;  // launches may come from several host threads
+    std::lock_guard<std::mutex> lock(mu);
     static const void* seen[64];
     static size_t seen_bytes[64];
     static int nseen = 0;
@@ -3344,6 +3844,22 @@ int apply_kernel_kind() {
     }
     return k;
 }
+
+// Where the |W| hierarchy of an updating kernel is finalized. Measured: the
+// flat apply kernels (thousands of short workgroups, latency-bound at full occupancy) are
+// faster with their owned-block re-reduction plus a short k_table_finalize launch than with
+// the in-launch hand-off (whose code and arrival protocol cost them occupancy and a tail
+// round trip per workgroup); the slot kernels (one workgroup per table slot) finalize in
+// the launch. DQRM_FINALIZE=launch / inline forces one scheme for every kernel (A/B).
+int finalize_mode() {  // 0 auto, 1 launch, 2 inline
+    static const int v = [] {
+        const char* e = getenv("DQRM_FINALIZE");
+        return (e && !strcmp(e, "launch")) ? 1 : (e && !strcmp(e, "inline")) ? 2 : 0;
+    }();
+    return v;
+}
+int finalize_launch() { return finalize_mode() == 1 ? 1 : 0; }          // slot kernels
+int finalize_launch_flat() { return finalize_mode() == 2 ? 0 : 1; }     // flat apply kernels
 
 // one backward call (K4a + K4b [+ finalize]) on the caller's workspace
 struct BwdCall {
@@ -3383,6 +3899,7 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     fused_ws_layout(reinterpret_cast<unsigned char*>(c.ws), T, Lc, &fa);
     fa.W = set->W; fa.packed = set->packed; fa.rowmax = set->rowmax; fa.blkmax = set->blkmax;
     fa.sblkmax = set->sblkmax; fa.tmax = set->tmax; fa.sdirty = set->sdirty; fa.bdirty = set->bdirty;
+    fa.sync = set->sync; fa.fin_launch = finalize_launch();
     fa.scale = set->scale; fa.pscale = set->pscale; fa.meta = set->meta; fa.err = set->err;
     fa.idx = c.batch->idx; fa.off = c.batch->off; fa.idx_base = c.batch->idx_base; fa.B = c.batch->num_bags;
     fa.pool1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
@@ -3390,12 +3907,23 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     fa.repack = c.repack; fa.tmask = c.tmask; fa.ws_cap_base = c.ws_cap_base; fa.ws_rows = c.ws_rows;
     fa.ws_vals = c.ws_vals; fa.ws_ucount = c.ws_ucount; fa.ws_absmax = c.ws_absmax; fa.Lc = Lc;
     int rc = 0;
+    // SGD of a small batch: one workgroup per table, no sort, no hand-off (k_sgd_small)
+    if (MODE == 0 && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && Lc <= sg_maxl(D / 4) &&
+        c.batch->num_bags * D <= SG_DY_FLOATS && set->total_rows <= 0x7fffffffll) {
+        const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float);
+        DISPATCH_LPR(D, {
+            if ((rc = allow_lds(k_sgd_small<LPR>, dyn))) return rc;
+            hipLaunchKernelGGL(k_sgd_small<LPR>, dim3(T), dim3(SG_TPB), dyn, st, fa);
+        });
+        LAUNCH_CHECK();
+        return DQRM_OK;
+    }
     DISPATCH_LPR(D, {
         if ((rc = allow_lds(k_bwd_fused<LPR, MODE>, FB_LDS))) return rc;
         hipLaunchKernelGGL((k_bwd_fused<LPR, MODE>), dim3(T * SPLIT), dim3(FB_TPB), FB_LDS, st, fa);
     });
-    LAUNCH_CHECK();
-    if (MODE != 1) return launch_finalize(set, st, true);
+    LAUNCH_CHECK();  // MODE 0 / 2: the |W| hierarchy is finalized inside the launch
+    if (MODE != 1 && fa.fin_launch) return launch_finalize(set, st, true);
     return DQRM_OK;
 }
 
@@ -3465,6 +3993,7 @@ int dqrm_refresh_absmax(const dqrm_table_set* set, void* stream) {
     LAUNCH_CHECK();
     HIP_TRY(hipMemsetAsync(set->sdirty, 0, (size_t)set->total_sblocks, st));
     HIP_TRY(hipMemsetAsync(set->bdirty, 0, (size_t)set->total_blocks, st));
+    HIP_TRY(hipMemsetAsync(set->sync, 0, (size_t)set->num_tables * DQRM_SYNC_STRIDE * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_table_max, dim3(set->num_tables), dim3(256), 0, st, set->sblkmax, set->tmax,
                        set->meta, set->num_tables);
     LAUNCH_CHECK();
@@ -3667,8 +4196,9 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
         ca.dy = dy; ca.dst_t = dy_stride_t; ca.dst_b = dy_stride_b; ca.scale = set->scale; ca.ste = ste;
         ca.err = set->err; ca.ws_cap_base = ws_cap_base; ca.ws_rows = ws_rows; ca.ws_vals = ws_vals;
         ca.ws_ucount = ws_ucount; ca.ws_absmax = ws_absmax;
-        if (dqrm_internal::launch_coalesce_pool1(ca, (hipStream_t)stream) != DQRM_OK)
-            return set_error(DQRM_E_HIP, "dqrm_emb_bwd_coalesce: launch failed: %s", hipGetErrorString(hipGetLastError()));
+        const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, (hipStream_t)stream);
+        if (e != hipSuccess)
+            return set_error(DQRM_E_HIP, "dqrm_emb_bwd_coalesce: launch failed: %s (%d)", hipGetErrorString(e), (int)e);
         return DQRM_OK;
     }
     return launch_bwd<1>(c, (hipStream_t)stream, "dqrm_emb_bwd_coalesce");
@@ -3774,7 +4304,8 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
     a.err = set->err; a.cap_base = cap_base; a.cap_total = cap_total;
     a.payloads = (const unsigned char*)payloads; a.payload_bytes = (int64_t)rank_pitch;  // rank stride
     a.N = num_ranks; a.T = set->num_tables; a.bits = grad_bits; a.s_avg = s_avg; a.nlr = -lr;
-    a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty; a.tmax = set->tmax;
+    a.mode = mode; a.repack = repack_bits == 4; a.bdirty = set->bdirty; a.tmax = set->tmax; a.sync = set->sync;
+    a.fin_launch = finalize_launch(); a.wt = 1;
     hipStream_t st = (hipStream_t)stream;
     const int D = set->dim;
     const int kind = apply_kernel_kind();
@@ -3788,6 +4319,8 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
         });
     } else {
         flat = true;
+        a.fin_launch = finalize_launch_flat();
+        a.wt = !a.fin_launch;
         // grid (entry chunks, tables, ranks): twice the chunks of an average table (the
         // per-table capacities live on the device); larger tables grid-stride, chunks past
         // a table's count exit at once
@@ -3797,12 +4330,17 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
             const int64_t lim = (32768 + (int64_t)a.T * num_ranks - 1) / ((int64_t)a.T * num_ranks);
             if (gx > lim) gx = lim;
             if (gx < 1) gx = 1;
-            hipLaunchKernelGGL(k_apply_flat<LPR>, dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
-                               dim3(FLAT_TPB), 0, st, a);
+            if (a.fin_launch)
+                hipLaunchKernelGGL((k_apply_flat<LPR, false>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
+                                   dim3(FLAT_TPB), 0, st, a);
+            else
+                hipLaunchKernelGGL((k_apply_flat<LPR, true>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
+                                   dim3(FLAT_TPB), 0, st, a);
         });
     }
-    LAUNCH_CHECK();
-    return launch_finalize(set, st, flat);
+    LAUNCH_CHECK();  // both kernels finalize the |W| hierarchy inside the launch
+    if (a.fin_launch) return launch_finalize(set, st, flat);
+    return DQRM_OK;
 }
 
 int dqrm_apply_sparse_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
@@ -3827,6 +4365,7 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
     ApplyArgs a{};
     a.W = set->W; a.packed = set->packed; a.rowmax = set->rowmax; a.blkmax = set->blkmax;
     a.sblkmax = set->sblkmax; a.sdirty = set->sdirty; a.bdirty = set->bdirty; a.tmax = set->tmax; a.pscale = set->pscale;
+    a.sync = set->sync; a.fin_launch = finalize_launch_flat(); a.wt = !a.fin_launch;
     a.meta = set->meta; a.err = set->err; a.N = 1; a.T = set->num_tables; a.bits = grad_bits;
     a.s_avg = s_avg; a.nlr = -lr; a.mode = DQRM_UPD_DP; a.repack = repack_bits == 4;
     hipStream_t st = (hipStream_t)stream;
@@ -3840,11 +4379,16 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
         const int64_t lim = (32768 + slots - 1) / (slots > 0 ? slots : 1);
         if (gx > lim) gx = lim;
         if (gx < 1) gx = 1;
-        hipLaunchKernelGGL(k_apply_local<LPR>, dim3((unsigned)gx, (unsigned)slots), dim3(FLAT_TPB), 0, st, a,
-                           ws_cap_base, ws_rows, ws_vals, ws_ucount, ws_absmax, s_avg);
+        if (a.fin_launch)
+            hipLaunchKernelGGL((k_apply_local<LPR, false>), dim3((unsigned)gx, (unsigned)slots), dim3(FLAT_TPB), 0, st,
+                               a, ws_cap_base, ws_rows, ws_vals, ws_ucount, ws_absmax, s_avg);
+        else
+            hipLaunchKernelGGL((k_apply_local<LPR, true>), dim3((unsigned)gx, (unsigned)slots), dim3(FLAT_TPB), 0, st,
+                               a, ws_cap_base, ws_rows, ws_vals, ws_ucount, ws_absmax, s_avg);
     });
-    LAUNCH_CHECK();
-    return launch_finalize(set, st, true);
+    LAUNCH_CHECK();  // the table's last working workgroup finalizes its |W| hierarchy
+    if (a.fin_launch) return launch_finalize(set, st, true);
+    return DQRM_OK;
 }
 
 int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {

@@ -39,19 +39,46 @@ _DEFAULT_GRAD_MODE = "sparse"
 _ERROR_CHECK_EVERY = 1
 
 
+_POOLING_ONE_HINT = False
+
+
 def set_error_check_interval(steps: int) -> None:
-    """Read the tables' device error flags (out-of-range index, bad offsets) every `steps`
+    """Poll the tables' device error flags (out-of-range index, bad offsets) every `steps`
     training calls -- in the module's forward for grad_mode "sparse" / "fused_sgd", in
     weight_update_parallel_comm for "dp" -- and raise DQRMError when one is set (ATen raises
-    on such input). 0 = never. Each read synchronises the host with the stream once."""
+    on such input). 0 = never. A poll never synchronises the host: it reads the last
+    completed asynchronous snapshot of the flag word (EmbeddingTableSet.poll_errors), so a
+    bad batch raises one or two calls after the call that consumed it."""
     global _ERROR_CHECK_EVERY
     _ERROR_CHECK_EVERY = max(0, int(steps))
+
+
+def set_pooling_one_inputs(promise: bool) -> None:
+    """Promise that every batch the modules see is in the Criteo form (one index per bag,
+    offsets == arange(B), dlrm_data_pytorch.py:328-345) even when the offsets already live
+    on the GPU (host offsets are checked without it); the kernels then never read the
+    offsets. Off by default: nn.EmbeddingBag accepts any offsets."""
+    global _POOLING_ONE_HINT
+    _POOLING_ONE_HINT = bool(promise)
+
+
+def _pooling_one_arg():
+    return True if _POOLING_ONE_HINT else None
 
 
 def error_check_due(owner) -> bool:
     n = getattr(owner, "_dqrm_err_calls", 0) + 1
     owner._dqrm_err_calls = n
     return _ERROR_CHECK_EVERY > 0 and n % _ERROR_CHECK_EVERY == 0
+
+
+def poll_device_errors(tset) -> None:
+    """Raise DQRMError if the last completed snapshot of `tset`'s error word is non-zero
+    (the flags are then cleared); never blocks."""
+    flags = tset.poll_errors()
+    if flags:
+        tset.read_errors(clear=True)
+        raise_device_errors(flags)
 
 
 def raise_device_errors(flags: int) -> None:
@@ -80,7 +107,9 @@ def _batch_from_input(input: torch.Tensor, offsets: torch.Tensor | None, device)
         input = input.reshape(-1)
     elif offsets is None:
         raise ValueError("offsets has to be a 1D Tensor but got None")
-    return LookupBatch([input.reshape(-1)], [offsets.reshape(-1)], device=device)
+    flat_off = offsets.reshape(-1)
+    p1 = _pooling_one_arg() if input.numel() == flat_off.numel() else False
+    return LookupBatch([input.reshape(-1)], [flat_off], device=device, pooling_one=p1)
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -135,21 +164,23 @@ class _QuantEmbeddingBase(nn.Module):
         self._ready = None        # grad bits of an exchanged, not yet applied update
         self._counters = None     # host mirror of (now_iteration, iteration_bound, iteration_nt)
         self._rr = None           # ranking range: (bits host int32 [T], bits dev, scale dev) of this step
-        self._ext_rows = None     # rows of the last sparse grad handed to an optimizer (grad_mode "sparse")
+        self._ext_rows = []       # rows of the sparse grads handed to an optimizer since the last sync
+                                  # (grad_mode "sparse"; several with gradient accumulation)
 
     def _sync_external_update(self) -> None:
         """grad_mode "sparse": the optimizer stepped W on the rows of the last COO outside
         libdqrm; bring their maxima (the refreshing forward's full-table scale) and INT4 rows
         up to date before the next forward reads them."""
-        if self._ext_rows is not None:
-            self._tset.rows_changed(self._ext_rows, repack=self._use_packed(False))
-            self._ext_rows = None
+        if self._ext_rows:
+            rows = self._ext_rows[0] if len(self._ext_rows) == 1 else torch.cat(self._ext_rows)
+            self._tset.rows_changed(rows, repack=self._use_packed(False))
+            self._ext_rows = []
 
     def _check_errors(self, test_mode: bool) -> None:
         """grad_mode "sparse" / "fused_sgd": flags raised by the previous call's kernels
         surface here, at the next training call (the DP hooks check them for "dp")."""
         if self.grad_mode != "dp" and not test_mode and error_check_due(self):
-            raise_device_errors(self._tset.read_errors())
+            poll_device_errors(self._tset)
 
     # ------------------------------------------------------------ scale refresh logic
     def _refresh_due(self, fp: bool, test_mode: bool) -> bool:
@@ -200,7 +231,7 @@ class _QuantEmbeddingBase(nn.Module):
         entry per lookup, in lookup order (one libdqrm launch, no host sync). torch.optim.SGD
         then adds it to W exactly as it adds the reference's own embedding gradient."""
         rows, vals = self._tset.lookup_grad(batch, dy, ste=ste, layout=layout)
-        self._ext_rows = rows
+        self._ext_rows.append(rows)
         return torch.sparse_coo_tensor(rows.view(1, -1), vals, (self._tset.R, self._tset.D), is_coalesced=False)
 
 
@@ -285,6 +316,51 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
         return out
 
 
+def consolidate_tables(modules, force: bool = False) -> EmbeddingTableSet | None:
+    """Move the tables of several single-table modules (the DP driver's ModuleList of
+    QuantEmbeddingBagTwo, dlrm_s_pytorch_tb_dp_one_parallel_comm.py:380) into ONE table set:
+    one slab per array, each module then running on a one-table view of it
+    (EmbeddingTableSet.view) and each ``embedding_bag.weight`` Parameter keeping its identity
+    with its data a view of the slab. The grad-comm hooks then launch once per phase for all
+    tables instead of once per module. State is copied exactly (W, INT4 rows, scales; the
+    |W| hierarchy is rebuilt from the same W, so it is bit-identical).
+
+    Needs room for a second copy of the tables while they are moved (checked against the
+    device's free memory unless force=True); returns the set, or None when the modules are
+    already consolidated, are not all alike (device, dim, packed rows), or do not fit."""
+    mods = list(modules)
+    if len(mods) < 2 or any(not isinstance(m, QuantEmbeddingBagTwo) for m in mods):
+        return None
+    first = mods[0]._tset
+    if first.parent is not None and all(m._tset.parent is first.parent for m in mods):
+        return None  # already one set
+    dev, D = first.device, first.D
+    packed = first.packed is not None
+    if any(m._tset.device != dev or m._tset.D != D or (m._tset.packed is not None) != packed for m in mods):
+        return None
+    rows = [m._tset.num_rows[0] for m in mods]
+    need = sum(rows) * (D * 4 + (D // 2 if packed else 0) + 4)  # W, INT4 rows, row maxima
+    if not force and dev.type == "cuda":
+        free, _ = torch.cuda.mem_get_info(dev)
+        if need * 1.1 + (256 << 20) > free:
+            return None
+    big = EmbeddingTableSet(rows, D, device=dev, packed=packed, init=None)
+    with torch.no_grad():
+        for t, m in enumerate(mods):
+            old = m._tset
+            big.table_weight(t).copy_(old.W)
+            if packed:
+                big.table_packed(t).copy_(old.packed)
+            big.scale[t: t + 1].copy_(old.scale)
+            big.pscale[t: t + 1].copy_(old.pscale)
+    big.refresh_absmax()
+    for t, m in enumerate(mods):
+        m._tset = big.view(t)
+        m.embedding_bag.weight.data = m._tset.W
+        m._exchange = None
+    return big
+
+
 class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
     """All tables of a DLRM in one resident slab; forward(lS_o, lS_i) replaces the per-table
     loop of DLRM_Net.apply_emb (dlrm_s_pytorch_single_gpu.py:609-674) with ONE launch."""
@@ -326,7 +402,7 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         self._check_errors(test_mode)
         self._sync_external_update()
         refresh = self._refresh_due(fp, test_mode)
-        batch = LookupBatch(lS_i, lS_o, device=self._tset.device)
+        batch = LookupBatch(lS_i, lS_o, device=self._tset.device, pooling_one=_pooling_one_arg())
         if refresh and self._use_packed(fp):
             self._tset.refresh_scale_and_pack(self.embedding_bit)
             refresh_in_fwd = False
@@ -348,4 +424,4 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
 
 
 __all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode",
-           "set_error_check_interval"]
+           "set_error_check_interval", "set_pooling_one_inputs", "consolidate_tables"]

@@ -29,15 +29,16 @@ blocking collectives per layer. The layers must live on the GPU (no CPU path).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 from torch import nn
 
 from . import _lib as L
-from .comm import MultiSetExchange, SparseGradExchange
+from .comm import ConsolidatedExchange, MultiSetExchange, SparseGradExchange
 from .dense import DenseGradExchange
-from .quant_modules_not_quantize_grad import (_QuantEmbeddingBase, error_check_due, raise_device_errors,
-                                              set_error_check_interval)
+from .quant_modules_not_quantize_grad import (_QuantEmbeddingBase, consolidate_tables, error_check_due,
+                                              poll_device_errors, set_error_check_interval)
 
 _MLP_PLAIN_LINEAR = False
 
@@ -84,22 +85,108 @@ def _detach_grad(g: torch.Tensor) -> None:
 def _ensure_exchange(m: _QuantEmbeddingBase, grad_bits: int, group) -> SparseGradExchange:
     batch = m._pending[0]
     ex = m._exchange
-    if ex is None or ex.grad_bits != grad_bits or ex.max_lookups < batch.max_lookups or ex.group is not group:
-        ex = SparseGradExchange(m._tset, max(batch.max_lookups, 1), grad_bits=grad_bits, group=group,
-                                device=m._tset.device)
+    fresh = ex is None or ex.grad_bits != grad_bits or ex.group is not group or ex.tables is not m._tset
+    if fresh or _outgrown([batch.max_lookups], [ex.max_lookups], group):
+        need = max(batch.max_lookups, 1) if fresh else max(batch.max_lookups, ex.max_lookups)
+        cap = _agreed_caps([need], group, m._tset.device)[0]
+        ex = SparseGradExchange(m._tset, cap, grad_bits=grad_bits, group=group, device=m._tset.device)
         m._exchange = ex
     return ex
 
 
-def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group) -> MultiSetExchange:
+_CONSOLIDATE = True
+
+
+def set_consolidate_tables(enable: bool) -> None:
+    """Whether the hooks move a ModuleList of per-table modules into one table set the first
+    time they see it (quant_modules_not_quantize_grad.consolidate_tables; skipped anyway when
+    a second copy of the tables would not fit in device memory). On by default."""
+    global _CONSOLIDATE
+    _CONSOLIDATE = bool(enable)
+
+
+_MAX_LOOKUPS = 0
+
+
+def set_max_lookups(n: int) -> None:
+    """Lookups per table and rank the embedding exchange plans its payload for (0: the
+    first step's, taken as the maximum over the ranks). The payload layout must agree on
+    every rank, so with N > 1 a later batch with more lookups than planned raises instead of
+    resizing one rank alone; drivers with variable-size bags (random multi-hot data) set
+    B * max_pooling here on every rank."""
+    global _MAX_LOOKUPS
+    _MAX_LOOKUPS = max(0, int(n))
+
+
+def _agreed_caps(need: list[int], group, dev) -> list[int]:
+    """Element-wise max of `need` over the ranks (one small all-reduce and one host read,
+    when the exchange is built -- not per step), so every rank sizes the same payload."""
+    need = [max(n, _MAX_LOOKUPS) for n in need]
+    if _world(group) == 1:
+        return need
+    on_dev = dist.get_backend(group) == "nccl"
+    t = torch.tensor(need, dtype=torch.int64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return [int(x) for x in t.cpu().tolist()]
+
+
+def _outgrown(need, caps, group) -> bool:
+    """A batch beyond the planned capacity: rebuild at N = 1; at N > 1 only this rank knows,
+    so raise rather than resize one rank's payload alone."""
+    if not any(n > c for n, c in zip(need, caps)):
+        return False
+    if _world(group) > 1:
+        raise L.DQRMError(f"a batch has {max(need)} lookups per table, beyond the {max(caps)} the embedding "
+                          "exchange planned on every rank: call set_max_lookups(n) on all ranks")
+    return True
+
+
+def _consolidated_set(model, mods):
+    """The one set holding every module's table (consolidating on first use), or None."""
+    big = getattr(model, "_dqrm_consolidated", None)
+    if big is None:
+        big = False
+        if _CONSOLIDATE and len(mods) > 1:
+            big = consolidate_tables(mods) or False
+        model._dqrm_consolidated = big
+    if big is False:
+        first = mods[0]._tset.parent
+        if first is not None and len(mods) == first.T and all(
+                m._tset.parent is first and m._tset.parent_index == t for t, m in enumerate(mods)):
+            return first  # consolidated by the caller
+        return None
+    if all(m._tset.parent is big for m in mods):
+        return big
+    return None
+
+
+def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group):
     """The model's one exchange over all its embedding modules (cached; rebuilt when the
     modules, bits, group or a batch beyond the planned lookups change). The modules' table
-    sets share one device error word so one read per step covers them all."""
+    sets share one device error word so one read per step covers them all. A ModuleList of
+    per-table modules is consolidated into one set (ConsolidatedExchange: one launch per
+    phase); otherwise one MultiSetExchange over the modules' sets."""
+    big = _consolidated_set(model, mods) if len(mods) > 1 else None
+    if big is not None and all(m._pending is not None for m in mods) \
+            and len({m._pending[0].num_bags for m in mods}) == 1:
+        need = max(max(m._pending[0].max_lookups, 1) for m in mods)
+        key = ("consolidated", id(big), grad_bits, id(group), _world(group))
+        ex = getattr(model, "_dqrm_emb_exchange", None)
+        fresh = ex is None or ex[0] != key
+        if fresh or _outgrown([need], ex[1].max_lookups[:1], group):
+            cap = _agreed_caps([need if fresh else max(need, ex[1].max_lookups[0])], group, big.device)[0]
+            ex = (key, ConsolidatedExchange(big, cap, grad_bits=grad_bits, group=group))
+            model._dqrm_emb_exchange = ex
+            for t, m in enumerate(mods):  # the modules' emb_scaling_factor: views of the averaged scales
+                m.emb_scaling_factor = ex[1].scales[t]
+        return ex[1]
     need = [max(m._pending[0].max_lookups if m._pending is not None else 1, 1) for m in mods]
     key = (tuple(id(m._tset) for m in mods), grad_bits, id(group), _world(group))
     ex = getattr(model, "_dqrm_emb_exchange", None)
-    if ex is None or ex[0] != key or any(n > c for n, c in zip(need, ex[1].max_lookups)):
-        caps = need if ex is None or ex[0] != key else [max(n, c) for n, c in zip(need, ex[1].max_lookups)]
+    fresh = ex is None or ex[0] != key
+    if fresh or _outgrown(need, ex[1].max_lookups, group):
+        caps = _agreed_caps(need if fresh else [max(n, c) for n, c in zip(need, ex[1].max_lookups)], group,
+                            mods[0]._tset.device)
         ex = (key, MultiSetExchange([m._tset for m in mods], caps, grad_bits=grad_bits, group=group,
                                     device=mods[0]._tset.device))
         model._dqrm_emb_exchange = ex
@@ -110,9 +197,10 @@ def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group)
 
 
 def _check_device_errors(model, mods: list[_QuantEmbeddingBase]) -> None:
-    """Raise if any kernel of this step flagged bad input (out-of-range index or offset,
-    understated max_lookups): the reference would have raised in ATen instead of training
-    on. One read (host sync) per distinct error word."""
+    """Raise if a kernel flagged bad input (out-of-range index or offset, understated
+    max_lookups): the reference would have raised in ATen instead of training on. One
+    non-blocking poll per distinct error word (the flags of a step surface a step or two
+    later; no host synchronisation)."""
     if not error_check_due(model):
         return
     seen = set()
@@ -121,7 +209,7 @@ def _check_device_errors(model, mods: list[_QuantEmbeddingBase]) -> None:
         if ptr in seen:
             continue
         seen.add(ptr)
-        raise_device_errors(m._tset.read_errors())
+        poll_device_errors(m._tset)
 
 
 def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, num_bits=16, ranking_range=False,
@@ -154,7 +242,7 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
                 ex = _emb_exchange(model, mods, bits, group)
                 s_avg = ex.exchange([m._pending for m in mods])
                 for m, s in zip(mods, s_avg):
-                    if bits != 32:
+                    if bits != 32 and s.data_ptr() != m.emb_scaling_factor.data_ptr():
                         m.emb_scaling_factor.copy_(s.view_as(m.emb_scaling_factor))
                     m._pending = None
                     m._ready = bits
@@ -253,24 +341,138 @@ def clear_gradients(model) -> None:
                 m._rr = None
 
 
-def weight_syncc(dlrm, num_gpus, group=None) -> None:
-    """s_q_g_p_c.py:963-970: all_reduce(SUM) * 1/N of every parameter, tables included.
-    (Replicas initialised from the same seed are bit-identical, and for N = 2^k the sum
-    then 1/N is exact, so this is then a no-op; it is kept for drop-in behaviour.) The
-    tables' |W| hierarchy and INT4 rows are rebuilt afterwards."""
-    with torch.no_grad():
-        for _, param in dlrm.named_parameters():
-            param.requires_grad_(False)
-            if _world(group) > 1:
-                dist.all_reduce(param, dist.ReduceOp.SUM, group=group)
+def _checksums(params, dev) -> torch.Tensor | None:
+    """One position-dependent 64-bit checksum per parameter (dqrm_checksum64), int64 [P] on
+    `dev`; None if a parameter cannot be hashed in place (not f32 / 16-B aligned / on dev)."""
+    lib = L.load()
+    out = torch.zeros(len(params), dtype=torch.int64, device=dev)
+    for i, p in enumerate(params):
+        if p.dtype != torch.float32 or not p.is_contiguous() or p.device != dev or p.data_ptr() % 16:
+            return None
+        L.check(lib.dqrm_checksum64(p.data_ptr(), p.numel(), out[i:].data_ptr(), _stream()), "dqrm_checksum64")
+    return out
+
+
+def _stream() -> int:
+    from .tables import _stream_handle
+    return _stream_handle()
+
+
+def _replicas_identical(params, dev, group) -> bool:
+    """Whether every rank holds the same bits in every parameter: one all-gather of the
+    per-parameter checksums and one host read per weight_syncc call."""
+    cs = _checksums(params, dev)
+    if cs is None:
+        return False
+    world = _world(group)
+    nccl = dist.get_backend(group) == "nccl"
+    mine = cs if nccl else cs.cpu()
+    allcs = torch.zeros(world, mine.numel(), dtype=torch.int64, device=mine.device)
+    dist.all_gather_into_tensor(allcs.view(-1), mine, group=group) if nccl else \
+        dist.all_gather(list(allcs.unbind(0)), mine, group=group)
+    allcs = allcs.cpu()
+    return bool((allcs == allcs[0]).all())
+
+
+def _ring_mean_is_identity(p: torch.Tensor, world: int, num_gpus: int, absmax: float) -> bool:
+    """The all-reduce of `world` identical copies times 1/num_gpus returns x unchanged for
+    world = num_gpus in {1, 2, 4} (dqrm_replica_mean; checked exhaustively over the f32
+    mantissas) unless world * |x| overflows."""
+    return world == num_gpus and world in (1, 2, 4) and absmax * world < 3.0e38
+
+
+def _sync_params(params, num_gpus: int, group, table_of: dict) -> set:
+    """weight_syncc's arithmetic over `params`; table_of maps a table parameter's data_ptr to
+    its table set (whose tmax bounds |W| without a pass over W). Returns the data_ptrs of
+    the parameters whose values changed."""
+    world = _world(group)
+    if not params:
+        return set()
+    dev = params[0].device
+    identical = world == 1 or (dev.type == "cuda" and _replicas_identical(params, dev, group))
+    inv = float(np.float32(1.0 / num_gpus))
+    absmax = [0.0] * len(params)
+    if identical and world == num_gpus and world in (1, 2, 4):  # |x| bound of the identity check
+        mx = []
+        for p in params:
+            ts = table_of.get(p.data_ptr())
+            if ts is not None:  # a table: its exact max |W| (the hierarchy's, no pass over W)
+                mx.append(ts.tmax.max())
+            else:
+                mx.append(p.detach().abs().max() if p.numel() else p.new_zeros(()))
+        absmax = torch.stack(mx).float().cpu().tolist()
+    changed = set()
+    lib = L.load()
+    for i, param in enumerate(params):
+        rg = param.requires_grad
+        param.requires_grad_(False)
+        if not identical:  # the reference's all-reduce
+            dist.all_reduce(param, dist.ReduceOp.SUM, group=group)
             param.mul_(1.0 / num_gpus)
-            param.requires_grad_(True)
-        emb = getattr(dlrm, "emb_l", None)
-        if emb is not None:
-            for m in _emb_modules(dlrm):
-                m._tset.refresh_absmax()
-                if m._tset.packed is not None:
-                    m._tset.repack_all(m.embedding_bit)
+            changed.add(param.data_ptr())
+        elif not _ring_mean_is_identity(param, world, num_gpus, absmax[i]):
+            if param.dtype == torch.float32 and param.is_contiguous() and param.data_ptr() % 16 == 0:
+                L.check(lib.dqrm_replica_mean(param.data_ptr(), param.numel(), world, inv, _stream()),
+                        "dqrm_replica_mean")
+            else:  # same arithmetic in torch (element-wise, IEEE-rounded)
+                acc = param.clone()
+                for _ in range(world - 1):
+                    acc.add_(param)
+                param.copy_(acc.mul_(inv))
+            changed.add(param.data_ptr())
+        param.requires_grad_(rg)
+    return changed
+
+
+def _refresh_tables(sets_bits) -> None:
+    """|W| hierarchy rebuild (and INT4 repack) of table sets whose W changed outside the
+    update kernels."""
+    for ts, bits in sets_bits:
+        ts.refresh_absmax()
+        if ts.packed is not None:
+            ts.repack_all(bits)
+
+
+def weight_syncc(dlrm, num_gpus, group=None) -> None:
+    """s_q_g_p_c.py:963-970: all_reduce(SUM) * 1/N of every parameter, tables included,
+    every 200 iterations of the DP driver (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1924-1936).
+
+    The DP step keeps replicas bit-identical by construction, and the reference's result on
+    identical replicas is computable locally: a ring all-reduce (Gloo's ring_chunked on the
+    reference's CPU ranks, RCCL's ring here) adds the ranks one after another, so every
+    element becomes fl(fl(...fl(x + x) + x ...) * 1/N) (dqrm_replica_mean) -- x itself for
+    N = 1, 2, 4, an ulp away for about half of the elements at N = 3 or 8. So: one
+    all-gather of per-parameter checksums (dqrm_checksum64); if every rank holds the same
+    bits, that local map (skipped where it is the identity) instead of the all-reduce --
+    bit-exact with the reference and a few streaming passes over HBM instead of an
+    all-reduce of the whole model (198 GB of tables at the config-5 shape); otherwise (e.g.
+    ranks initialised from different random tables, as the reference's are before training,
+    dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1801) the reference's all-reduce. The
+    tables' |W| hierarchy and INT4 rows are rebuilt when W changed."""
+    with torch.no_grad():
+        params = [p for _, p in dlrm.named_parameters()]
+        mods = _emb_modules(dlrm) if getattr(dlrm, "emb_l", None) is not None else []
+        table_of = {m.embedding_bag.weight.data_ptr(): m._tset for m in mods}
+        changed = _sync_params(params, num_gpus, group, table_of)
+        todo, seen = [], set()
+        for m in mods:
+            if m.embedding_bag.weight.data_ptr() not in changed:
+                continue
+            ts = m._tset.parent if m._tset.parent is not None else m._tset
+            if id(ts) not in seen:
+                seen.add(id(ts))
+                todo.append((ts, m.embedding_bit))
+        _refresh_tables(todo)
+
+
+def sync_table_set(ts, num_gpus: int, group=None, bits: int = 4) -> bool:
+    """weight_syncc for one resident table set (the bench's, or a QuantEmbeddingBagCollection's
+    ``_tset``): returns whether W changed."""
+    with torch.no_grad():
+        changed = _sync_params([ts.W], num_gpus, group, {ts.W.data_ptr(): ts})
+        if changed:
+            _refresh_tables([(ts, bits)])
+        return bool(changed)
 
 
 def quantized_gradients_update(model, arg, lr, num_gpus) -> None:
@@ -358,4 +560,5 @@ grad_upduate_parallel_comm = grad_update_parallel_comm
 
 __all__ = ["grad_update_parallel_comm", "grad_upduate_parallel_comm", "weight_update_parallel_comm",
            "clear_gradients", "weight_syncc", "quantized_gradients_update", "grad_precision_and_scale",
-           "set_mlp_plain_linear", "set_error_check_interval"]
+           "set_mlp_plain_linear", "set_error_check_interval", "set_consolidate_tables", "set_max_lookups",
+           "sync_table_set"]

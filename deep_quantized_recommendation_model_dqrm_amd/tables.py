@@ -41,6 +41,22 @@ def _ceil_div(a: int, b: int) -> int:
     return (a + b - 1) // b
 
 
+_BASE_CACHE: dict = {}
+
+
+def _device_base(base: list[int], dev: torch.device) -> torch.Tensor:
+    """Device copy of a batch's idx_base, created once per distinct (lookup counts, device):
+    steady-state steps reuse it instead of a pageable host-to-device copy per call."""
+    key = (tuple(base), str(dev))
+    t = _BASE_CACHE.get(key)
+    if t is None:
+        if len(_BASE_CACHE) > 256:
+            _BASE_CACHE.clear()
+        t = torch.tensor(base, dtype=torch.int64, device=dev)
+        _BASE_CACHE[key] = t
+    return t
+
+
 class LookupBatch:
     """All tables' lookups of one batch in the reference's (lS_i, lS_o) form.
 
@@ -50,9 +66,11 @@ class LookupBatch:
     Offsets are nn.EmbeddingBag offsets (bag b = [off[b], off[b+1]), last bag ends at L_t).
     """
 
-    def __init__(self, indices, offsets, device: torch.device | str | None = None, pooling_one: bool = False):
+    def __init__(self, indices, offsets, device: torch.device | str | None = None,
+                 pooling_one: bool | None = False):
         """pooling_one: promise that every table has one lookup per bag (offsets = arange(B),
-        the Criteo collate form) -- the kernels then skip reading the offsets."""
+        the Criteo collate form) -- the kernels then skip reading the offsets. None: detect it
+        when the offsets are host tensors (no device read, hence no host sync)."""
         if isinstance(indices, torch.Tensor):
             if indices.dim() != 2:
                 raise ValueError("stacked indices must be [T, L]")
@@ -85,7 +103,10 @@ class LookupBatch:
         self.idx_base_host = base
         self.idx = idx.to(device=dev, dtype=torch.int64).contiguous()
         self.off = off.to(device=dev, dtype=torch.int64).contiguous()
-        self.idx_base = torch.tensor(base, dtype=torch.int64, device=dev)
+        self.idx_base = _device_base(base, dev)
+        if pooling_one is None:  # auto: provable only from host offsets (a device copy would sync)
+            pooling_one = (all(n == self.num_bags for n in lens) and off.device.type == "cpu"
+                           and bool(torch.equal(off, torch.arange(self.num_bags, dtype=off.dtype).expand_as(off))))
         if pooling_one and any(n != self.num_bags for n in lens):
             raise ValueError("pooling_one needs exactly one lookup per bag in every table")
         self.pooling_one = bool(pooling_one)
@@ -97,6 +118,18 @@ class LookupBatch:
     @property
     def c(self) -> L.Batch:
         return self._c
+
+    @classmethod
+    def concat(cls, batches: Sequence["LookupBatch"]) -> "LookupBatch":
+        """One batch holding the tables of several batches in order (the per-table batches
+        of a ModuleList's modules, for one launch over their consolidated set). All must
+        have the same number of bags. Device concatenation only, no host sync."""
+        B = batches[0].num_bags
+        if any(b.num_bags != B for b in batches):
+            raise ValueError("all batches must have the same number of bags")
+        idx = [b.idx[b.idx_base_host[t]: b.idx_base_host[t + 1]] for b in batches for t in range(b.num_tables)]
+        off = torch.cat([b.off for b in batches], dim=0)
+        return cls(idx, off, pooling_one=all(b.pooling_one for b in batches))
 
     @classmethod
     def pooling_one(cls, indices: torch.Tensor) -> "LookupBatch":
@@ -120,6 +153,7 @@ class EmbeddingTableSet:
         weights: Sequence[torch.Tensor] | None = None,
     ):
         self.lib = L.load()
+        self.parent, self.parent_index = None, 0  # set on views (EmbeddingTableSet.view)
         self.num_rows = [int(n) for n in num_rows]
         self.T = len(self.num_rows)
         self.D = int(dim)
@@ -157,14 +191,20 @@ class EmbeddingTableSet:
         ).contiguous()
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tflags = torch.zeros(T, dtype=torch.int32, device=dev)
-        self.sdirty = torch.zeros(NS, dtype=torch.uint8, device=dev)
-        self.bdirty = torch.zeros(NB, dtype=torch.uint8, device=dev)
+        # flag arrays padded to whole 32-bit words (the kernels set / read them word-wise)
+        self.sdirty = torch.zeros(_ceil_div(NS, 4) * 4, dtype=torch.uint8, device=dev)
+        self.bdirty = torch.zeros(_ceil_div(NB, 4) * 4, dtype=torch.uint8, device=dev)
+        # per-table arrival counters of the in-launch finalize, one per 256 bytes
+        self.sync = torch.zeros(T * L.DQRM_SYNC_STRIDE, dtype=torch.int32, device=dev)
         self._bws: torch.Tensor | None = None  # backward workspace, grown to the largest batch seen
+        self._err_host: torch.Tensor | None = None  # pinned snapshot of the error word (poll_errors)
+        self._err_evt = None
+        self._err_pending = False
         self._c = L.TableSet(
             T, D, self.R, NB, NS,
             _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
             _ptr(self.tmax), _ptr(self.scale), _ptr(self.pscale), _ptr(self.meta), _ptr(self.err),
-            _ptr(self.tflags), _ptr(self.sdirty), _ptr(self.bdirty),
+            _ptr(self.tflags), _ptr(self.sdirty), _ptr(self.bdirty), _ptr(self.sync),
         )
         if weights is not None:
             if len(weights) != T:
@@ -179,6 +219,43 @@ class EmbeddingTableSet:
     @property
     def c(self) -> L.TableSet:
         return self._c
+
+    def view(self, t: int) -> "EmbeddingTableSet":
+        """Table t of this set as a one-table set over the SAME device memory (its rows,
+        packed rows, |W| maxima, scale, flags and arrival counter; the error word is shared).
+        Kernels launched on the view see and update exactly table t's part of the slabs, so a
+        ModuleList of per-table modules can run on views of one consolidated set while the
+        grad-comm hooks launch once for all tables on the set itself."""
+        if not 0 <= t < self.T:
+            raise IndexError(t)
+        v = object.__new__(EmbeddingTableSet)
+        n = self.num_rows[t]
+        rb, bb, sbb = self.row_base[t], self.blk_base[t], self.sblk_base[t]
+        nb = _ceil_div(n, L.DQRM_BLOCK_ROWS)
+        ns = _ceil_div(nb, L.DQRM_SBLOCK_ROWS // L.DQRM_BLOCK_ROWS)
+        v.lib, v.num_rows, v.T, v.D, v.device = self.lib, [n], 1, self.D, self.device
+        v.row_base, v.blk_base, v.sblk_base, v.R = [0], [0], [0], n
+        v.parent, v.parent_index = self, t
+        v.W = self.W[rb: rb + n]
+        v.packed = self.packed[rb: rb + n] if self.packed is not None else None
+        v.rowmax = self.rowmax[rb: rb + n]
+        v.blkmax = self.blkmax[bb: bb + nb]
+        v.sblkmax = self.sblkmax[sbb: sbb + ns]
+        v.tmax, v.scale, v.pscale = self.tmax[t: t + 1], self.scale[t: t + 1], self.pscale[t: t + 1]
+        v.meta = torch.tensor([[0], [n], [0], [0]], dtype=torch.int64, device=self.device)
+        v.err = self.err
+        v.tflags = self.tflags[t: t + 1]
+        v.sdirty = self.sdirty[sbb:]  # to the end: word-wise flag reads stay inside the allocation
+        v.bdirty = self.bdirty[bb:]
+        v.sync = self.sync[t * L.DQRM_SYNC_STRIDE: (t + 1) * L.DQRM_SYNC_STRIDE]
+        v._bws, v._err_host, v._err_evt, v._err_pending = None, None, None, False
+        v._c = L.TableSet(
+            1, self.D, n, nb, ns,
+            _ptr(v.W), _ptr(v.packed), _ptr(v.rowmax), _ptr(v.blkmax), _ptr(v.sblkmax),
+            _ptr(v.tmax), _ptr(v.scale), _ptr(v.pscale), _ptr(v.meta), _ptr(v.err),
+            _ptr(v.tflags), _ptr(v.sdirty), _ptr(v.bdirty), _ptr(v.sync),
+        )
+        return v
 
     def table_weight(self, t: int) -> torch.Tensor:
         b = self.row_base[t]
@@ -217,6 +294,27 @@ class EmbeddingTableSet:
         word.bitwise_or_(self.err)
         self.err = word
         self._c.err = _ptr(word)
+
+    def poll_errors(self) -> int:
+        """Non-blocking read of the device error flags: the value of the last snapshot whose
+        copy has completed (0 when none has), then a new asynchronous snapshot (pinned host
+        memory, stream-ordered, no host synchronisation) if none is in flight. Flags are
+        sticky on the device until read_errors(clear=True)."""
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self._err_evt = torch.cuda.Event()
+            self._err_pending = False
+        flags = 0
+        if self._err_pending:
+            if not self._err_evt.query():
+                return 0  # the previous snapshot is still in flight
+            flags = int(self._err_host[0])
+            self._err_pending = False
+        if flags == 0:
+            self._err_host.copy_(self.err, non_blocking=True)
+            self._err_evt.record()
+            self._err_pending = True
+        return flags
 
     def read_errors(self, clear: bool = True) -> int:
         f = C.c_uint32(0)
@@ -333,6 +431,10 @@ class EmbeddingTableSet:
         nn.EmbeddingBag(sparse=True)'s backward yields."""
         st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
         Lk = int(batch.idx.numel())
+        if batch.num_bags <= 0:  # no bag covers any lookup: an all-zero gradient on row 0
+            return (torch.zeros(Lk, dtype=torch.int64, device=self.device),
+                    torch.zeros(Lk, self.D, dtype=torch.float32, device=self.device))
+        # every entry is written by the kernel (lookups before off[0] as zero rows, flagged)
         rows = torch.empty(Lk, dtype=torch.int64, device=self.device)
         vals = torch.empty(Lk, self.D, dtype=torch.float32, device=self.device)
         L.check(

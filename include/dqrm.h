@@ -45,8 +45,9 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 3  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
-                               3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap */
+#define DQRM_ABI_VERSION 4  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+                               3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
+                               4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags */
 
 /* status codes */
 #define DQRM_OK            0
@@ -64,6 +65,7 @@ extern "C" {
 #define DQRM_BLOCK_ROWS   256     /* rows per blkmax entry */
 #define DQRM_SBLOCK_ROWS  65536   /* rows per sblkmax entry */
 #define DQRM_TABLE_SPLIT  8       /* workgroups (row-range slots) per table in the backward */
+#define DQRM_SYNC_STRIDE  64      /* uint32 words between two tables' arrival counters */
 #define DQRM_SLOT_KEYS    8192    /* merged payload entries the slot apply kernel sorts on chip
                                      (a fuller slot is applied by the flat method instead) */
 
@@ -85,8 +87,13 @@ typedef struct dqrm_table_set {
     const int64_t* meta;      /* [4][T]: row_base, num_rows, blk_base, sblk_base */
     uint32_t* err;            /* 1 word, device-side error flags */
     uint32_t* tflags;         /* [T] scratch (repack decision), library-internal */
-    uint8_t*  sdirty;         /* [NS] zero-initialised scratch (superblock rescan flags) */
-    uint8_t*  bdirty;         /* [NB] zero-initialised scratch (block rescan flags) */
+    uint8_t*  sdirty;         /* [NS] zero-initialised scratch (superblock rescan flags); the
+                                 allocation is readable up to the next 4-byte boundary */
+    uint8_t*  bdirty;         /* [NB] zero-initialised scratch (block rescan flags), same padding */
+    uint32_t* sync;           /* [T * DQRM_SYNC_STRIDE] zero-initialised scratch: per-table
+                                 arrival counters of the updating kernels (the last workgroup
+                                 of a table finalizes its |W| hierarchy inside the launch), one
+                                 per 256 bytes; library-internal */
 } dqrm_table_set;
 
 /* A batch of lookups for all T tables, in the reference's per-table
@@ -153,10 +160,12 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits,
  * Backward workspace. The three backward calls below (SGD, coalesce, local update) sort
  * the lookups of every (table, row-range slot) by row on the device (in LDS up to 4096
  * lookups, in this workspace beyond) and process the distinct rows from a device-built
- * work list. Its size depends only on the table count and dqrm_batch.max_lookups.
- * Returns the bytes needed (0 on bad arguments). The workspace must be 16-B aligned and
- * ZERO-FILLED before its first use; every call leaves its counters at zero again, so the
- * same buffer is reused without clearing (one call at a time per workspace).
+ * work list. Its size depends only on the table count and dqrm_batch.max_lookups: 16 bytes
+ * up to 4096 lookups per table, T * DQRM_TABLE_SPLIT * max_lookups * 20 bytes beyond (each
+ * of a table's row-range slots gets a spill region for all of the table's lookups, since a
+ * slot's share is only known on the device; e.g. 26 tables x 1 M lookups = 4.2 GB).
+ * Returns the bytes needed (0 on bad arguments). The workspace must be 16-B aligned; it
+ * needs no initialisation (one call at a time per workspace).
  * ------------------------------------------------------------------------------ */
 size_t dqrm_bwd_workspace_bytes(int num_tables, int64_t max_lookups);
 
@@ -324,12 +333,14 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
 #define DQRM_APPLY_SLOT 2
 int dqrm_set_apply_kernel(int kind);
 
-/* Which kernel dqrm_emb_bwd_coalesce launches (process-wide; returns the previous choice,
- * or DQRM_E_INVALID). AUTO (default): batches in the Criteo form (DQRM_BATCH_POOLING_ONE)
- * with num_bags <= 4096 and max_lookups >= num_bags take the Criteo-form kernel
- * (dqrm_coalesce.hip), everything else the general one; GENERAL: always the general
- * kernel. Both give bit-identical workspaces (rows, values, counts; the max over a table's
- * DQRM_TABLE_SPLIT ws_absmax entries). */
+/* Which backward kernels dqrm_emb_bwd_coalesce and dqrm_emb_bwd_sgd launch (process-wide;
+ * returns the previous choice, or DQRM_E_INVALID). AUTO (default): batches in the Criteo
+ * form (DQRM_BATCH_POOLING_ONE) with num_bags <= 4096 and max_lookups >= num_bags take the
+ * Criteo-form coalesce kernel (dqrm_coalesce.hip), and SGD batches of at most 512 lookups
+ * per table (fewer for D > 32) with num_bags * dim <= 16384 the one-workgroup-per-table SGD
+ * kernel; everything else the general (sorting) kernel. GENERAL: always the general
+ * kernel. Both give bit-identical results (coalesce: rows, values, counts, the max over a
+ * table's DQRM_TABLE_SPLIT ws_absmax entries; SGD: W, the |W| maxima, packed rows). */
 #define DQRM_COALESCE_AUTO 0
 #define DQRM_COALESCE_GENERAL 1
 int dqrm_set_coalesce_kernel(int kind);
@@ -442,6 +453,23 @@ int dqrm_criteo_unpack(const int32_t* records, int64_t num_samples, int32_t max_
 /* Synthetic on-device init U(-sqrt(1/n_t), +sqrt(1/n_t)) from a counter-based hash
  * (same distribution as quant_modules_not_quantize_grad.py:273-275; not numpy's stream). */
 int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Replica synchronisation: weight_syncc (sgd_quantized_gradients_parallel_comm.py:963-970,
+ * all_reduce(param, SUM) then param *= 1/N, every 200 iterations of the DP driver,
+ * dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1801,1924-1936).
+ * ------------------------------------------------------------------------------ */
+/* *out (device u64, caller-zeroed) += sum_i mix64(word_i | i << 32) over num_words 32-bit
+ * words of data (16-B aligned): a position-dependent, order-free 64-bit checksum whose
+ * all-gather tells whether every rank holds the same bits. */
+int dqrm_checksum64(const void* data, int64_t num_words, uint64_t* out, void* stream);
+
+/* In place, the reference's all-reduce + scale of num_replicas IDENTICAL replicas of data:
+ * x = fl(fl(...fl(x + x) + x ...) * inv_n), num_replicas - 1 sequential adds -- the order in
+ * which a ring all-reduce (Gloo ring_chunked, RCCL ring) accumulates the ranks. Bit-exact
+ * with that all-reduce when every rank holds x; the identity for num_replicas 1, 2 and 4
+ * with inv_n = 1/num_replicas (barring overflow of num_replicas * x), not for 3 or 8. */
+int dqrm_replica_mean(float* data, int64_t n, int num_replicas, float inv_n, void* stream);
 
 /* Synchronises `stream`, returns the accumulated DQRM_ERRF_* flags in *flags and
  * clears them (if clear != 0). */

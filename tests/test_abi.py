@@ -32,7 +32,7 @@ def test_header_declares_what_binding_expects():
 def test_library_exports_every_header_symbol(lib):
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 3
+    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 4
 
 
 def test_payload_bytes_agree(lib):
@@ -41,8 +41,8 @@ def test_payload_bytes_agree(lib):
 
 
 def test_struct_layouts():
-    # dqrm_table_set: 2 x i32 + 3 x i64 + 13 pointers; dqrm_batch: 3 pointers + 2 x i64
-    assert C.sizeof(L.TableSet) == 8 + 24 + 13 * 8
+    # dqrm_table_set: 2 x i32 + 3 x i64 + 14 pointers; dqrm_batch: 3 pointers + 2 x i64
+    assert C.sizeof(L.TableSet) == 8 + 24 + 14 * 8
     assert C.sizeof(L.Batch) == 6 * 8
 
 

@@ -262,8 +262,10 @@ def test_dp_hooks_over_module_list_of_26_tables(dq, emb_q):
 
 def test_hooks_and_modules_raise_on_device_errors(dq):
     """An out-of-range index is flagged by the kernels and surfaces as DQRMError: from
-    weight_update_parallel_comm for grad_mode="dp", from the next training call for the
-    single-GPU modes (ATen raises on such input; nothing trains on silently)."""
+    weight_update_parallel_comm for grad_mode="dp", from a following training call for the
+    single-GPU modes (ATen raises on such input; nothing trains on silently). The checks
+    poll an asynchronous snapshot of the flag word (no host sync), so the error surfaces
+    once that snapshot has landed: within two calls here."""
     from deep_quantized_recommendation_model_dqrm_amd import _lib as L
     from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
 
@@ -276,12 +278,16 @@ def test_hooks_and_modules_raise_on_device_errors(dq):
     model(torch.rand(B, 13, device="cuda"), lS_o, torch.from_numpy(P).cuda()).sum().backward()
     H.grad_update_parallel_comm(model, 1, num_bits=8)
     with pytest.raises(L.DQRMError, match="0x1"):
-        H.weight_update_parallel_comm(model, 0.1, num_gpus=1)
+        for _ in range(2):
+            H.weight_update_parallel_comm(model, 0.1, num_gpus=1)
+            torch.cuda.synchronize()
     m = _qebt(rows[1], D, Ws[1], grad_mode="fused_sgd", lr=0.1)
     x, off = torch.from_numpy(P[1]).cuda(), torch.arange(B, device="cuda")
     m(x, off).sum().backward()
     with pytest.raises(L.DQRMError):
-        m(x, off)
+        for _ in range(2):
+            m(x, off)
+            torch.cuda.synchronize()
 
 
 def test_weight_syncc_single_rank_is_identity(dq):

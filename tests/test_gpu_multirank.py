@@ -108,7 +108,7 @@ def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits):
 SYNC_ROWS, SYNC_D = [5, 300, 20000], 16
 
 
-def _sync_rank(rank, world, port, out_dir):
+def _sync_rank(rank, world, port, out_dir, same=False):
     sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -120,16 +120,22 @@ def _sync_rank(rank, world, port, out_dir):
             QuantEmbeddingBagCollection)
 
         torch.cuda.set_device(0)
-        torch.manual_seed(rank)  # each rank starts from its own tables and MLP, as the
+        seed = 0 if same else rank
+        torch.manual_seed(seed)  # each rank starts from its own tables and MLP, as the
         # reference's ranks do before the first weight_syncc (dp_one_parallel_comm.py:1801)
         model = nn.Module()
-        Ws = G.table_weights(SYNC_ROWS, SYNC_D, 300 + rank)
+        Ws = G.table_weights(SYNC_ROWS, SYNC_D, 300 + seed)
         model.emb_l = QuantEmbeddingBagCollection(SYNC_ROWS, SYNC_D, weights=[torch.from_numpy(w) for w in Ws],
                                                   grad_mode="dp", use_packed_int4=True)
         model.emb_l._tset.refresh_scale_and_pack(4)
         model.bot_l = nn.Sequential(nn.Linear(13, SYNC_D)).cuda()
         model.top_l = nn.Sequential(nn.Linear(SYNC_D, 1)).cuda()
         before = {n: p.detach().cpu().numpy().copy() for n, p in model.named_parameters()}
+        real = {}
+        for n, p in model.named_parameters():  # the reference's arithmetic, on host copies
+            x = p.detach().cpu().clone()
+            dist.all_reduce(x, dist.ReduceOp.SUM)
+            real[n] = x.mul_(1.0 / world).numpy()
         H.weight_syncc(model, world)
         ts = model.emb_l._tset
         inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
@@ -138,7 +144,7 @@ def _sync_rank(rank, world, port, out_dir):
         after = {n: p.detach().cpu().numpy() for n, p in model.named_parameters()}
         np.savez(os.path.join(out_dir, f"s{rank}.npz"), hier_ok=np.array(hier_ok), packed=ts.packed.cpu().numpy(),
                  scale=ts.scale.cpu().numpy(), **{"b_" + k: v for k, v in before.items()},
-                 **{"a_" + k: v for k, v in after.items()})
+                 **{"a_" + k: v for k, v in after.items()}, **{"r_" + k: v for k, v in real.items()})
     finally:
         dist.destroy_process_group()
 
@@ -171,3 +177,29 @@ def test_weight_syncc_two_ranks_different_tables(tmp_path):
             s = O.table_scale(Wt, 4)
             assert got[r]["scale"][t] == s
             np.testing.assert_array_equal(got[r]["packed"][base[t]: base[t + 1]], O.pack_int4(Wt, s))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_weight_syncc_identical_replicas_local(tmp_path, world):
+    """weight_syncc on bit-identical replicas (what the DP step maintains): one checksum
+    all-gather, then the all-reduce's result computed locally -- the identity at N = 2,
+    fl(fl(x + x) + x) * fl(1/3) at N = 3 (dqrm_replica_mean). Every parameter must equal
+    what Gloo's all_reduce(SUM) * 1/N gives on the same inputs, on every rank, and the |W|
+    hierarchy must equal a rebuild."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mp.spawn(_sync_rank, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True)
+    got = [dict(np.load(os.path.join(tmp_path, f"s{r}.npz"))) for r in range(world)]
+    names = [k[2:] for k in got[0] if k.startswith("b_")]
+    moved = 0
+    for n in names:
+        for r in range(world):
+            np.testing.assert_array_equal(got[r]["b_" + n], got[0]["b_" + n], err_msg=n)  # identical start
+            np.testing.assert_array_equal(got[r]["a_" + n], got[r]["r_" + n], err_msg=n)  # = the all-reduce
+        moved += int(np.sum(got[0]["a_" + n].view(np.int32) != got[0]["b_" + n].view(np.int32)))
+    if world == 2:
+        assert moved == 0
+    else:
+        assert moved > 0  # N = 3 moves about half of the elements by an ulp
+    for r in range(world):
+        assert bool(got[r]["hier_ok"])

@@ -653,6 +653,57 @@ def test_config5_exchange_n8_d64(dq, dist, grad_bits, apply_kernel):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("dist", ["uniform", "zipf"])
+def test_config4_kaggle_full_tables_n4(dq, dist, apply_kernel):
+    """BASELINE config 4 at its own shape (run_dlrm_kaggle_gpu_gtone.sh:1): the 26 full
+    Kaggle tables (33.8 M rows, D=16, on-device init), 4 emulated ranks x 128 samples (global
+    512), INT8 gradients, two steps, both apply kernels. Every touched row equals oracle.dp_step
+    on the compacted rows, the averaged scales equal the oracle's, untouched rows keep their
+    bits, and the incrementally kept |W| hierarchy equals a rebuild."""
+    rows, D, N, Bg = list(G.KAGGLE_ROWS), 16, 4, 512
+    T = len(rows)
+    torch.cuda.empty_cache()
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=91)
+    try:
+        for k in range(2):
+            P = G.pooling_one(rows, Bg, 190 + k, dist=dist)
+            dy = G.upstream_grad(T, Bg, D, 195 + k)
+            sls = [dq.get_my_slice(Bg, N, r) for r in range(N)]
+            Ps = [np.ascontiguousarray(P[:, sl]) for sl in sls]
+            dys = [np.ascontiguousarray(dy[:, sl]) for sl in sls]
+            rank_batches = [dq.LookupBatch.pooling_one(torch.from_numpy(x).cuda()) for x in Ps]
+            ts.forward(rank_batches[0])
+            s_fwd = ts.scale.cpu().numpy()
+            compact, before, probe = [], [], []
+            for t in range(T):  # the rows the step may touch, compacted (host copies stay small)
+                u, inv = np.unique(P[t], return_inverse=True)
+                compact.append((u, inv.astype(np.int64).reshape(P[t].shape)))
+                Wt = ts.table_weight(t)
+                before.append(Wt[torch.from_numpy(u).cuda()].cpu().numpy())
+                mn, mx = torch.aminmax(Wt)
+                assert s_fwd[t] == O.sym_scale(max(-float(mn), float(mx)), 4)
+                free = np.setdiff1d(np.arange(min(rows[t], 4096)), u)[:64]  # untouched rows
+                probe.append((free, Wt[torch.from_numpy(free).cuda()].cpu().numpy()))
+            _, _, s_avg, _ = _emulate_ranks(dq, ts, rank_batches, [torch.from_numpy(d).cuda() for d in dys], 8, 0.1)
+            ar = np.arange(Bg // N, dtype=np.int64)
+            res = O.dp_step(before, [[(compact[t][1][sl], ar) for t in range(T)] for sl in sls],
+                            [[dys[r][t] for t in range(T)] for r in range(N)], list(s_fwd), 0.1, grad_bits=8)
+            np.testing.assert_array_equal(s_avg.cpu().numpy(), np.array([x[0] for x in res], np.float32))
+            for t in range(T):
+                got = ts.table_weight(t)[torch.from_numpy(compact[t][0]).cuda()].cpu().numpy()
+                np.testing.assert_array_equal(got, before[t])
+                free, wf = probe[t]
+                np.testing.assert_array_equal(ts.table_weight(t)[torch.from_numpy(free).cuda()].cpu().numpy(), wf)
+        assert ts.read_errors() == 0
+        inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+        ts.refresh_absmax()
+        for x, y in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
+            assert torch.equal(x, y)
+    finally:
+        del ts
+        torch.cuda.empty_cache()
+
+
 def test_terabyte_full_size_773m_rows(dq):
     """The bench's N=1 workload at full size (26 tables, 773,280,534 rows x 64, 198 GB in
     HBM): forward of every table equals the oracle on the rows it reads, the per-step table

@@ -2,7 +2,9 @@
 """Summarise a rocprofv3 run of bench.py (tools/prof_cfg.sh) into profiles/:
 
   <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim copy)
-  <tag>_summary.json       per libdqrm kernel: calls, average duration (us), and the
+  <tag>_summary.json       per libdqrm kernel: calls, average and MEDIAN duration (us, the
+                           median from the per-dispatch kernel trace, so a rare outlier
+                           does not move roofline fractions), and the
                            per-launch HBM traffic from the separate --pmc passes:
                            FETCH_SIZE x 2 (gfx950 reports half the bytes of wide coalesced
                            reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, in bytes.
@@ -31,6 +33,18 @@ def main(src: str, tag: str) -> None:
         k = short(r["Name"])
         if k.startswith("k_"):
             out[k] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3}
+    trace = stats.replace("kernel_stats.csv", "kernel_trace.csv")
+    try:
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(trace)):
+            durs[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for k, v in out.items():
+            d = sorted(durs.get(k, []))
+            if d:
+                v["median_us"] = d[len(d) // 2]
+                v["p10_us"], v["p90_us"] = d[len(d) // 10], d[(len(d) * 9) // 10]
+    except (OSError, KeyError, ValueError):
+        pass
     counters = {}
     for f, cname in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         acc = collections.defaultdict(list)
@@ -48,7 +62,8 @@ def main(src: str, tag: str) -> None:
                "kernels": out}, open(f"{tag}_summary.json", "w"), indent=1)
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
         hb = v["hbm_bytes_per_launch"]
-        print(f"{k:32s} calls={v['calls']:4d} avg={v['avg_us']:10.2f} us  hbm/launch="
+        print(f"{k:32s} calls={v['calls']:4d} avg={v['avg_us']:10.2f} us  median={v.get('median_us', float('nan')):8.2f}"
+              f"  hbm/launch="
               f"{(hb / 1e6 if hb is not None else float('nan')):10.2f} MB")
 
 
