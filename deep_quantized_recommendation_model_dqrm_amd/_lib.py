@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_bwd_sgd",
     "dqrm_coalesce_slot_caps",
     "dqrm_emb_bwd_coalesce",
+    "dqrm_emb_bwd_coalesce_scaled",
     "dqrm_emb_bwd_lookup_grad",
     "dqrm_rows_changed",
     "dqrm_payload_bytes",
@@ -183,6 +184,10 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_emb_bwd_coalesce": (
             C.c_int,
             [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P, P, P, P, C.c_size_t, P],
+        ),
+        "dqrm_emb_bwd_coalesce_scaled": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_int, P, P, P, P, P, P, C.c_size_t, P],
         ),
         "dqrm_emb_bwd_lookup_grad": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P]),
         "dqrm_rows_changed": (C.c_int, [TS, P, C.c_int64, C.c_int, P]),

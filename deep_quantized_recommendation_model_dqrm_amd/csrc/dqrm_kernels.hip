@@ -1520,6 +1520,7 @@ struct DySource {
     float s;
     int ste;
     int off4;
+    float div = 1.0f;   // dqrm_emb_bwd_coalesce_scaled: g' / div (simulated DP's grad / N)
     using Raw = float4;
     DQRM_INLINE float4 fetch(uint32_t bag, int sub) const {
         return reinterpret_cast<const float4*>(base + (int64_t)bag * st_b)[off4 + sub];
@@ -1527,6 +1528,9 @@ struct DySource {
     DQRM_INLINE float4 finish(float4 g) const {
         if (ste) {
             g.x = (g.x * s) / s; g.y = (g.y * s) / s; g.z = (g.z * s) / s; g.w = (g.w * s) / s;
+        }
+        if (div != 1.0f) {
+            g.x = g.x / div; g.y = g.y / div; g.z = g.z / div; g.w = g.w / div;
         }
         return g;
     }
@@ -2597,6 +2601,7 @@ struct FArgs {
     uint8_t* bdirty;
     uint32_t* sync;
     int fin_launch;
+    float div;                   // MODE 1: divide each lookup's gradient by this (1 = not)
     const float* scale;
     const float* pscale;
     const int64_t* meta;
@@ -3041,7 +3046,7 @@ DQRM_INLINE void fused_slot(const FArgs& a, unsigned char* lds, int k, int t, in
     DIAG_T(1);
     // 2. prefetch this workgroup's slice of every gathered lookup's dy row into registers:
     //    the loads stay in flight across the sort (barriers wait for LDS traffic only)
-    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, dsplit ? z * LG : 0};
+    const DySource src{a.dy + (int64_t)t * a.dst_t, a.dst_b, a.scale[t], a.ste, dsplit ? z * LG : 0, a.div};
     float4 pfv[FB_PFR];
     if (pf) {
 #pragma unroll
@@ -3878,6 +3883,7 @@ struct BwdCall {
     float* ws_absmax;
     void* ws;
     size_t ws_bytes;
+    float div = 1.0f;
 };
 
 int64_t bwd_lookup_cap(const dqrm_batch* batch) { return batch->max_lookups > 0 ? batch->max_lookups : 1; }
@@ -3899,7 +3905,7 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     fused_ws_layout(reinterpret_cast<unsigned char*>(c.ws), T, Lc, &fa);
     fa.W = set->W; fa.packed = set->packed; fa.rowmax = set->rowmax; fa.blkmax = set->blkmax;
     fa.sblkmax = set->sblkmax; fa.tmax = set->tmax; fa.sdirty = set->sdirty; fa.bdirty = set->bdirty;
-    fa.sync = set->sync; fa.fin_launch = finalize_launch();
+    fa.sync = set->sync; fa.fin_launch = finalize_launch(); fa.div = c.div;
     fa.scale = set->scale; fa.pscale = set->pscale; fa.meta = set->meta; fa.err = set->err;
     fa.idx = c.batch->idx; fa.off = c.batch->off; fa.idx_base = c.batch->idx_base; fa.B = c.batch->num_bags;
     fa.pool1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
@@ -4202,6 +4208,29 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
         return DQRM_OK;
     }
     return launch_bwd<1>(c, (hipStream_t)stream, "dqrm_emb_bwd_coalesce");
+}
+
+int dqrm_emb_bwd_coalesce_scaled(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                                 int64_t dy_stride_t, int64_t dy_stride_b, int ste, int divisor,
+                                 const int64_t* ws_cap_base, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
+                                 float* ws_absmax, void* workspace, size_t workspace_bytes, void* stream) {
+    if (divisor < 1) return set_error(DQRM_E_INVALID, "%s: divisor must be >= 1", "dqrm_emb_bwd_coalesce_scaled");
+    if (divisor == 1)
+        return dqrm_emb_bwd_coalesce(set, batch, dy, dy_stride_t, dy_stride_b, ste, ws_cap_base, ws_rows, ws_vals,
+                                     ws_ucount, ws_absmax, workspace, workspace_bytes, stream);
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_coalesce_scaled"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0",
+                         "dqrm_emb_bwd_coalesce_scaled");
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !ws_absmax || (((uintptr_t)ws_vals) & 15))
+        return set_error(DQRM_E_INVALID, "%s: null/unaligned workspace", "dqrm_emb_bwd_coalesce_scaled");
+    BwdCall c{};
+    c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
+    c.ws_cap_base = ws_cap_base; c.ws_rows = ws_rows; c.ws_vals = ws_vals; c.ws_ucount = ws_ucount;
+    c.ws_absmax = ws_absmax; c.ws = workspace; c.ws_bytes = workspace_bytes; c.div = (float)divisor;
+    return launch_bwd<1>(c, (hipStream_t)stream, "dqrm_emb_bwd_coalesce_scaled");  // the general kernel
 }
 
 size_t dqrm_payload_bytes(int num_tables, int64_t cap_total, int dim, int grad_bits) {

@@ -24,7 +24,7 @@ import torch
 from . import _lib as L
 from .comm import HipExchangeKernels, payload_bytes
 from .quant_modules_not_quantize_grad import _QuantEmbeddingBase
-from .tables import CoalescedGrad, default_caps
+from .tables import CoalescedGrad, LookupBatch, default_caps
 
 GRAD_BITS = 8  # the reference hard-codes num_bits = 8 here (:77,:80)
 
@@ -62,9 +62,20 @@ def _emb_modules(model) -> list[_QuantEmbeddingBase]:
 
 
 def grad_buffer_update_added_quantization(model, number_of_gpus, emb_grad_quantized=True) -> None:
-    """sgd_quantized_gradients.py:56-94 (embedding branch), one micro-step."""
+    """sgd_quantized_gradients.py:56-94 (embedding branch), one micro-step. Unquantized
+    (emb_grad_quantized=False, :88-91): the micro-step's lookups and upstream gradient are
+    kept on the device; the update applies buffer = sum of grad / N in the reference's order."""
     if not emb_grad_quantized:
-        raise NotImplementedError("the unquantized simulated buffer (grad / N accumulation) is not built")
+        with torch.no_grad():
+            for m in _emb_modules(model):
+                if m._pending is None:
+                    continue
+                fb = getattr(m, "_sim_fp32", None)
+                if fb is None:
+                    fb = m._sim_fp32 = []
+                fb.append((m._pending, int(number_of_gpus)))
+                m._pending = None
+        return
     with torch.no_grad():
         for m in _emb_modules(model):
             if m._pending is None:
@@ -87,10 +98,44 @@ def grad_buffer_update_added_quantization(model, number_of_gpus, emb_grad_quanti
             m._pending = None
 
 
+def _apply_fp32_buffer(m: _QuantEmbeddingBase, lr: float) -> None:
+    """The unquantized buffer's update (:374-377): W.add_(-lr * buffer), where the buffer is
+    sum over the micro-steps, in order, of grad / N (grad_buffer_update_added_quantization,
+    :88-91: buffer.add_(grad / N); buffer.coalesce()). The micro-steps' batches are joined
+    bag after bag; one coalesce divides every lookup's gradient by N before the ordered sum
+    (dqrm_emb_bwd_coalesce_scaled), and the FP32 payload path applies W + (-lr * buffer)."""
+    items = m._sim_fp32
+    ts = m._tset
+    (b0, _, ste, layout), N = items[0]
+    if any(it[1] != N for it in items) or any(it[0][2] != ste for it in items):
+        raise ValueError("micro-steps of one accumulation differ in number_of_gpus or full precision")
+    batch = LookupBatch.concat_bags([it[0][0] for it in items])
+    if layout != "tbd":
+        raise ValueError("the simulated buffer expects tbd-layout gradients")
+    dy = torch.cat([it[0][1].reshape(ts.T, it[0][0].num_bags, ts.D) for it in items], dim=1)
+    ws = CoalescedGrad.allocate(ts.num_rows, max(batch.max_lookups, 1), ts.D, ts.device)
+    ts.backward_coalesce_scaled(batch, dy, ws, N, ste=ste)
+    caps = default_caps(ts.num_rows, max(batch.max_lookups, 1))
+    base = [0]
+    for c in caps:
+        base.append(base[-1] + c)
+    cap_base = torch.tensor(base, dtype=torch.int64, device=ts.device)
+    pb = payload_bytes(ts.T, base[-1], ts.D, 32)
+    payload = torch.zeros(pb, dtype=torch.uint8, device=ts.device)
+    k = HipExchangeKernels(ts)
+    k.quant_pack(ws, None, 1, 32, cap_base, base[-1], None, payload)
+    k.apply(cap_base, base[-1], payload.view(1, -1), pb, 1, 32, None, lr, L.DQRM_UPD_FP32, m._use_packed(False))
+
+
 def weights_update_added_quantization(model, lr, num_gpus, emb_grad_quantized=True, update_embedding=True) -> None:
-    """sgd_quantized_gradients.py:349-379 (embedding branch): W += -lr * buffer * (s / N)."""
+    """sgd_quantized_gradients.py:349-379 (embedding branch): W += -lr * buffer * (s / N);
+    unquantized (:374-377): W += -lr * buffer."""
     if not emb_grad_quantized:
-        raise NotImplementedError("the unquantized simulated buffer (grad / N accumulation) is not built")
+        with torch.no_grad():
+            for m in _emb_modules(model):
+                if update_embedding and getattr(m, "_sim_fp32", None):
+                    _apply_fp32_buffer(m, lr)
+        return
     with torch.no_grad():
         if not update_embedding:
             return
@@ -112,6 +157,7 @@ def grad_buffer_zeroing(model) -> None:
         if buf is not None:
             buf.payloads.clear()
             buf.first_absmax = None
+        m._sim_fp32 = []
         m.emb_scaling_factor.zero_()
 
 

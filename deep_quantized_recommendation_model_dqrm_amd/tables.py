@@ -132,6 +132,24 @@ class LookupBatch:
         return cls(idx, off, pooling_one=all(b.pooling_one for b in batches))
 
     @classmethod
+    def concat_bags(cls, batches: Sequence["LookupBatch"]) -> "LookupBatch":
+        """The bags of several batches of the same tables back to back (batch i's bags after
+        batch i-1's, per table; lookups likewise): the simulated-DP micro-steps as one batch.
+        Device concatenation and an offset shift per (batch, table); no host sync."""
+        T = batches[0].num_tables
+        if any(b.num_tables != T for b in batches):
+            raise ValueError("all batches must have the same tables")
+        idx, off = [], []
+        shift = [0] * T
+        for b in batches:
+            off.append(b.off + _device_base(list(shift), b.off.device).view(T, 1))
+            for t in range(T):
+                shift[t] += b.lookups[t]
+        for t in range(T):
+            idx.append(torch.cat([b.idx[b.idx_base_host[t]: b.idx_base_host[t + 1]] for b in batches]))
+        return cls(idx, torch.cat(off, dim=1), pooling_one=all(b.pooling_one for b in batches))
+
+    @classmethod
     def pooling_one(cls, indices: torch.Tensor) -> "LookupBatch":
         """Criteo form: one index per (table, sample); offsets = arange(B) per table."""
         T, B = indices.shape
@@ -423,6 +441,19 @@ class EmbeddingTableSet:
         rows = rows.to(device=self.device, dtype=torch.int64).contiguous()
         L.check(self.lib.dqrm_rows_changed(C.byref(self._c), _ptr(rows), rows.numel(), 4 if repack else 0,
                                            _stream_handle()), "dqrm_rows_changed")
+
+    def backward_coalesce_scaled(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad", divisor: int,
+                                 ste: bool = True, layout: str = "tbd") -> None:
+        """backward_coalesce with every lookup's gradient divided by `divisor` before the
+        sum (dqrm_emb_bwd_coalesce_scaled; the simulated-DP buffer's grad / N)."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_coalesce_scaled(
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), int(divisor), _ptr(ws.slot_cap_base),
+                _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), *self._ws_args(batch),
+                _stream_handle()),
+            "dqrm_emb_bwd_coalesce_scaled",
+        )
 
     def lookup_grad(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True,
                     layout: str = "tbd") -> tuple[torch.Tensor, torch.Tensor]:

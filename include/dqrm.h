@@ -213,6 +213,18 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch,
                           int32_t* ws_ucount, float* ws_absmax, void* workspace, size_t workspace_bytes,
                           void* stream);
 
+/* dqrm_emb_bwd_coalesce with every lookup's gradient divided by `divisor` before the
+ * coalescing sum: values = sum over the row's lookups, in lookup order, of
+ * ((dy*s)/s) / divisor -- the unquantized simulated-DP buffer of sgd_quantized_gradients.py:88-91
+ * (embedding_grad_buffer.add_(grad / number_of_gpus); .coalesce()) when the batch holds the
+ * N micro-steps' lookups back to back. Always the general (sorting) kernel; divisor 1 is
+ * dqrm_emb_bwd_coalesce. */
+int dqrm_emb_bwd_coalesce_scaled(const dqrm_table_set* set, const dqrm_batch* batch,
+                                 const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
+                                 int ste, int divisor, const int64_t* ws_cap_base, int32_t* ws_rows,
+                                 float* ws_vals, int32_t* ws_ucount, float* ws_absmax, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+
 /* Per-lookup (uncoalesced) sparse gradient, the COO nn.EmbeddingBag(mode="sum",
  * sparse=True) produces (embedding_bag_backward, sparse branch): for every lookup j of
  * table t, in lookup order, rows[j] = row_base[t] + idx[j] (slab row) and

@@ -223,16 +223,22 @@ class ListDLRM(nn.Module):
         return self.top_l(torch.cat([x] + ly, dim=1))
 
 
+@pytest.mark.parametrize("consolidate", [True, False])
 @pytest.mark.parametrize("emb_q", [True, False])
-def test_dp_hooks_over_module_list_of_26_tables(dq, emb_q):
+def test_dp_hooks_over_module_list_of_26_tables(dq, emb_q, consolidate):
     """grad_update / weight_update_parallel_comm over a ModuleList of 26 single-table
-    modules run ONE exchange for all of them (one MultiSetExchange: 2 collectives/step at
-    N>1) and match oracle.dp_step table by table; emb_scaling_factor per module."""
+    modules run ONE exchange for all of them and match oracle.dp_step table by table;
+    emb_scaling_factor per module. consolidate: the hooks move the 26 tables into one table
+    set on first use (one coalesce / quantize-pack / apply launch per step for all tables,
+    the modules running on one-table views of it); otherwise one MultiSetExchange over the
+    modules' own sets (launches per module, still 2 collectives per step at N>1)."""
     from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+    from deep_quantized_recommendation_model_dqrm_amd.comm import ConsolidatedExchange, MultiSetExchange
 
     rows, D, B = [min(n, 20000) for n in G.KAGGLE_ROWS], 16, 128
     Ws = G.table_weights(rows, D, 61)
     torch.manual_seed(0)
+    H.set_consolidate_tables(consolidate)
     model = ListDLRM(rows, D, Ws)
     Wo = [w.copy() for w in Ws]
     for k in range(2):
@@ -250,8 +256,15 @@ def test_dp_hooks_over_module_list_of_26_tables(dq, emb_q):
         if emb_q:
             for t, m in enumerate(model.emb_l):
                 assert m.emb_scaling_factor.item() == res[t][0]
+    H.set_consolidate_tables(True)
     ex = model._dqrm_emb_exchange[1]
-    assert len(ex.parts) == len(rows)  # one exchange object for all 26 modules
+    if consolidate:  # one exchange over one set, the modules on views of it
+        assert isinstance(ex, ConsolidatedExchange) and ex.tables.T == len(rows)
+        assert all(m._tset.parent is ex.tables and m._tset.parent_index == t for t, m in enumerate(model.emb_l))
+        assert all(m.embedding_bag.weight.data_ptr() == ex.tables.table_weight(t).data_ptr()
+                   for t, m in enumerate(model.emb_l))
+    else:
+        assert isinstance(ex, MultiSetExchange) and len(ex.parts) == len(rows)
     assert len({m._tset.err.data_ptr() for m in model.emb_l}) == 1  # one error word, one read per step
     for t, m in enumerate(model.emb_l):
         np.testing.assert_array_equal(m.embedding_bag.weight.detach().cpu().numpy(), Wo[t])
@@ -337,6 +350,36 @@ def test_simulated_dp_module_api(dq):
         b_rows = np.array(sorted(buf), dtype=np.int64)
         O.simulated_dp_apply(Wo[t], b_rows, np.stack([buf[r] for r in b_rows.tolist()]), s, N, 0.1)
         np.testing.assert_array_equal(model.emb_l.table_weight(t).detach().cpu().numpy(), Wo[t])
+
+
+def test_simulated_dp_unquantized_module_api(dq):
+    """sgd_quantized_gradients.py:88-91 + :374-377 (emb_grad_quantized=False): the buffer
+    sums grad / N per lookup in micro-step order; W += -lr * buffer. Bit-exact vs the oracle."""
+    from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients as S
+
+    rows, D, B, N = [6, 700, 40000], 16, 128, 3
+    Ws = G.table_weights(rows, D, 15)
+    model = TinyDLRM(dq, rows, D, Ws)
+    Wo = [w.copy() for w in Ws]
+    s_fwd = [O.table_scale(w, 4) for w in Wo]
+    batches, dys = [[] for _ in rows], [[] for _ in rows]
+    S.grad_buffer_zeroing(model)
+    for k in range(N):
+        P = G.pooling_one(rows, B, 60 + k, dist="zipf")
+        out = model(torch.rand(B, 13, device="cuda"), torch.arange(B, device="cuda").repeat(len(rows), 1),
+                    torch.from_numpy(P).cuda())
+        out.pow(2).mean().backward()
+        dy_np = model.emb_l._pending[1].detach().permute(1, 0, 2).contiguous().cpu().numpy()
+        S.grad_buffer_update_added_quantization(model, N, emb_grad_quantized=False)
+        for t in range(len(rows)):
+            batches[t].append((P[t], np.arange(B)))
+            dys[t].append(dy_np[t])
+    S.weights_update_added_quantization(model, 0.1, N, emb_grad_quantized=False)
+    for t in range(len(rows)):
+        O.simulated_dp_fp32(Wo[t], batches[t], dys[t], s_fwd[t], N, 0.1)
+        np.testing.assert_array_equal(model.emb_l.table_weight(t).detach().cpu().numpy(), Wo[t])
+    S.grad_buffer_zeroing(model)
+    assert model.emb_l._sim_fp32 == []
 
 
 @pytest.mark.parametrize("packed", [False, True])
