@@ -8,8 +8,9 @@
   comm      RCCL all-gather of the per-slot max|grad|, quantize-pack to INT8, RCCL
             all-gather of the fixed-capacity {rows, int8} payloads
   update    decode all ranks' payloads, integer union-sum, dequant, SGD (+ INT4 repack)
-  At N=1 there is nothing to exchange: quantize-pack + apply run fused (dqrm_apply_local,
-  the same arithmetic, bit-identical W; --unfused-local times the payload round trip).
+  At N=1 there is nothing to exchange: backward + quantize + update run as ONE launch
+  (dqrm_emb_bwd_apply_local; bit-identical W): --two-launch-local times the coalesce +
+  dqrm_apply_local pair, --unfused-local the payload round trip.
 --mode fwd (BASELINE config 2) the forward alone.
 --mode sgd (BASELINE config 3) forward + fused STE/sparse-backward/SGD (dqrm_emb_bwd_sgd).
 --graph captures one step per resident batch in a HIP graph (torch.cuda.CUDAGraph) and
@@ -98,6 +99,8 @@ def parse(argv=None):
                    help="nccl (= RCCL on ROCm) for measurements; gloo only to rehearse N>1 on one GPU")
     p.add_argument("--unfused-local", action="store_true",
                    help="N=1: run quant-pack + payload apply instead of the fused dqrm_apply_local")
+    p.add_argument("--two-launch-local", action="store_true",
+                   help="N=1: coalesce + dqrm_apply_local as two launches (not dqrm_emb_bwd_apply_local)")
     p.add_argument("--sample-every", type=int, default=8,
                    help="bracket the dominant kernel with HIP events on every k-th timed step")
     p.add_argument("--traffic-profile", default=None,
@@ -110,7 +113,8 @@ PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "kaggle": "kaggle"}
 KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
     "emb_fwd": "k_emb_fwd<{lpr},",
     "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
-    "bwd_coalesce": ("k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),  # Criteo-form batches / general
+    "bwd_coalesce": ("k_coalesce_p1<false>", "k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),  # Criteo form / general
+    "bwd_apply_local": ("k_coalesce_p1<true>",),  # N=1: coalesce + update in one launch
     "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "grad_quant_pack": "k_quant_pack<{lpr}>",
     "apply_sparse_update": "k_apply_flat<{lpr},",
@@ -158,6 +162,8 @@ def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
         "bwd_coalesce": L * 8 + offs + L * D * 4 + U * (D * 4 + 4),
         # index + dy row per lookup; W row read+write and |W| row max per distinct row
         "bwd_sgd": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
+        # N=1 backward + update in one launch: as bwd_sgd (the coalesced rows never need HBM)
+        "bwd_apply_local": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
         "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
         "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4 + pk,
         "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4 + pk,
@@ -177,12 +183,14 @@ def timed_events(n):
     return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
 
 
-def phase_names(mode, use_packed, fused):
+def phase_names(mode, use_packed, fused, one_launch=False):
     fwd = "emb_fwd_packed" if use_packed else "emb_fwd"
     if mode == "fwd":
         return [fwd]
     if mode == "sgd":
         return [fwd, "bwd_sgd"]
+    if fused and one_launch:
+        return [fwd, "bwd_apply_local"]
     return [fwd, "bwd_coalesce"] + (["apply_local"] if fused else ["grad_quant_pack", "apply_sparse_update"])
 
 
@@ -237,8 +245,10 @@ def main():
     # N=1: quantize-pack + apply fused (dqrm_apply_local; same quantize/dequantize/SGD
     # arithmetic, bit-identical W, no payload since nothing is exchanged)
     fused = world == 1 and not a.unfused_local
+    # one launch (dqrm_emb_bwd_apply_local) for Criteo-form batches of <= 4096 lookups, <= 32 tables
+    one_launch = fused and not a.two_launch_local and B <= 4096 and T <= 32
     repack = a.use_packed
-    names = phase_names(a.mode, a.use_packed, fused)
+    names = phase_names(a.mode, a.use_packed, fused, one_launch)
 
     def step(i, ev=None, only=None, refresh=None):
         """One step of the selected mode. ev: per-phase (start, end) events; only: bracket
@@ -267,6 +277,10 @@ def main():
             mark(1, 1)
             return
         kern = ex.kernels
+        if one_launch:
+            kern.coalesce_apply_local(b, dy, ex.ws, True, "tbd", a.grad_bits, ex.s_avg, a.lr, repack)
+            mark(1, 1)
+            return
         kern.coalesce(b, dy, ex.ws, True, "tbd")
         mark(1, 1)
         if fused:
@@ -450,6 +464,9 @@ def main():
                 "grad_bits": a.grad_bits if a.mode == "dp" else None,
                 "scale_period": max(a.scale_period, 1), "packed_int4_forward": a.use_packed,
                 "hip_graph": a.graph, "graph_steps": gs if a.graph else None,
+                "n1_update": (None if a.mode != "dp" or world > 1 else
+                              "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
+                              "coalesce + dqrm_apply_local" if fused else "coalesce + quant-pack + payload apply"),
                 "parallelism": f"dp{world} (tables replicated)",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -16,6 +16,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_coalesce.hip", "dqrm_dense.hip",
                                                 "dqrm_input.hip", "dqrm_sync.hip")]
+DEVICE_HEADER = os.path.join(CSRC_DIR, "dqrm_device.h")
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
 INTERNAL_HEADER = os.path.join(CSRC_DIR, "dqrm_internal.h")
 LIB_PATH = os.path.join(PKG_DIR, "libdqrm.so")
@@ -49,7 +50,7 @@ def _stale(out: str, deps) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(LIB_PATH, [*SOURCES, HEADER, INTERNAL_HEADER, __file__])
+    return _stale(LIB_PATH, [*SOURCES, HEADER, INTERNAL_HEADER, DEVICE_HEADER, __file__])
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
@@ -60,7 +61,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     objs, jobs = [], []
     for src in SOURCES:  # translation units compile in parallel (one hipcc each)
         obj = _obj(src)
-        if force or _stale(obj, [src, HEADER, INTERNAL_HEADER, __file__]):
+        if force or _stale(obj, [src, HEADER, INTERNAL_HEADER, DEVICE_HEADER, __file__]):
             tmp = obj + ".tmp.o"
             cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO_DIR, "include"), "-c", src, "-o", tmp]
             if verbose:

@@ -21,6 +21,7 @@ DQRM_BATCH_POOLING_ONE = 1
 DQRM_ERRF_INDEX = 1
 DQRM_ERRF_OFFSET = 2
 DQRM_ERRF_OVERFLOW = 4
+DQRM_ERRF_STALL = 8
 
 DQRM_BLOCK_ROWS = 256
 DQRM_SBLOCK_ROWS = 65536
@@ -50,7 +51,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 4  # include/dqrm.h
+DQRM_ABI_VERSION = 5  # include/dqrm.h
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
@@ -72,6 +73,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_apply_sparse_update",
     "dqrm_apply_sparse_update_strided",
     "dqrm_apply_local",
+    "dqrm_emb_bwd_apply_local",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
     "dqrm_dense_grad_quant",
@@ -219,6 +221,11 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_apply_local": (
             C.c_int,
             [TS, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P],
+        ),
+        "dqrm_emb_bwd_apply_local": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P,
+             C.c_size_t, P],
         ),
         "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
         "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),

@@ -47,6 +47,9 @@ class ExchangeKernels(Protocol):
     def local_update(self, batch: LookupBatch, dy: torch.Tensor, ste: bool, layout: str, lr: float,
                      table_mask: torch.Tensor, repack: bool) -> None: ...
 
+    def coalesce_apply_local(self, batch: LookupBatch, dy: torch.Tensor, ws: CoalescedGrad, ste: bool, layout: str,
+                             grad_bits: int, s_avg: torch.Tensor, lr: float, repack: bool) -> None: ...
+
 
 class HipExchangeKernels:
     """libdqrm kernels; the only implementation the product uses."""
@@ -91,6 +94,10 @@ class HipExchangeKernels:
                 _ptr(ws.absmax), grad_bits, _ptr(s_avg), float(lr), 4 if repack else 0, _stream_handle()),
             "dqrm_apply_local",
         )
+
+    def coalesce_apply_local(self, batch, dy, ws, ste, layout, grad_bits, s_avg, lr, repack):
+        """world size 1: coalesce + apply_local, one launch for Criteo-form batches."""
+        self.tables.backward_apply_local(batch, dy, ws, grad_bits, s_avg, lr, repack=repack, ste=ste, layout=layout)
 
     def quant_pack_ranked(self, ws, table_bits, table_scale, cap_base, cap_total, payload):
         t = self.tables
@@ -228,6 +235,10 @@ class SparseGradExchange:
         fused = getattr(self.kernels, "apply_local", None)
         if (fused is not None and self.world == 1 and 2 <= gb <= 16
                 and (mode is None or mode == L.DQRM_UPD_DP)):
+            one = getattr(self.kernels, "coalesce_apply_local", None)
+            if one is not None:  # the whole local step in one launch (Criteo-form batches)
+                one(batch, dy, self.ws, ste, layout, gb, self.s_avg, lr, repack)
+                return
             self.kernels.coalesce(batch, dy, self.ws, ste, layout)
             fused(self.ws, gb, self.s_avg, lr, repack)
             return

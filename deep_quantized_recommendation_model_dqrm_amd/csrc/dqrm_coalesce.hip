@@ -38,6 +38,7 @@
 #include <stdint.h>
 
 #include "../../include/dqrm.h"
+#include "dqrm_device.h"
 #include "dqrm_internal.h"
 
 namespace {
@@ -53,7 +54,6 @@ __device__ unsigned long long g_coal_clk[8192 * 16];
 #define CDIAG_W(k) do { } while (0)
 #endif
 
-constexpr int WAVE = 64;
 #ifndef DQRM_COAL_TPB
 #define DQRM_COAL_TPB 1024
 #endif
@@ -64,7 +64,6 @@ constexpr int TPB = DQRM_COAL_TPB;
 constexpr int NW = TPB / WAVE;
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
 static_assert(SPLIT == 8, "the XCD-aware block map puts a table's SPLIT slots on one XCD");
-constexpr int BLK = DQRM_BLOCK_ROWS;
 constexpr int MAXB = (int)dqrm_internal::kCoalesceMaxB;
 constexpr int MAXI = MAXB / TPB;  // lookups per thread
 constexpr int PFR = DQRM_COAL_PFR;  // prefetched float4 per thread
@@ -120,8 +119,13 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
 __device__ __forceinline__ uint32_t krow(uint64_t x) { return (uint32_t)(x >> 32); }
 __device__ __forceinline__ uint32_t kgat(uint64_t x) { return (uint32_t)x >> LK_BITS; }
 __device__ __forceinline__ uint32_t kbag(uint64_t x) { return (uint32_t)x & LK_MASK; }
-__device__ __forceinline__ float abs_max4(float4 v) {
-    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+// 16-B load of bytes another workgroup of the launch stored write-through (sc1): an sc1
+// buffer load (L2-served, past this CU's L1), tracked by the compiler's vmcnt accounting
+__device__ __forceinline__ float4 ld4_sc1(const float* base, uint32_t byte_off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16 /* sc1 */);
+    return make_float4(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]), __uint_as_float(x[3]));
 }
 
 // Items (i, tid), i < ni, in the order i * TPB + tid: the ones whose pred holds get
@@ -377,7 +381,23 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
     return acc;
 }
 
-__global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs a) {
+#ifndef DQRM_COAL_WPF
+#define DQRM_COAL_WPF 4
+#endif
+constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
+constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
+constexpr int RDV_WORD = 32;        // the table's gradient-max rendezvous counter in its sync words
+constexpr int DIRTY_WORD = 16;      // ... and its "a superblock was flagged" counter
+
+// APPLY (dqrm_emb_bwd_apply_local, world size 1): after the coalesce, the table's workgroups
+// meet once (each publishes its max|grad|, then waits for the table's others: all of them are
+// resident, one per CU), and each updates the rows of its row-range slot exactly as
+// k_apply_local does -- quantize with the table scale, SGD, rowmax, block maxima it owns
+// re-reduced here, superblock / table growth by atomicMax, shrunk superblocks flagged for the
+// table's last workgroup. The W rows are loaded before the segment phase, so the update's
+// random-row latency hides behind the coalesce.
+template <bool APPLY>
+__global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs a, dqrm_internal::LocalApplyArgs la) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int s_cnt[MAXI * NW];
     __shared__ int s_cnt2[MAXI * NW];
@@ -388,6 +408,10 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_uf[SPLIT + 1];
     __shared__ int s_ucnt[SPLIT];
     __shared__ float s_red[NW];
+    __shared__ float s_am;
+    __shared__ int s_oq_n;
+    __shared__ uint32_t s_oq_blk[OWN_Q];
+    __shared__ float s_oq_old[OWN_Q];
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
     uint16_t* pos = reinterpret_cast<uint16_t*>(lds + OFF_POS);
     uint16_t* hpos = reinterpret_cast<uint16_t*>(lds + OFF_HPOS);
@@ -792,6 +816,39 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     }
     }  // comparison sort
     CDIAG(4);
+    // fused update: the entries of row-range slot sl are segments [ua, ua + nu) (a dimension-
+    // split table: its rows in that range; a row split: all of the slot's), entry s_cb[sl] +
+    // (u - ua). Workgroup s updates slots s, s + NA, ... (NA = the table's active workgroups).
+    const int NA = dsplit ? DS : SPLIT;
+    const int lpr_sh = __ffs(LPR) - 1;
+    auto slot_entries = [&](int sl, int& ua, int& nu) {
+        ua = dsplit ? s_uf[sl] : 0;
+        nu = dsplit ? s_uf[sl + 1] - ua : U;
+        const int cap = (int)(s_cb[sl + 1] - s_cb[sl]);
+        nu = nu < cap ? nu : cap;
+    };
+    int64_t rb = 0, bb = 0, sbb = 0;
+    int ua0 = 0, nu0 = 0;
+    float4 wpf[WPF];
+    float bpf[WPF];
+    if constexpr (APPLY) {
+        rb = a.meta[t];
+        bb = a.meta[2 * a.T + t];
+        sbb = a.meta[3 * a.T + t];
+        slot_entries(s, ua0, nu0);
+        if (tid == 0) s_oq_n = 0;
+#pragma unroll
+        for (int j = 0; j < WPF; ++j) {
+            const int q = tid + TPB * j;
+            wpf[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            bpf[j] = 0.0f;
+            if (q < (nu0 << lpr_sh)) {
+                const int64_t x = r0 + krow(keys[hpos[ua0 + (q >> lpr_sh)]]);
+                wpf[j] = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
+                bpf[j] = la.blkmax[bb + (x >> 8)];
+            }
+        }
+    }
     float amax = 0.0f;
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
         const int64_t row = r0 + krow(keys[hpos[u]]);
@@ -802,7 +859,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             e = s_cb[sl] + (u - s_uf[sl]);
         }
         if (e < s_cb[sl + 1]) {
-            a.ws_vals[e * a.D + q0 * 4 + d] = acc;
+            if constexpr (APPLY) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
+            else a.ws_vals[e * a.D + q0 * 4 + d] = acc;
             if (q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
         }
         amax = fmaxf(amax, fabsf(acc));
@@ -825,7 +883,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         };
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
-            reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D)[q0 + (q & (LG - 1))] = v;
+            float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
+            if constexpr (APPLY) st4_wt(dst, v);
+            else *dst = v;
             if (q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
             amax = fmaxf(amax, abs_max4(v));
         };
@@ -900,11 +960,33 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // the workgroup's max|grad| (dimension-split: its slice's) and the slot counts
     for (int o = WAVE / 2; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, WAVE));
     if (tid % WAVE == 0) s_red[w] = amax;
+    if constexpr (APPLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's value stores have landed
     __syncthreads();
     if (tid == 0) {
         float m = 0.0f;
         for (int q = 0; q < NW; ++q) m = fmaxf(m, s_red[q]);
-        a.ws_absmax[k] = m;
+        if constexpr (APPLY) {
+            // publish this slot's max|grad| (write-through), then one arrival for all the
+            // workgroup's stores; wait for the table's NA arrivals of this launch (the counter
+            // only grows, by NA per launch: this launch's base is old rounded down to NA)
+            st_wt(a.ws_absmax + k, m);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            uint32_t* rdv = la.sync + (int64_t)t * DQRM_SYNC_STRIDE + RDV_WORD;
+            const uint32_t old = atomicAdd(rdv, 1u);
+            const uint32_t base = old - old % (uint32_t)NA;
+            for (int spin = 0; ld_wt(rdv) - base < (uint32_t)NA; ++spin) {
+                if (spin > (1 << 20)) {  // the table's workgroups were not all resident: flagged, no hang
+                    flag_error(a.err, DQRM_ERRF_STALL);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            float am = 0.0f;
+            for (int j = 0; j < NA; ++j) am = fmaxf(am, ld_wt(a.ws_absmax + t * SPLIT + j));
+            s_am = am;
+        } else {
+            a.ws_absmax[k] = m;
+        }
     }
     if (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT)) {
         const int sl = dsplit ? tid : s;
@@ -917,22 +999,145 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         a.ws_ucount[t * SPLIT + sl] = c;
     }
     CDIAG_W(7);
+    if constexpr (APPLY) {
+        __syncthreads();
+        CDIAG(11);
+        // the update of dqrm_apply_local: s = clamp(max|g|, 1e-8) / (2^(bits-1)-1) (* 1/N,
+        // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
+        const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
+        if (s == 0 && tid == 0) la.s_avg[t] = sv;
+        const float rr = 1.0f / sv;
+        const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
+        const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
+        const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
+        bool dirty = false;
+        // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk = its
+        // block's max before this step
+        auto update = [&](int ua, int q, float4 w0, float oblk, float4 v) {
+            const int u = ua + (q >> lpr_sh), sub = q & (LPR - 1);
+            const int64_t x = r0 + krow(keys[hpos[u]]), grow = rb + x;
+            float4 acc;  // + 0.0f: the payload's integer round trip turns -0 into +0
+            acc.x = fake_quant(v.x, rr, qlo, qhi) + 0.0f; acc.y = fake_quant(v.y, rr, qlo, qhi) + 0.0f;
+            acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
+            float4 wn;
+            wn.x = upd(w0.x, acc.x); wn.y = upd(w0.y, acc.y); wn.z = upd(w0.z, acc.z); wn.w = upd(w0.w, acc.w);
+            reinterpret_cast<float4*>(la.W + grow * a.D)[sub] = wn;
+            if (la.repack) pack4_row(wn, la.packed + grow * (a.D / 2), sub, r_pack);
+            float old_rm = abs_max4(w0), rm = abs_max4(wn);
+            for (int o = 1; o < LPR; o <<= 1) {
+                old_rm = fmaxf(old_rm, __shfl_xor(old_rm, o, WAVE));
+                rm = fmaxf(rm, __shfl_xor(rm, o, WAVE));
+            }
+            if (sub != 0) return;
+            st_wt(la.rowmax + grow, rm);
+            const int64_t blk = x >> 8, sb = sbb + (blk >> 8);
+            if (rm > oblk) {  // growth: order-free atomicMax on the non-negative float bits
+                atomicMax(reinterpret_cast<unsigned int*>(la.blkmax) + bb + blk, __float_as_uint(rm));
+                if (rm > la.sblkmax[sb]) {
+                    atomicMax(reinterpret_cast<unsigned int*>(la.sblkmax) + sb, __float_as_uint(rm));
+                    if (rm > la.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(la.tmax) + t, __float_as_uint(rm));
+                }
+            }
+            if (old_rm == oblk && rm < old_rm) {  // the block's max holder shrank: this slot owns the block
+                const int p = atomicAdd(&s_oq_n, 1);
+                if (p < OWN_Q) {
+                    s_oq_blk[p] = (uint32_t)blk;
+                    s_oq_old[p] = oblk;
+                } else {  // queue full: the finalize re-reduces it
+                    flag_set(la.bdirty, bb + blk);
+                    flag_set(la.sdirty, sb);
+                    dirty = true;
+                }
+            }
+        };
+        for (int sl = s, j0 = 0; sl < SPLIT; sl += NA, j0 = 1) {  // uniform
+            int ua, nu;
+            slot_entries(sl, ua, nu);
+            const int nit = nu << lpr_sh;
+            const float* vb = a.ws_vals + s_cb[sl] * a.D;  // the slot's entries, D floats each
+            int q = tid;
+            if (j0 == 0) {  // the prefetched rows: all value loads in flight, then the updates
+                float4 v[WPF];
+#pragma unroll
+                for (int j = 0; j < WPF; ++j)
+                    v[j] = q + TPB * j < nit ? ld4_sc1(vb, (uint32_t)(q + TPB * j) * 16u) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int j = 0; j < WPF; ++j)
+                    if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], v[j]);
+                q += TPB * WPF;
+            }
+            for (; q < nit; q += TPB) {
+                const int64_t x = r0 + krow(keys[hpos[ua + (q >> lpr_sh)]]);
+                const float4 w0 = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
+                const float ob = la.blkmax[bb + (x >> 8)];
+                update(ua, q, w0, ob, ld4_sc1(vb, (uint32_t)q * 16u));
+            }
+        }
+        // owned blocks whose max holder shrank: re-reduce their 256 row maxima (written
+        // through by this workgroup, read with sc1 loads)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int nq = s_oq_n < OWN_Q ? s_oq_n : OWN_Q;
+        for (int qi = w; qi < nq; qi += NW) {  // one wave per block
+            const int64_t blk = s_oq_blk[qi];
+            float mv = 0.0f;
+#pragma unroll
+            for (int i = 0; i < BLK / WAVE; ++i) {
+                const int64_t r = blk * BLK + tid % WAVE + i * WAVE;
+                if (r < nrows) mv = fmaxf(mv, ld_wt(la.rowmax + rb + r));
+            }
+            mv = wave_max(mv);
+            if (tid % WAVE == 0) {
+                st_wt(la.blkmax + bb + blk, mv);
+                const int64_t sb = sbb + (blk >> 8);
+                if (mv < s_oq_old[qi] && s_oq_old[qi] == ld_wt(la.sblkmax + sb)) {  // it held the superblock max
+                    flag_set(la.sdirty, sb);
+                    dirty = true;
+                }
+            }
+        }
+        if (dirty) atomicAdd(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + DIRTY_WORD, 1u);
+        CDIAG(12);
+        // the table's last workgroup re-reduces flagged superblocks and the table max
+        if (arrive_last(la.sync + (int64_t)t * DQRM_SYNC_STRIDE, (uint32_t)NA)) {
+            __shared__ int s_dirty;
+            if (tid == 0) {
+                uint32_t* dw = la.sync + (int64_t)t * DQRM_SYNC_STRIDE + DIRTY_WORD;
+                s_dirty = ld_wt(dw) != 0u;
+                if (s_dirty) __hip_atomic_store(dw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (s_dirty)
+                finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
+                                     la.bdirty, la.tmax, a.D, true, false);
+        }
+        CDIAG_W(13);
+    }
 }
 
 }  // namespace
 
 namespace dqrm_internal {
 
-hipError_t launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream) {
+hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream) {
     // the attribute is per function, process-wide: set once (thread-safe), re-checked each call
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
-        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1),
+        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1<false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        if (attr == hipSuccess)
+            attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     });
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_coalesce_p1, dim3((a.T + 7) / 8 * 64), dim3(TPB), LDS_BYTES, stream, a);
+    const dim3 grid((a.T + 7) / 8 * 64);
+    if (la) {
+        if (a.T > kCoalesceApplyMaxT) return hipErrorInvalidValue;  // not all resident at once
+        hipLaunchKernelGGL(k_coalesce_p1<true>, grid, dim3(TPB), LDS_BYTES, stream, a, *la);
+    } else {
+        hipLaunchKernelGGL(k_coalesce_p1<false>, grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
+    }
     return hipGetLastError();
 }
 

@@ -28,10 +28,35 @@ struct CoalesceArgs {
     float* ws_absmax;
 };
 
+// The single-rank update fused behind the coalesce (dqrm_emb_bwd_apply_local): quantize the
+// coalesced rows with the table's scale, SGD into W and keep the |W| hierarchy exact
+// (dqrm_apply_local's arithmetic), inside the same launch.
+struct LocalApplyArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    uint8_t* sdirty;
+    uint8_t* bdirty;
+    float* tmax;
+    const float* pscale;
+    uint32_t* sync;             // [T * DQRM_SYNC_STRIDE]: arrival counters of the table's workgroups
+    float* s_avg;               // [T] the table scale the update used
+    int bits;
+    float nlr;                  // -lr
+    int repack;
+};
+
 // largest B the Criteo-form coalesce kernel takes (larger batches use the general kernel)
 constexpr int64_t kCoalesceMaxB = 4096;
+// largest table count the fused coalesce + update runs with: its (T+7)/8*64 workgroups of
+// 1024 threads (one per CU: 156 KiB LDS) must all be resident at once, since a table's
+// workgroups wait for each other's gradient maxima
+constexpr int kCoalesceApplyMaxT = 32;
 
-// launches k_coalesce_p1 (dqrm_coalesce.hip); returns the HIP error of the launch
-hipError_t launch_coalesce_pool1(const CoalesceArgs& a, hipStream_t stream);
+// launches k_coalesce_p1 (dqrm_coalesce.hip); la != nullptr: the fused update as well.
+// Returns the HIP error of the launch.
+hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream);
 
 }  // namespace dqrm_internal

@@ -27,8 +27,7 @@
 
 #include "../../include/dqrm.h"
 #include "dqrm_internal.h"
-
-#define DQRM_INLINE __device__ __forceinline__
+#include "dqrm_device.h"
 
 namespace {
 
@@ -77,154 +76,9 @@ int set_error(int code, const char* fmt, ...) {
 
 #define LAUNCH_CHECK() HIP_TRY(hipGetLastError())
 
-constexpr int WAVE = 64;
-constexpr int BLK = DQRM_BLOCK_ROWS;     // 256
-constexpr int SBLK_BLOCKS = 256;         // blocks per superblock
 constexpr int MAX_TABLES = 256;
 constexpr int DQRM_MAX_RANKS = 64;    // dqrm_apply_sparse_update: num_ranks <= 64
 
-// ------------------------------------------------------------------------------------
-// device helpers
-// ------------------------------------------------------------------------------------
-struct Meta {
-    const int64_t* row_base;
-    const int64_t* num_rows;
-    const int64_t* blk_base;
-    const int64_t* sblk_base;
-};
-
-DQRM_INLINE Meta make_meta(const int64_t* m, int T) {
-    return Meta{m, m + T, m + 2 * T, m + 3 * T};
-}
-
-DQRM_INLINE int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
-
-// largest t with base[t] <= x (base ascending, base[0] == 0)
-DQRM_INLINE int find_table(const int64_t* base, int T, int64_t x) {
-    int lo = 0, hi = T - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (base[mid] <= x) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-// symmetric scale: clamp(absmax, min=1e-8) / (2^(bits-1)-1)      quant_utils.py:189-192
-DQRM_INLINE float sym_scale(float absmax, int bits) {
-    const float n = (float)((1 << (bits - 1)) - 1);
-    float a = absmax < 1e-8f ? 1e-8f : absmax;
-    return a / n;
-}
-
-// linear_quantize + clamp: clamp(round(1/s * x + 0), -n-1, n)  quant_utils.py:101,343
-// r = 1/s is precomputed by the caller with an IEEE division (torch: reciprocal(s)*1.0).
-DQRM_INLINE float fake_quant(float x, float r, float lo, float hi) {
-    float t = r * x;
-    t = t + 0.0f;          // `+ zero_point` (zero_point = 0): turns -0 products into +0
-    t = rintf(t);          // torch.round: half to even
-    t = fmaxf(t, lo);      // torch.clamp(min) then (max)
-    t = fminf(t, hi);
-    return t;
-}
-
-DQRM_INLINE float abs_max4(float4 v) {
-    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
-}
-
-// max over a group of `G` consecutive lanes (G power of two <= 64)
-template <int G>
-DQRM_INLINE float group_max(float v) {
-#pragma unroll
-    for (int m = 1; m < G; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, WAVE));
-    return v;
-}
-
-DQRM_INLINE float wave_max(float v) { return group_max<WAVE>(v); }
-
-// pack 4 quantized values (ints in [-8,7] held as float) into 2 offset-binary bytes
-DQRM_INLINE uint16_t pack4_int4(float q0, float q1, float q2, float q3) {
-    uint32_t n0 = (uint32_t)((int)q0 + 8), n1 = (uint32_t)((int)q1 + 8);
-    uint32_t n2 = (uint32_t)((int)q2 + 8), n3 = (uint32_t)((int)q3 + 8);
-    return (uint16_t)(n0 | (n1 << 4) | (n2 << 8) | (n3 << 12));
-}
-
-DQRM_INLINE void flag_error(uint32_t* err, uint32_t f) { atomicOr(err, f); }
-
-// ------------------------------------------------------------------------------------
-// In-launch hand-off of the |W| hierarchy to a table's last workgroup (no finalize launch).
-// MI355X_MICROARCH.md "inter-workgroup visibility", hand-off row 1: every byte the last
-// workgroup reads was stored write-through (sc1 stores, or device-scope atomics), every
-// storing wave waits vmcnt(0), a workgroup barrier, then ONE lane adds to the table's
-// arrival counter; the workgroup whose add returns expected-1 reads with sc1 loads only.
-// No L2 write-back (release fence) and no L1 invalidate (acquire) on either side.
-// ------------------------------------------------------------------------------------
-DQRM_INLINE void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DQRM_INLINE float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DQRM_INLINE uint32_t ld_wt(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16-B write-through store (global_store_dwordx4 ... sc1)
-DQRM_INLINE void st4_wt(float4* p, float4 v) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
-}
-// W stores of a narrow table (<= 256 rows: finalize rebuilds its maxima from W) go write-through
-DQRM_INLINE void st4_w(float4* p, float4 v, bool wt) {
-    if (wt) st4_wt(p, v); else *p = v;
-}
-DQRM_INLINE void st_w(float* p, float v, bool wt) {
-    if (wt) st_wt(p, v); else *p = v;
-}
-
-// dirty flags (u8 arrays sdirty / bdirty) are set / cleared by device-scope atomics on their
-// aligned 32-bit word and read with sc1 word loads (the arrays are padded to whole words)
-DQRM_INLINE uint32_t* flag_word(const uint8_t* f, int64_t i, int* sh) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(f + i);
-    *sh = (int)(a & 3u) * 8;
-    return reinterpret_cast<uint32_t*>(a & ~(uintptr_t)3u);
-}
-DQRM_INLINE void flag_set(uint8_t* f, int64_t i) {
-    int sh;
-    uint32_t* w = flag_word(f, i, &sh);
-    atomicOr(w, 1u << sh);
-}
-DQRM_INLINE void flag_clear(uint8_t* f, int64_t i) {
-    int sh;
-    uint32_t* w = flag_word(f, i, &sh);
-    atomicAnd(w, ~(0xFFu << sh));
-}
-DQRM_INLINE bool flag_get(const uint8_t* f, int64_t i) {
-    int sh;
-    const uint32_t* w = flag_word(f, i, &sh);
-    return ((ld_wt(w) >> sh) & 0xFFu) != 0u;
-}
-
-// loads of the finalize: sc1 inside the updating launch (WT), plain in a launch of its own
-template <bool WT> DQRM_INLINE float ld_h(const float* p) { if constexpr (WT) return ld_wt(p); else return *p; }
-template <bool WT> DQRM_INLINE uint32_t ld_h(const uint32_t* p) { if constexpr (WT) return ld_wt(p); else return *p; }
-template <bool WT> DQRM_INLINE bool flag_get_h(const uint8_t* f, int64_t i) {
-    int sh;
-    const uint32_t* w = flag_word(f, i, &sh);
-    return ((ld_h<WT>(w) >> sh) & 0xFFu) != 0u;
-}
-
-// All threads of the workgroup call this after their last store for table t; returns
-// (uniformly) whether this is the last of the `expected` arriving workgroups. The last one
-// re-arms the counter for the next launch.
-DQRM_INLINE bool arrive_last(uint32_t* cnt, uint32_t expected) {
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores and atomics have landed
-    __syncthreads();                                   // ... and every other wave's
-    if (threadIdx.x == 0) {
-        const uint32_t old = atomicAdd(cnt, 1u);
-        const bool last = old + 1u == expected;
-        if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = last ? 1 : 0;
-    }
-    __syncthreads();
-    return s_last != 0;
-}
 
 // ------------------------------------------------------------------------------------
 // K0: synthetic init, U(-sqrt(1/n), sqrt(1/n)) per table (q_m_n_q_g.py:273-275 distribution)
@@ -336,12 +190,6 @@ __global__ void k_refresh_scale(const float* __restrict__ tmax, float* __restric
     tflags[t] = need;
 }
 
-// INT4-pack the 4 dims of float4 number idx4 of a row (prow = the row's packed bytes)
-DQRM_INLINE void pack4_row(const float4 w, uint8_t* __restrict__ prow, int idx4, float r) {
-    float q0 = fake_quant(w.x, r, -8.0f, 7.0f), q1 = fake_quant(w.y, r, -8.0f, 7.0f);
-    float q2 = fake_quant(w.z, r, -8.0f, 7.0f), q3 = fake_quant(w.w, r, -8.0f, 7.0f);
-    reinterpret_cast<uint16_t*>(prow)[idx4] = pack4_int4(q0, q1, q2, q3);
-}
 
 template <int LPR>
 DQRM_INLINE void pack_row_int4(const float4 w, uint8_t* __restrict__ packed, int64_t grow,
@@ -1259,182 +1107,6 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
     }
 }
 
-// Per table, after its slot workgroups: re-reduce flagged superblocks, then tmax over all
-// superblocks. Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their
-// rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats).
-template <bool WT>
-DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
-                               float* __restrict__ blkmax, float* __restrict__ sblkmax,
-                               uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
-                               int D, bool tracked) {
-    // Every load below is an sc1 (write-through) load: this runs either as its own launch or
-    // in the table's last workgroup of the updating kernel (arrive_last), whose producers
-    // stored the hierarchy write-through.
-    __shared__ float red[16];
-    __shared__ int s_rescan;
-    if (m.num_rows[t] <= BLK) {
-        const int64_t grow = m.row_base[t] + threadIdx.x;
-        float v = 0.0f;
-        if (threadIdx.x < m.num_rows[t]) {
-            const float* wr = W + grow * D;
-            if constexpr (WT) {
-                for (int k0 = 0; k0 < D; k0 += 16) {  // 16 loads in flight
-                    float x[16];
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) x[j] = k0 + j < D ? ld_h<WT>(wr + k0 + j) : 0.0f;
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) v = fmaxf(v, fabsf(x[j]));
-                }
-            } else {
-                for (int k = 0; k < D / 4; ++k) v = fmaxf(v, abs_max4(reinterpret_cast<const float4*>(wr)[k]));
-            }
-            rowmax[grow] = v;
-        }
-        v = wave_max(v);
-        if (threadIdx.x % WAVE == 0) red[threadIdx.x / WAVE] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            float r = 0.0f;
-            for (int k = 0; k < (int)(blockDim.x / WAVE); ++k) r = fmaxf(r, red[k]);
-            blkmax[m.blk_base[t]] = r;
-            sblkmax[m.sblk_base[t]] = r;
-            if (flag_get_h<WT>(sdirty, m.sblk_base[t])) flag_clear(sdirty, m.sblk_base[t]);
-            if (flag_get_h<WT>(bdirty, m.blk_base[t])) flag_clear(bdirty, m.blk_base[t]);
-            tmax[t] = r;
-        }
-        return;
-    }
-    const int64_t nblk = ceil_div(m.num_rows[t], BLK);
-    const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
-    const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
-    const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    constexpr int U4 = 4;  // loads in flight per thread
-    // tracked (flat apply kernels): tmax already holds every grown row max (atomicMax), so
-    // the table-wide rescan is needed only if a rescanned superblock held the table max
-    const float tmax0 = tracked ? ld_h<WT>(tmax + t) : 0.0f;
-    if (threadIdx.x == 0) s_rescan = tracked ? 0 : 1;
-    __syncthreads();
-    // the table's superblock flags, 4 per 32-bit word (word 0 holds superblock 0 at byte sh0)
-    int sh0;
-    const uint32_t* sdw = flag_word(sdirty, sbb, &sh0);
-    sh0 /= 8;
-    const int64_t nwords = (ns + sh0 + 3) / 4;
-    // one superblock whose max holder shrank, by one wave: re-reduce its flagged blocks' 256
-    // rowmax (the owning lane keeps the new block max in a register), then the superblock
-    auto fix_superblock = [&](int64_t sb) {
-        const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-        float nv[SBLK_BLOCKS / WAVE];
-        bool dq[SBLK_BLOCKS / WAVE];
-        const float old_sb = ld_h<WT>(sblkmax + sbb + sb);  // with the flags and block maxima: one round trip
-#pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-            const int64_t b = b0 + lane + q * WAVE;
-            dq[q] = b < b1 && flag_get_h<WT>(bdirty, bb + b);
-            nv[q] = b < b1 ? ld_h<WT>(blkmax + bb + b) : 0.0f;
-        }
-#pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-            uint64_t dm = __ballot(dq[q]);
-            while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
-                constexpr int DB = 8;
-                int dl[DB];
-                float x[DB];
-#pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
-                    dm &= dm ? dm - 1 : 0;
-                }
-#pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    x[i] = 0.0f;
-                    if (dl[i] < 0) continue;
-                    const int64_t blk = b0 + q * WAVE + dl[i];
-#pragma unroll
-                    for (int k = 0; k < BLK / WAVE; ++k) {
-                        const int64_t rr = blk * BLK + lane + k * WAVE;
-                        if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], ld_h<WT>(rowmax + m.row_base[t] + rr));
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    if (dl[i] < 0) continue;
-                    const float y = wave_max(x[i]);
-                    if (lane == dl[i]) nv[q] = y;
-                }
-            }
-            if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; flag_clear(bdirty, b0 + lane + q * WAVE + bb); }
-        }
-        float v = 0.0f;
-#pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
-        v = wave_max(v);
-        if (lane == 0) {
-            sblkmax[sbb + sb] = v;
-            flag_clear(sdirty, sbb + sb);
-            if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
-        }
-    };
-    // 1. list the flagged superblocks in LDS (one scan of the flag words); 2. one wave per
-    // listed superblock. A list that overflows is finished by another scan (the fixed
-    // superblocks' flags are clear by then).
-    constexpr int FIN_LIST = 128;
-    __shared__ int s_dl[FIN_LIST];
-    __shared__ int s_dn;
-    for (;;) {
-        if (threadIdx.x == 0) s_dn = 0;
-        __syncthreads();
-        for (int64_t k0 = (int64_t)threadIdx.x; k0 < nwords; k0 += (int64_t)blockDim.x * U4) {
-            uint32_t fw[U4];
-#pragma unroll
-            for (int j = 0; j < U4; ++j) {
-                const int64_t k = k0 + (int64_t)j * blockDim.x;
-                uint32_t x = k < nwords ? ld_h<WT>(sdw + k) : 0u;
-                if (k == 0) x &= 0xFFFFFFFFu << (8 * sh0);            // bytes before superblock 0
-                const int64_t nb = ns + sh0 - k * 4;                   // valid bytes in this word
-                if (nb < 4) x &= nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u);
-                fw[j] = x;
-            }
-#pragma unroll
-            for (int j = 0; j < U4; ++j) {
-                uint32_t x = fw[j];
-                while (x) {  // rare: a superblock's max holder shrank
-                    const int by = (__ffs((int)x) - 1) / 8;
-                    x &= ~(0xFFu << (8 * by));
-                    const int p = atomicAdd(&s_dn, 1);
-                    if (p < FIN_LIST) s_dl[p] = (int)((k0 + (int64_t)j * blockDim.x) * 4 + by - sh0);
-                }
-            }
-        }
-        __syncthreads();
-        const int nd = s_dn;
-        for (int i = w; i < nd && i < FIN_LIST; i += nw) fix_superblock(s_dl[i]);
-        if (nd <= FIN_LIST) break;  // uniform
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cleared flags land before the next scan
-        __syncthreads();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new superblock maxima reach L2 first
-    __syncthreads();
-    if (!s_rescan) return;  // uniform: tmax is exact already
-    float v = 0.0f;
-    for (int64_t k0 = threadIdx.x; k0 < ns; k0 += (int64_t)blockDim.x * U4) {
-        float x[U4];
-#pragma unroll
-        for (int j = 0; j < U4; ++j) {
-            const int64_t k = k0 + (int64_t)j * blockDim.x;
-            x[j] = k < ns ? ld_h<WT>(sblkmax + sbb + k) : 0.0f;
-        }
-#pragma unroll
-        for (int j = 0; j < U4; ++j) v = fmaxf(v, x[j]);
-    }
-    v = wave_max(v);
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float r = 0.0f;
-        for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
-        tmax[t] = r;
-    }
-}
 
 // One workgroup per table after the slot kernels (a kernel boundary is the cheap way to
 // make the slots' writes visible here: an agent-scope fence inside the slot kernel, e.g. a
@@ -1772,18 +1444,6 @@ struct PayloadSource {
     DQRM_INLINE float4 load(uint32_t lo, int sub) const { return finish(fetch(lo, sub)); }
 };
 
-// dequantize + SGD of one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
-struct ApplyUpdate {
-    int mode;
-    float inv_n, sc, sim_f, nlr;
-    DQRM_INLINE float operator()(float w, float acc) const {
-        float v;
-        if (mode == DQRM_UPD_DP) v = (acc * inv_n) * sc;                  // s_q_g_p_c.py:885,618-622
-        else if (mode == DQRM_UPD_SIMULATED) v = acc * sim_f;            // sgd_quantized_gradients.py:366-371
-        else v = acc * inv_n;                                            // FP32 sparse all_reduce (:319-327)
-        return w + nlr * v;  // separately rounded product, then add
-    }
-};
 
 template <int LPR, int LPRS>
 DQRM_INLINE void apply_segments(const ApplyArgs& a, const SlotLds& sl, uint16_t* s_long, int* s_wsum, const Meta& m,
@@ -4202,7 +3862,7 @@ int dqrm_emb_bwd_coalesce(const dqrm_table_set* set, const dqrm_batch* batch, co
         ca.dy = dy; ca.dst_t = dy_stride_t; ca.dst_b = dy_stride_b; ca.scale = set->scale; ca.ste = ste;
         ca.err = set->err; ca.ws_cap_base = ws_cap_base; ca.ws_rows = ws_rows; ca.ws_vals = ws_vals;
         ca.ws_ucount = ws_ucount; ca.ws_absmax = ws_absmax;
-        const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, (hipStream_t)stream);
+        const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, nullptr, (hipStream_t)stream);
         if (e != hipSuccess)
             return set_error(DQRM_E_HIP, "dqrm_emb_bwd_coalesce: launch failed: %s (%d)", hipGetErrorString(e), (int)e);
         return DQRM_OK;
@@ -4418,6 +4078,54 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
     LAUNCH_CHECK();  // the table's last working workgroup finalizes its |W| hierarchy
     if (a.fin_launch) return launch_finalize(set, st, true);
     return DQRM_OK;
+}
+
+int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                             int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
+                             int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
+                             float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_apply_local"))) return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_apply_local");
+    if (!ws_cap_base || !ws_rows || !ws_vals || !ws_ucount || !ws_absmax || !s_avg || ws_cap_total < 0 ||
+        (((uintptr_t)ws_vals) & 15))
+        return set_error(DQRM_E_INVALID, "%s: null/unaligned workspace", "dqrm_emb_bwd_apply_local");
+    if (grad_bits < 2 || grad_bits > 16)
+        return set_error(DQRM_E_INVALID, "%s: grad_bits must be 2..16 (got %d)", "dqrm_emb_bwd_apply_local", grad_bits);
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)",
+                         "dqrm_emb_bwd_apply_local", repack_bits);
+    static const bool fused_off = [] {
+        const char* e = getenv("DQRM_LOCAL_FUSED");
+        return e && !strcmp(e, "0");
+    }();
+    if (!fused_off && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && (batch->flags & DQRM_BATCH_POOLING_ONE) &&
+        batch->num_bags <= dqrm_internal::kCoalesceMaxB && batch->max_lookups >= batch->num_bags &&
+        set->total_rows <= 0xffffffffll && set->num_tables <= dqrm_internal::kCoalesceApplyMaxT) {
+        if (batch->num_bags <= 0) return DQRM_OK;
+        dqrm_internal::CoalesceArgs ca{};
+        ca.meta = set->meta; ca.T = set->num_tables; ca.D = set->dim; ca.B = batch->num_bags; ca.idx = batch->idx;
+        ca.dy = dy; ca.dst_t = dy_stride_t; ca.dst_b = dy_stride_b; ca.scale = set->scale; ca.ste = ste;
+        ca.err = set->err; ca.ws_cap_base = ws_cap_base; ca.ws_rows = ws_rows; ca.ws_vals = ws_vals;
+        ca.ws_ucount = ws_ucount; ca.ws_absmax = ws_absmax;
+        dqrm_internal::LocalApplyArgs la{};
+        la.W = set->W; la.packed = set->packed; la.rowmax = set->rowmax; la.blkmax = set->blkmax;
+        la.sblkmax = set->sblkmax; la.sdirty = set->sdirty; la.bdirty = set->bdirty; la.tmax = set->tmax;
+        la.pscale = set->pscale; la.sync = set->sync; la.s_avg = s_avg; la.bits = grad_bits; la.nlr = -lr;
+        la.repack = repack_bits == 4;
+        const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, &la, (hipStream_t)stream);
+        if (e != hipSuccess)
+            return set_error(DQRM_E_HIP, "dqrm_emb_bwd_apply_local: launch failed: %s (%d)", hipGetErrorString(e), (int)e);
+        return DQRM_OK;
+    }
+    if ((rc = dqrm_emb_bwd_coalesce(set, batch, dy, dy_stride_t, dy_stride_b, ste, ws_cap_base, ws_rows, ws_vals,
+                                    ws_ucount, ws_absmax, workspace, workspace_bytes, stream)))
+        return rc;
+    return dqrm_apply_local(set, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, ws_absmax, grad_bits, s_avg,
+                            lr, repack_bits, stream);
 }
 
 int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {

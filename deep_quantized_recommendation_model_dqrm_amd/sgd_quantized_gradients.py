@@ -106,13 +106,16 @@ def _apply_fp32_buffer(m: _QuantEmbeddingBase, lr: float) -> None:
     (dqrm_emb_bwd_coalesce_scaled), and the FP32 payload path applies W + (-lr * buffer)."""
     items = m._sim_fp32
     ts = m._tset
-    (b0, _, ste, layout), N = items[0]
+    (_, _, ste, _), N = items[0]
     if any(it[1] != N for it in items) or any(it[0][2] != ste for it in items):
         raise ValueError("micro-steps of one accumulation differ in number_of_gpus or full precision")
     batch = LookupBatch.concat_bags([it[0][0] for it in items])
-    if layout != "tbd":
-        raise ValueError("the simulated buffer expects tbd-layout gradients")
-    dy = torch.cat([it[0][1].reshape(ts.T, it[0][0].num_bags, ts.D) for it in items], dim=1)
+
+    def tbd(it):  # a micro-step's upstream gradient as [T, B_i, D] (the modules hand tbd or btd)
+        b, g, _, lay = it[0]
+        return g.reshape(ts.T, b.num_bags, ts.D) if lay == "tbd" else g.reshape(b.num_bags, ts.T, ts.D).transpose(0, 1)
+
+    dy = torch.cat([tbd(it) for it in items], dim=1).contiguous()
     ws = CoalescedGrad.allocate(ts.num_rows, max(batch.max_lookups, 1), ts.D, ts.device)
     ts.backward_coalesce_scaled(batch, dy, ws, N, ste=ste)
     caps = default_caps(ts.num_rows, max(batch.max_lookups, 1))

@@ -487,6 +487,20 @@ class EmbeddingTableSet:
             "dqrm_emb_bwd_coalesce",
         )
 
+    def backward_apply_local(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad", grad_bits: int,
+                             s_avg: torch.Tensor, lr: float, repack: bool = False, ste: bool = True,
+                             layout: str = "tbd") -> None:
+        """World size 1: backward_coalesce + the local quantized update (dqrm_apply_local),
+        one launch for Criteo-form batches (dqrm_emb_bwd_apply_local); same results."""
+        st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_apply_local(
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.slot_cap_base),
+                ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), int(grad_bits),
+                _ptr(s_avg), float(lr), 4 if repack else 0, *self._ws_args(batch), _stream_handle()),
+            "dqrm_emb_bwd_apply_local",
+        )
+
 
 def slot_caps(num_rows: Sequence[int], max_lookups: int) -> list[int]:
     """Exclusive prefix of the coalesce-slot capacities (dqrm_coalesce_slot_caps): slot

@@ -45,9 +45,10 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 4  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 5  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
-                               4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags */
+                               4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
+                               5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch) */
 
 /* status codes */
 #define DQRM_OK            0
@@ -61,6 +62,8 @@ extern "C" {
 #define DQRM_ERRF_OFFSET   2u  /* offsets not non-decreasing / outside [0, L_t] */
 #define DQRM_ERRF_OVERFLOW 4u  /* a table had more lookups than dqrm_batch.max_lookups promised, or a
                                       caller-sized workspace / payload was too small */
+#define DQRM_ERRF_STALL    8u  /* the workgroups of a fused launch could not all be resident at once
+                                  (dqrm_emb_bwd_apply_local): its update is incomplete */
 
 #define DQRM_BLOCK_ROWS   256     /* rows per blkmax entry */
 #define DQRM_SBLOCK_ROWS  65536   /* rows per sblkmax entry */
@@ -332,6 +335,21 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
                      const int32_t* ws_rows, const float* ws_vals, const int32_t* ws_ucount,
                      const float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
                      void* stream);
+
+/* World size 1: dqrm_emb_bwd_coalesce followed by dqrm_apply_local, with the same results
+ * (W, the |W| hierarchy, s_avg, packed rows, and the coalesced workspace) -- for a
+ * Criteo-form batch (DQRM_BATCH_POOLING_ONE, num_bags <= 4096, num_tables <= 32) in ONE
+ * launch: each table's workgroups meet once to share their gradient maxima and then
+ * update their row ranges, the W rows having been read during the coalesce. Replaces
+ * quantize_emb_grad (s_q_g_p_c.py:850-869) + weight_update_parallel_comm (:601-628) at N=1,
+ * the order grad_update_parallel_comm -> weight_update_parallel_comm runs them in
+ * (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1895-1904). Other batches: the two calls.
+ * DQRM_ERRF_STALL flags a launch whose workgroups could not all be resident. */
+int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                             int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
+                             int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
+                             float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* Which kernel dqrm_apply_sparse_update launches (process-wide; returns the previous
  * choice, or DQRM_E_INVALID). FLAT: one lane group per payload entry over the whole chip,

@@ -815,3 +815,59 @@ def test_criteo_form_coalesce_bitexact(dq, general_coalesce, D, B, dist):
         am = ws.absmax.view(T, -1)[t].max().item()
         assert am == (np.abs(v_o).max() if v_o.size else 0.0)
         assert am == ws_g.absmax.view(T, -1)[t].max().item()
+
+
+@pytest.mark.parametrize("D,B,dist,bits,repack", [(64, 2048, "uniform", 8, False), (64, 2048, "zipf", 8, True),
+                                                  (16, 2048, "uniform", 8, False), (16, 4096, "zipf", 4, False),
+                                                  (4, 3000, "zipf", 8, False), (8, 700, "uniform", 16, False),
+                                                  (256, 700, "zipf", 8, False), (32, 1, "uniform", 8, False)])
+def test_fused_coalesce_apply_matches_two_launches(dq, D, B, dist, bits, repack):
+    """dqrm_emb_bwd_apply_local (coalesce + local update in one launch: the table's
+    workgroups meet once for the gradient maxima, then update their row ranges) against
+    dqrm_emb_bwd_coalesce + dqrm_apply_local on a copy of the same tables, bit for bit over
+    three steps with large updates (block-max holders shrink, other rows grow): W, packed
+    rows, s_avg, rowmax / block / superblock / table maxima and the coalesced workspace; the
+    kept hierarchy equals a rebuild; out-of-range indices raise the same flags."""
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
+
+    rows = COAL_ROWS
+    T = len(rows)
+    sets = [dq.EmbeddingTableSet(rows, D, device="cuda", packed=repack, init="uniform", seed=91) for _ in range(2)]
+    assert torch.equal(sets[0].W, sets[1].W)
+    s_avg = [torch.zeros(T, dtype=torch.float32, device="cuda") for _ in range(2)]
+    for it in range(3):
+        P = G.pooling_one(rows, B, 93 + it, dist=dist)
+        if B > 8 and it == 1:
+            P[0, 5] = 3          # out of range on the 3-row table
+            P[2, 7] = -1         # negative on the 971-row table
+        dy = torch.from_numpy(G.upstream_grad(T, B, D, 95 + it) * 30).cuda()
+        b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+        wss = []
+        for j, ts in enumerate(sets):
+            if repack:
+                ts.refresh_scale_and_pack(4)
+            ts.forward(b)
+            ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+            if j == 0:
+                ts.backward_apply_local(b, dy, ws, bits, s_avg[0], 0.5, repack=repack)
+            else:
+                ts.backward_coalesce(b, dy, ws)
+                HipExchangeKernels(ts).apply_local(ws, bits, s_avg[1], 0.5, repack)
+            wss.append(ws)
+        errs = [ts.read_errors() for ts in sets]
+        assert errs[0] == errs[1]
+        assert (errs[0] != 0) == (B > 8 and it == 1)
+        assert torch.equal(s_avg[0], s_avg[1])
+        assert torch.equal(wss[0].ucount, wss[1].ucount)
+        assert torch.equal(wss[0].absmax, wss[1].absmax)
+        for t in range(T):
+            r0, v0 = _table_slots(wss[0], t)
+            r1, v1 = _table_slots(wss[1], t)
+            np.testing.assert_array_equal(r0, r1)
+            np.testing.assert_array_equal(v0, v1)
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax") + (("packed",) if repack else ()):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
+    inc = [x.clone() for x in (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)]
+    sets[0].refresh_absmax()
+    for x, y in zip(inc, (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)):
+        assert torch.equal(x, y)
