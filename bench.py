@@ -624,6 +624,9 @@ def dropin_main(a, world, rank, dev):
         direct(a.warmup + i)
     torch.cuda.synchronize()
     direct_s = time.perf_counter() - tdt
+    del ts, ex
+    torch.cuda.empty_cache()
+    ref_us = torch_reference_gpu(a, rows, D, B, dev, batches, dys, dp) if world == 1 else None
     if rank == 0:
         us = elapsed / a.steps * 1e6
         dus = direct_s / a.steps * 1e6
@@ -643,12 +646,68 @@ def dropin_main(a, world, rank, dev):
             "launches_per_step": launches,
             "direct_api": {"us_per_step": round(dus, 2), "launches_per_step": direct_launches,
                            "dropin_over_direct": round(us / dus, 2)},
+            "torch_gpu_reference": ({"us_per_step": round(ref_us, 2), "dropin_speedup": round(ref_us / us, 2),
+                                     "what": "the reference's modules as PyTorch ops on this GPU, same shape "
+                                             "(nn.EmbeddingBag sparse + per-step full-table aminmax scale + "
+                                             "fake-quant STE, autograd, " +
+                                             ("quantize_emb_grad + weight update at one rank)" if dp else
+                                              "torch.optim.SGD)")} if ref_us else None),
             "device_errors": errs, "setup_s": round(setup_s, 1),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def torch_reference_gpu(a, rows, D, B, dev, batches, dys, dp, steps=30):
+    """The reference's own step as PyTorch ops on this GPU at the drop-in's shape (what a user
+    of the reference runs on MI355X without this package): per table nn.EmbeddingBag(mode="sum",
+    sparse=True), the full-table aminmax scale every forward (quant_utils.py:141-194), fake
+    quant + dequant with the STE backward (_FakeQuantSTE); autograd; then torch.optim.SGD's
+    sparse step (single GPU) or quantize_emb_grad at one rank + W.add_ (s_q_g_p_c.py:850-890,
+    601-628). Returns us per step (host work included, as the drop-in line)."""
+    T = len(rows)
+    embs = []
+    for n in rows:
+        w = torch.empty(n, D, device=dev).uniform_(-float(np.sqrt(1 / n)), float(np.sqrt(1 / n)))
+        embs.append(torch.nn.EmbeddingBag(n, D, mode="sum", sparse=True, _weight=w))
+    off = torch.arange(B, dtype=torch.int64, device=dev)
+    opt = None if dp else torch.optim.SGD([e.weight for e in embs], lr=a.lr)
+
+    def step(i):
+        P = batches[i % len(batches)].idx.view(T, B)
+        ys = []
+        for t, e in enumerate(embs):
+            with torch.no_grad():
+                mn, mx = torch.aminmax(e.weight)
+                s = torch.clamp(torch.maximum(mn.abs(), mx.abs()), min=1e-8) / 7.0
+            ys.append(_FakeQuantSTE.apply(e(P[t], off), s, 4))
+        torch.autograd.backward(ys, dys)
+        if opt is not None:
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            return
+        with torch.no_grad():
+            for e in embs:
+                gc = e.weight.grad.coalesce()
+                v = gc.values()
+                sg = torch.clamp(v.abs().max(), min=1e-8) / 127.0
+                q = torch.clamp(torch.round(1.0 / sg * v), -128, 127)
+                e.weight.add_(torch.sparse_coo_tensor(gc.indices(), q * sg, gc.shape), alpha=-a.lr)
+                e.weight.grad = None
+
+    for i in range(5):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(5 + i)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / steps * 1e6
+    del embs, opt
+    torch.cuda.empty_cache()
+    return us
 
 
 def gather_phase(a, ts, rows, T, D, dev):

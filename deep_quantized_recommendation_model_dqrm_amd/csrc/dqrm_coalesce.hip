@@ -386,8 +386,8 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
 #endif
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
 constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
-constexpr int RDV_WORD = 32;        // the table's gradient-max rendezvous counter in its sync words
-constexpr int DIRTY_WORD = 16;      // ... and its "a superblock was flagged" counter
+constexpr int GRAN_WORD = 32;       // the table's 8 gradient-max granules {max bits, epoch} in its sync words
+constexpr uint32_t DIRTY_ONE = 1u << 16;  // arrival counter (sync word 0): arrivals | dirty arrivals << 16
 
 // APPLY (dqrm_emb_bwd_apply_local, world size 1): after the coalesce, the table's workgroups
 // meet once (each publishes its max|grad|, then waits for the table's others: all of them are
@@ -410,8 +410,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ float s_red[NW];
     __shared__ float s_am;
     __shared__ int s_oq_n;
+    __shared__ int s_dirty;
+    __shared__ int s_fin;
     __shared__ uint32_t s_oq_blk[OWN_Q];
     __shared__ float s_oq_old[OWN_Q];
+    __shared__ float s_oq_sold[OWN_Q];
     uint64_t* keys = reinterpret_cast<uint64_t*>(lds);
     uint16_t* pos = reinterpret_cast<uint16_t*>(lds + OFF_POS);
     uint16_t* hpos = reinterpret_cast<uint16_t*>(lds + OFF_HPOS);
@@ -464,6 +467,12 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     const int SP = (STAGE_FLOATS / SW) & ~3;  // column pitch (16-B columns)
     const int CE = SP - 4;                    // stage entries per chunk
     const float* dyt = a.dy + (int64_t)t * a.dst_t;
+    // fused update: this launch's epoch = this slot's previous granule epoch + 1 (every slot
+    // of a table publishes once per launch, so the table's granules always agree)
+    uint64_t* gran = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + GRAN_WORD);
+    uint32_t epoch = 0;
+    if (APPLY && tid < WAVE)
+        epoch = (uint32_t)(__hip_atomic_load(gran + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) + 1u;
     auto fetch = [&](int b, int sub) -> float4 {
         return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
     };
@@ -830,24 +839,31 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     int64_t rb = 0, bb = 0, sbb = 0;
     int ua0 = 0, nu0 = 0;
     float4 wpf[WPF];
-    float bpf[WPF];
+    float bpf[WPF], sbpf[WPF];
+    float otm = 0.0f;
     if constexpr (APPLY) {
         rb = a.meta[t];
         bb = a.meta[2 * a.T + t];
         sbb = a.meta[3 * a.T + t];
         slot_entries(s, ua0, nu0);
-        if (tid == 0) s_oq_n = 0;
+        if (tid == 0) {
+            s_oq_n = 0;
+            s_dirty = 0;
+        }
 #pragma unroll
         for (int j = 0; j < WPF; ++j) {
             const int q = tid + TPB * j;
             wpf[j] = make_float4(0.f, 0.f, 0.f, 0.f);
             bpf[j] = 0.0f;
+            sbpf[j] = 0.0f;
             if (q < (nu0 << lpr_sh)) {
                 const int64_t x = r0 + krow(keys[hpos[ua0 + (q >> lpr_sh)]]);
                 wpf[j] = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
                 bpf[j] = la.blkmax[bb + (x >> 8)];
+                sbpf[j] = la.sblkmax[sbb + (x >> 16)];
             }
         }
+        otm = la.tmax[t];
     }
     float amax = 0.0f;
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
@@ -859,7 +875,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             e = s_cb[sl] + (u - s_uf[sl]);
         }
         if (e < s_cb[sl + 1]) {
-            if constexpr (APPLY) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
+            if (APPLY && dsplit) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
             else a.ws_vals[e * a.D + q0 * 4 + d] = acc;
             if (q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
         }
@@ -884,7 +900,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
             float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
-            if constexpr (APPLY) st4_wt(dst, v);
+            if (APPLY && dsplit) st4_wt(dst, v);
             else *dst = v;
             if (q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
             amax = fmaxf(amax, abs_max4(v));
@@ -960,33 +976,37 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // the workgroup's max|grad| (dimension-split: its slice's) and the slot counts
     for (int o = WAVE / 2; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, WAVE));
     if (tid % WAVE == 0) s_red[w] = amax;
-    if constexpr (APPLY) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's value stores have landed
+    // a dimension-split table's values are read by its other workgroups: every wave's value
+    // stores land before the granule below signals them (hand-off row 1, sc1 stores)
+    if (APPLY && dsplit) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         float m = 0.0f;
         for (int q = 0; q < NW; ++q) m = fmaxf(m, s_red[q]);
-        if constexpr (APPLY) {
-            // publish this slot's max|grad| (write-through), then one arrival for all the
-            // workgroup's stores; wait for the table's NA arrivals of this launch (the counter
-            // only grows, by NA per launch: this launch's base is old rounded down to NA)
-            st_wt(a.ws_absmax + k, m);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            uint32_t* rdv = la.sync + (int64_t)t * DQRM_SYNC_STRIDE + RDV_WORD;
-            const uint32_t old = atomicAdd(rdv, 1u);
-            const uint32_t base = old - old % (uint32_t)NA;
-            for (int spin = 0; ld_wt(rdv) - base < (uint32_t)NA; ++spin) {
-                if (spin > (1 << 20)) {  // the table's workgroups were not all resident: flagged, no hang
-                    flag_error(a.err, DQRM_ERRF_STALL);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+        a.ws_absmax[k] = m;
+        // publish this slot's max|grad| as ONE 8-B sc1 store of {max bits, epoch} (a data-
+        // tagged granule: no counter, no ordering needed for the value itself)
+        if constexpr (APPLY)
+            __hip_atomic_store(gran + s, ((uint64_t)epoch << 32) | __float_as_uint(m), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (APPLY && tid < WAVE) {  // wave 0: lane j polls slot j's granule until it shows this launch's epoch
+        uint64_t g = 0;
+        bool ok = tid >= NA;
+        for (int spin = 0;; ++spin) {
+            if (!ok) {
+                g = __hip_atomic_load(gran + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = (uint32_t)(g >> 32) == epoch;
             }
-            float am = 0.0f;
-            for (int j = 0; j < NA; ++j) am = fmaxf(am, ld_wt(a.ws_absmax + t * SPLIT + j));
-            s_am = am;
-        } else {
-            a.ws_absmax[k] = m;
+            if (__all(ok)) break;
+            if (spin > (1 << 20)) {  // the table's workgroups were not all resident: flagged, no hang
+                if (tid == 0) flag_error(a.err, DQRM_ERRF_STALL);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
         }
+        const float am = wave_max(tid < NA ? __uint_as_float((uint32_t)g) : 0.0f);
+        if (tid == 0) s_am = am;
     }
     if (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT)) {
         const int sl = dsplit ? tid : s;
@@ -1011,9 +1031,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
         const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
         bool dirty = false;
-        // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk = its
-        // block's max before this step
-        auto update = [&](int ua, int q, float4 w0, float oblk, float4 v) {
+        // a workgroup that updates ONE row-range slot keeps its rows' new maxima in LDS (the
+        // stage, free by now): a shrunk block is then re-reduced from the other rows' stored
+        // maxima (untouched this launch) and these, with no wait for its own stores
+        const bool one_slot = NA == SPLIT;
+        float* s_newrm = stage;                       // [nu0]
+        float* s_blkrm = stage + MAXB;                // [NW][BLK] per-wave block scratch
+        // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk / osb its
+        // block's / superblock's max before this step (a stale-low superblock or table max
+        // only costs a redundant atomicMax: within the launch they only grow)
+        auto update = [&](int ua, int q, float4 w0, float oblk, float osb, float4 v) {
             const int u = ua + (q >> lpr_sh), sub = q & (LPR - 1);
             const int64_t x = r0 + krow(keys[hpos[u]]), grow = rb + x;
             float4 acc;  // + 0.0f: the payload's integer round trip turns -0 into +0
@@ -1030,12 +1057,13 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             }
             if (sub != 0) return;
             st_wt(la.rowmax + grow, rm);
+            if (one_slot) s_newrm[u - ua] = rm;
             const int64_t blk = x >> 8, sb = sbb + (blk >> 8);
             if (rm > oblk) {  // growth: order-free atomicMax on the non-negative float bits
                 atomicMax(reinterpret_cast<unsigned int*>(la.blkmax) + bb + blk, __float_as_uint(rm));
-                if (rm > la.sblkmax[sb]) {
+                if (rm > osb) {
                     atomicMax(reinterpret_cast<unsigned int*>(la.sblkmax) + sb, __float_as_uint(rm));
-                    if (rm > la.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(la.tmax) + t, __float_as_uint(rm));
+                    if (rm > otm) atomicMax(reinterpret_cast<unsigned int*>(la.tmax) + t, __float_as_uint(rm));
                 }
             }
             if (old_rm == oblk && rm < old_rm) {  // the block's max holder shrank: this slot owns the block
@@ -1043,12 +1071,18 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 if (p < OWN_Q) {
                     s_oq_blk[p] = (uint32_t)blk;
                     s_oq_old[p] = oblk;
+                    s_oq_sold[p] = osb;
                 } else {  // queue full: the finalize re-reduces it
                     flag_set(la.bdirty, bb + blk);
                     flag_set(la.sdirty, sb);
                     dirty = true;
                 }
             }
+        };
+        // a row split reads back its own values (plain loads after the workgroup barrier); a
+        // dimension-split table's rows hold the slices of all its workgroups (sc1 loads)
+        auto load_val = [&](const float* vb, int q) -> float4 {
+            return dsplit ? ld4_sc1(vb, (uint32_t)q * 16u) : reinterpret_cast<const float4*>(vb)[q];
         };
         for (int sl = s, j0 = 0; sl < SPLIT; sl += NA, j0 = 1) {  // uniform
             int ua, nu;
@@ -1060,57 +1094,91 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 float4 v[WPF];
 #pragma unroll
                 for (int j = 0; j < WPF; ++j)
-                    v[j] = q + TPB * j < nit ? ld4_sc1(vb, (uint32_t)(q + TPB * j) * 16u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    v[j] = q + TPB * j < nit ? load_val(vb, q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
                 for (int j = 0; j < WPF; ++j)
-                    if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], v[j]);
+                    if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], sbpf[j], v[j]);
                 q += TPB * WPF;
             }
             for (; q < nit; q += TPB) {
                 const int64_t x = r0 + krow(keys[hpos[ua + (q >> lpr_sh)]]);
                 const float4 w0 = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
-                const float ob = la.blkmax[bb + (x >> 8)];
-                update(ua, q, w0, ob, ld4_sc1(vb, (uint32_t)q * 16u));
+                const float ob = la.blkmax[bb + (x >> 8)], osb = la.sblkmax[sbb + (x >> 16)];
+                update(ua, q, w0, ob, osb, load_val(vb, q));
             }
         }
-        // owned blocks whose max holder shrank: re-reduce their 256 row maxima (written
-        // through by this workgroup, read with sc1 loads)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // owned blocks whose max holder shrank: re-reduce their 256 row maxima
         __syncthreads();
         const int nq = s_oq_n < OWN_Q ? s_oq_n : OWN_Q;
+        if (nq > 0 && !one_slot) {  // uniform: the stored maxima (write-through), once they have landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        const int lane = tid % WAVE;
         for (int qi = w; qi < nq; qi += NW) {  // one wave per block
             const int64_t blk = s_oq_blk[qi];
             float mv = 0.0f;
+            if (one_slot) {
+                // the block's untouched rows keep their stored maxima; its touched rows (the
+                // slot's entries [e0, e1), ascending rows) take their new maxima from LDS
+                float* sc = s_blkrm + w * BLK;
 #pragma unroll
-            for (int i = 0; i < BLK / WAVE; ++i) {
-                const int64_t r = blk * BLK + tid % WAVE + i * WAVE;
-                if (r < nrows) mv = fmaxf(mv, ld_wt(la.rowmax + rb + r));
+                for (int i = 0; i < BLK / WAVE; ++i) {
+                    const int64_t r = blk * BLK + lane + i * WAVE;
+                    sc[lane + i * WAVE] = r < nrows ? la.rowmax[rb + r] : 0.0f;
+                }
+                auto first_at_least = [&](int64_t row) {  // first entry with a row >= `row`
+                    int lo = 0, hi = nu0;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (r0 + (int64_t)krow(keys[hpos[ua0 + mid]]) < row) lo = mid + 1; else hi = mid;
+                    }
+                    return lo;
+                };
+                const int e0 = first_at_least(blk * BLK), e1 = first_at_least((blk + 1) * BLK);
+                for (int e = e0 + lane; e < e1; e += WAVE)
+                    sc[(r0 + krow(keys[hpos[ua0 + e]])) & (BLK - 1)] = s_newrm[e];
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) mv = fmaxf(mv, sc[lane + i * WAVE]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) {
+                    const int64_t r = blk * BLK + lane + i * WAVE;
+                    if (r < nrows) mv = fmaxf(mv, ld_wt(la.rowmax + rb + r));
+                }
             }
             mv = wave_max(mv);
-            if (tid % WAVE == 0) {
+            if (lane == 0) {
                 st_wt(la.blkmax + bb + blk, mv);
-                const int64_t sb = sbb + (blk >> 8);
-                if (mv < s_oq_old[qi] && s_oq_old[qi] == ld_wt(la.sblkmax + sb)) {  // it held the superblock max
-                    flag_set(la.sdirty, sb);
+                // it held the superblock's max before this step: the finalize re-reduces the
+                // superblock (exact whatever grew meanwhile)
+                if (mv < s_oq_old[qi] && s_oq_old[qi] == s_oq_sold[qi]) {
+                    flag_set(la.sdirty, sbb + (blk >> 8));
                     dirty = true;
                 }
             }
         }
-        if (dirty) atomicAdd(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + DIRTY_WORD, 1u);
+        if (dirty) s_dirty = 1;
         CDIAG(12);
-        // the table's last workgroup re-reduces flagged superblocks and the table max
-        if (arrive_last(la.sync + (int64_t)t * DQRM_SYNC_STRIDE, (uint32_t)NA)) {
-            __shared__ int s_dirty;
-            if (tid == 0) {
-                uint32_t* dw = la.sync + (int64_t)t * DQRM_SYNC_STRIDE + DIRTY_WORD;
-                s_dirty = ld_wt(dw) != 0u;
-                if (s_dirty) __hip_atomic_store(dw, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-            if (s_dirty)
-                finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
-                                     la.bdirty, la.tmax, a.D, true, false);
+        // one arrival per workgroup after all its stores landed, carrying whether it flagged
+        // a superblock (hand-off row 1 of MI355X_MICROARCH.md: sc1 stores / atomics, vmcnt(0),
+        // barrier, one lane's agent-scope add; the last arriver reads with sc1 loads only).
+        // The last one re-reduces the flagged superblocks and the table max -- only if some
+        // workgroup flagged one -- and re-arms the counter.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t* cnt = la.sync + (int64_t)t * DQRM_SYNC_STRIDE;
+            const uint32_t add = 1u + (s_dirty ? DIRTY_ONE : 0u);
+            const uint32_t now = atomicAdd(cnt, add) + add;
+            const bool last = (now & (DIRTY_ONE - 1u)) == (uint32_t)NA;
+            if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_fin = last && (now >> 16) != 0u;
         }
+        __syncthreads();
+        if (s_fin)
+            finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
+                                 la.bdirty, la.tmax, a.D, true, false);
         CDIAG_W(13);
     }
 }

@@ -2962,6 +2962,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     __shared__ float s_red[NW];
     __shared__ int s_n[3];                                       // queue lengths, rescan flag
     const int t = blockIdx.x;
+    DIAG_T(0);
     const Meta m = make_meta(a.meta, a.T);
     const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
     const bool narrow = nrows <= BLK;
@@ -3016,6 +3017,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
         }
         if (i < L && sub == 0) s_row[i] = xk[k];
     }
+    DIAG_T(1);
 #pragma unroll
     for (int f = 0; f < DYF; ++f) {
         const int q = threadIdx.x + f * SG_TPB;
@@ -3042,6 +3044,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
         for (int j = s0; j < s1; ++j) s_bag[j] = b;
     }
     if (!p1) __syncthreads();
+    DIAG_T(2);
     // 3. duplicate scan: lane `sub` of a group compares positions [sub*ch, sub*ch + ch)
     const int ch = (L + LPR - 1) / LPR;  // <= 64
     const int j0 = sub * ch, j1 = j0 + ch < L ? j0 + ch : L;
@@ -3062,6 +3065,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
         own[k] = i < L && xk[k] >= 0 && !(__ballot(earlier != 0ull) & gmask);
     }
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    DIAG_T(3);
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
         if (!own[k]) continue;  // group-uniform
@@ -3109,6 +3113,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     // 4. the table's maxima (LDS work first; a store round trip only when a block needs its
     //    row maxima re-read)
     __syncthreads();
+    DIAG_T(4);
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE;
     if (narrow) {
         float v = threadIdx.x < nrows ? s_rm[threadIdx.x] : 0.0f;
@@ -3122,11 +3127,15 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             a.sblkmax[sbb] = r;
             a.tmax[t] = r;
         }
+        DIAG_W(5);
         return;
     }
     const int64_t nblk = ceil_div(nrows, BLK);
     const int nq = s_n[0];
-    if (nq == 0) return;  // uniform: no block max holder shrank (the common case)
+    if (nq == 0) {  // uniform: no block max holder shrank (the common case)
+        DIAG_W(5);
+        return;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the workgroup's row maxima have landed
     __syncthreads();
     for (int q = w; q < nq; q += NW) {  // a wave per shrunk block: its 256 row maxima
@@ -3164,6 +3173,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             if (s_sqo[q] == otm && v < otm) s_n[2] = 1;  // it held the table max
         }
     }
+    DIAG_T(6);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (s_n[2]) {  // uniform: rescan the table's superblock maxima
@@ -3179,6 +3189,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             a.tmax[t] = r;
         }
     }
+    DIAG_W(5);
 }
 
 // ------------------------------------------------------------------------------------
