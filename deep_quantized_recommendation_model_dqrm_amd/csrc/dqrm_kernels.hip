@@ -3051,10 +3051,14 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     uint64_t mk[NPG];
 #pragma unroll
     for (int k = 0; k < NPG; ++k) mk[k] = 0ull;
-    for (int j = j0; j < j1; ++j) {
-        const int32_t v = s_row[j];
+    for (int jb = j0; jb < j1; jb += 8) {  // 8 LDS reads in flight, then the compares
+        int32_t v[8];
 #pragma unroll
-        for (int k = 0; k < NPG; ++k) mk[k] |= (uint64_t)(v == xk[k] && v >= 0) << (j - j0);
+        for (int i = 0; i < 8; ++i) v[i] = jb + i < j1 ? s_row[jb + i] : -1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int k = 0; k < NPG; ++k) mk[k] |= (uint64_t)(v[i] == xk[k] && v[i] >= 0) << (jb + i - j0);
     }
     bool own[NPG];
 #pragma unroll

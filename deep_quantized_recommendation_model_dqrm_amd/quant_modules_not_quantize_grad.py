@@ -36,7 +36,10 @@ from .tables import EmbeddingTableSet, LookupBatch
 
 
 _DEFAULT_GRAD_MODE = "sparse"
-_ERROR_CHECK_EVERY = 1
+# every 8th training call polls the device error flags: a poll is a stream-ordered snapshot
+# (event + pinned copy, ~20 us of host time), and the reference's driver calls 26 per-table
+# modules per step
+_ERROR_CHECK_EVERY = 8
 
 
 _POOLING_ONE_HINT = False
@@ -46,9 +49,9 @@ def set_error_check_interval(steps: int) -> None:
     """Poll the tables' device error flags (out-of-range index, bad offsets) every `steps`
     training calls -- in the module's forward for grad_mode "sparse" / "fused_sgd", in
     weight_update_parallel_comm for "dp" -- and raise DQRMError when one is set (ATen raises
-    on such input). 0 = never. A poll never synchronises the host: it reads the last
-    completed asynchronous snapshot of the flag word (EmbeddingTableSet.poll_errors), so a
-    bad batch raises one or two calls after the call that consumed it."""
+    on such input). Default 8; 0 = never. A poll never synchronises the host: it reads the
+    last completed asynchronous snapshot of the flag word (EmbeddingTableSet.poll_errors), so
+    a bad batch raises within `steps` + 2 calls after the call that consumed it."""
     global _ERROR_CHECK_EVERY
     _ERROR_CHECK_EVERY = max(0, int(steps))
 

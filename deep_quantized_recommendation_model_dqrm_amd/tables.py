@@ -80,7 +80,8 @@ class LookupBatch:
         else:
             T = len(indices)
             lens = [int(x.numel()) for x in indices]
-            idx = torch.cat([x.reshape(-1) for x in indices]) if T else torch.empty(0, dtype=torch.int64)
+            idx = (indices[0].reshape(-1) if T == 1 else  # one table (a per-table module): no copy
+                   torch.cat([x.reshape(-1) for x in indices]) if T else torch.empty(0, dtype=torch.int64))
         if isinstance(offsets, torch.Tensor):
             if offsets.dim() != 2 or offsets.shape[0] != T:
                 raise ValueError("stacked offsets must be [T, B]")
@@ -91,7 +92,8 @@ class LookupBatch:
             B0 = int(offsets[0].numel()) if T else 0
             if any(int(o.numel()) != B0 for o in offsets):
                 raise ValueError("all tables must have the same number of bags")
-            off = torch.stack([o.reshape(-1) for o in offsets]) if T else torch.empty(0, 0, dtype=torch.int64)
+            off = (offsets[0].reshape(1, -1) if T == 1 else
+                   torch.stack([o.reshape(-1) for o in offsets]) if T else torch.empty(0, 0, dtype=torch.int64))
         dev = torch.device(device) if device is not None else idx.device
         self.num_tables = T
         self.num_bags = int(off.shape[1]) if T else 0

@@ -280,8 +280,17 @@ def test_hooks_and_modules_raise_on_device_errors(dq):
     poll an asynchronous snapshot of the flag word (no host sync), so the error surfaces
     once that snapshot has landed: within two calls here."""
     from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
     from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
 
+    Q.set_error_check_interval(1)  # poll on every call (default: every 8th)
+    try:
+        _raise_on_device_errors(dq, L, H)
+    finally:
+        Q.set_error_check_interval(8)
+
+
+def _raise_on_device_errors(dq, L, H):
     rows, D, B = [10, 300], 16, 64
     Ws = G.table_weights(rows, D, 71)
     model = ListDLRM(rows, D, Ws)

@@ -7,7 +7,7 @@ K="--config kaggle --batch-per-gpu 128 --steps 100 --warmup 10"
 one() {  # <name> <args...>
   n=$1; shift
   timeout -k 10 300 python bench.py $K "$@" > gpurun_out/${T}_dropin_$n.log 2>&1 || { tail -n 30 gpurun_out/${T}_dropin_$n.log; exit 1; }
-  tail -n 1 gpurun_out/${T}_dropin_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n', d['value'], d['us_per_step'], 'launches', d['launches_per_step'], 'direct', d['direct_api'])"
+  tail -n 1 gpurun_out/${T}_dropin_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n', d['value'], d['us_per_step'], 'launches', d['launches_per_step'], 'direct', d['direct_api'], 'torch', d.get('torch_gpu_reference'))"
 }
 one sgd_list_sparse --mode dropin-sgd --dropin-form list --grad-mode sparse
 one sgd_list_fused --mode dropin-sgd --dropin-form list --grad-mode fused_sgd

@@ -1,0 +1,71 @@
+"""Host-side profile (cProfile) of the drop-in call patterns at Kaggle B=128: where the
+per-step host time of the modules + hooks goes (the kernels take ~20 us of it).
+usage: python tools/prof_dropin.py [coll-dp|coll-sgd|list-sgd] [steps]"""
+import cProfile
+import os
+import pstats
+import sys
+import time
+
+import torch
+from torch import nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H  # noqa: E402
+from deep_quantized_recommendation_model_dqrm_amd.workloads import CONFIGS, synthetic_indices  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "coll-dp"
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+rows, D = CONFIGS["kaggle"]
+T, B, dev = len(rows), 128, torch.device("cuda")
+Q.set_pooling_one_inputs(True)
+dp = kind.endswith("dp")
+gm = "dp" if dp else ("sparse" if kind == "list-sgd" else "fused_sgd")
+if kind.startswith("list"):
+    emb = nn.ModuleList([Q.QuantEmbeddingBagTwo(n, D, 4, embedding_id=i, init="device", grad_mode=gm, lr=0.1,
+                                                device=dev) for i, n in enumerate(rows)])
+else:
+    emb = Q.QuantEmbeddingBagCollection(rows, D, 4, init="device", grad_mode=gm, lr=0.1, device=dev)
+model = nn.Module()
+model.emb_l, model.bot_l, model.top_l = emb, nn.ModuleList(), nn.ModuleList()
+opt = torch.optim.SGD(list(model.parameters()), lr=0.1) if gm == "sparse" else None
+P = [synthetic_indices(rows, B, 7 + k) for k in range(8)]
+lS_o = torch.arange(B, dtype=torch.int64, device=dev)
+dys = [torch.randn(B, D, device=dev) * 0.05 for _ in range(T)]
+
+
+def step(i):
+    Pi = P[i % 8]
+    if dp:
+        H.clear_gradients(model)
+    if kind.startswith("list"):
+        ly = [emb[t](Pi[t], lS_o) for t in range(T)]
+    else:
+        ly = emb(lS_o.expand(T, B), Pi)
+    torch.autograd.backward(ly, dys)
+    if dp:
+        H.grad_update_parallel_comm(model, 1, True, 8)
+        H.weight_update_parallel_comm(model, 0.1, num_gpus=1)
+    elif opt is not None:
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+
+for i in range(10):
+    step(i)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i in range(steps):
+    step(i)
+torch.cuda.synchronize()
+print(f"{kind}: {(time.perf_counter() - t0) / steps * 1e6:.1f} us/step")
+pr = cProfile.Profile()
+pr.enable()
+for i in range(steps):
+    step(i)
+torch.cuda.synchronize()
+pr.disable()
+st = pstats.Stats(pr)
+st.sort_stats("tottime").print_stats(25)
