@@ -27,14 +27,16 @@ lib = L.load()
 lib.dqrm_diag_coal_read.argtypes = [C.c_void_p, C.c_int]
 ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
 g = torch.Generator(device="cuda").manual_seed(5)
-P = torch.stack([torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows])
-b = dq.LookupBatch.pooling_one(P)
+NB = 8  # distinct resident batches cycled, as bench.py (cold rows and translations every launch)
+bs = [dq.LookupBatch.pooling_one(torch.stack([torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows]))
+      for _ in range(NB)]
 dy = torch.randn(T, B, D, device="cuda", generator=g) * 0.05
 ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
 s_avg = torch.zeros(T, device="cuda")
 
 
-def run():
+def run(i):
+    b = bs[i % NB]
     if APPLY:
         ts.forward(b)
         ts.backward_apply_local(b, dy, ws, 8, s_avg, 0.01)
@@ -42,39 +44,50 @@ def run():
         ts.backward_coalesce(b, dy, ws)
 
 
-ts.forward(b)
-for _ in range(20):
-    run()
+ts.forward(bs[0])
+for i in range(3 * NB):
+    run(i)
 torch.cuda.synchronize()
-buf = np.zeros(T * 8 * 16, dtype=np.uint64)
-run()
-lib.dqrm_diag_coal_read(buf.ctypes.data, buf.size)
-c = buf.reshape(T, 8, 16).astype(np.int64)
-k0 = c[:, :, 0].min()
-print(f"{cfg} B={B} D={D}: span {(c[:, :, 7].max() - k0) / 100:.1f} us")
-print("per table, slowest slot (us): start | idx | compact | sort | heads | land | segs | tail || end")
-order = np.argsort(-c[:, :, 7].max(axis=1))
+cs = []
+for i in range(NB):  # one launch per batch, read after each
+    buf = np.zeros(T * 8 * 16, dtype=np.uint64)
+    run(i)
+    lib.dqrm_diag_coal_read(buf.ctypes.data, buf.size)
+    c = buf.reshape(T, 8, 16).astype(np.int64)
+    k0 = c[:, :, 0][c[:, :, 0] > 0].min()
+    c = np.where(c >= k0, c - k0, -1)  # -1: not stamped in this launch
+end = 13 if APPLY else 7
+spans = [c[:, :, end].max() / 100 for c in cs]
+print(f"{cfg} B={B} D={D}: span median {np.median(spans):.1f} us over {NB} launches (min {min(spans):.1f}, "
+      f"max {max(spans):.1f}), each on a batch not used in the previous {NB - 1}")
+print("per table, slowest slot, median over launches (us): start | idx | compact | sort | heads | land | segs | tail || end")
+
+
+def slow(c, t, k):
+    return c[t, int(np.argmax(c[t, :, k]))]
+
+
+order = np.argsort(-np.median([c[:, :, 7].max(axis=1) for c in cs], axis=0))
 for t in order:
-    s = int(np.argmax(c[t, :, 7]))
-    p = c[t, s]
-    if p[2] == 0:
-        print(f"t{t:2d} n={rows[t]:>10d} slot{s}: inactive end {(p[7] - k0) / 100:.1f}")
+    ps = [slow(c, t, 7) for c in cs]
+    if ps[0][2] < 0:
+        print(f"t{t:2d} n={rows[t]:>10d}: inactive")
         continue
-    ph = [p[0] - k0] + [p[i + 1] - p[i] for i in range(7)]
-    print(f"t{t:2d} n={rows[t]:>10d} slot{s}: " + " ".join(f"{x / 100:5.1f}" for x in ph) + f" || {(p[7] - k0) / 100:5.1f}")
+    ph = np.median([[p[0]] + [p[i + 1] - p[i] for i in range(7)] for p in ps], axis=0)
+    print(f"t{t:2d} n={rows[t]:>10d}: " + " ".join(f"{x / 100:5.1f}" for x in ph)
+          + f" || {np.median([p[7] for p in ps]) / 100:5.1f}")
 sub = [(c[t, s, 8] - c[t, s, 1], c[t, s, 9] - c[t, s, 8], c[t, s, 10] - c[t, s, 9], c[t, s, 2] - c[t, s, 10])
-       for t in range(T) for s in range(8) if c[t, s, 2] > 0]
+       for c in cs for t in range(T) for s in range(8) if c[t, s, 2] >= 0 and c[t, s, 10] >= 0]
 sub = np.array(sub) / 100
 print("compact split (median us): idx-wait %.2f  compaction %.2f  report+barrier %.2f  prefetch-issue %.2f" %
       tuple(np.median(sub, axis=0)))
 if APPLY:
-    print("apply phases per table, slowest slot (us): segments done->met (incl. the wait) | met->updated | updated->end || end")
-    for t in order:
-        s = int(np.argmax(c[t, :, 13]))
-        p = c[t, s]
-        if p[11] == 0:
+    print("apply phases per table, slowest slot, median (us): segments done->met (incl. the wait) | "
+          "met->updated | updated->end || end")
+    for t in np.argsort(-np.median([c[:, :, 13].max(axis=1) for c in cs], axis=0)):
+        ps = [slow(c, t, 13) for c in cs]
+        if ps[0][11] < 0:
             continue
-        print(f"t{t:2d} n={rows[t]:>10d} slot{s}: {(p[11] - p[6]) / 100:5.1f} {(p[12] - p[11]) / 100:5.1f} "
-              f"{(p[13] - p[12]) / 100:5.1f} || {(p[13] - k0) / 100:5.1f}")
-    print(f"span incl. update {(c[:, :, 13].max() - k0) / 100:.1f} us")
+        ph = np.median([[p[11] - p[6], p[12] - p[11], p[13] - p[12], p[13]] for p in ps], axis=0) / 100
+        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} {ph[1]:5.1f} {ph[2]:5.1f} || {ph[3]:5.1f}")
 print("errors", ts.read_errors())
