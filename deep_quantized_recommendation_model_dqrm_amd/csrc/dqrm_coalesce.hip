@@ -385,6 +385,7 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
 #define DQRM_COAL_WPF 4
 #endif
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
+constexpr int WPFA = WPF > 0 ? WPF : 1;  // array extent (WPF = 0: no early W loads, an A/B build)
 constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
 constexpr int GRAN_WORD = 32;       // the table's 8 gradient-max granules {max bits, epoch} in its sync words
 constexpr uint32_t DIRTY_ONE = 1u << 16;  // arrival counter (sync word 0): arrivals | dirty arrivals << 16
@@ -429,6 +430,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if (t >= a.T) return;
     const int k = t * SPLIT + s;
     const int tid = threadIdx.x, w = tid / WAVE;
+    // dy float4 prefetched per thread: 4 in the fused kernel (its update needs the registers;
+    // a Criteo slot of <= 256 lookups x 16 float4 still lands in one round)
+    constexpr int PF = APPLY ? (PFR < 4 ? PFR : 4) : PFR;
     const int B = (int)a.B;
     CDIAG(0);
     // 1. the table's uniform values (scalar loads), then this thread's lookups
@@ -492,11 +496,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // sort. A row-split slot issues the same number of placeholder loads (one hot 16-B line,
     // overwritten after the compaction), so on both paths the compiler waits for the index
     // loads alone.
-    float4 pf[PFR];
+    float4 pf[PF];
     {
         const int lim = B > 0 ? (B << lg_sh) - 1 : 0;
 #pragma unroll
-        for (int f = 0; f < PFR; ++f) {
+        for (int f = 0; f < PF; ++f) {
             const int q = min(tid + TPB * f, lim);
             const float4* src = dsplit && B > 0
                                     ? reinterpret_cast<const float4*>(dyt + (int64_t)(q >> lg_sh) * a.dst_b) + q0 + (q & (LG - 1))
@@ -563,7 +567,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // between here and their use waits for global memory.
     if (!dsplit) {
 #pragma unroll
-        for (int f = 0; f < PFR; ++f) {
+        for (int f = 0; f < PF; ++f) {
             const int q = tid + TPB * f;
             if (q < (n << lg_sh)) pf[f] = fetch((int)kbag(keys[q >> lg_sh]), q & (LG - 1));
         }
@@ -836,10 +840,15 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const int cap = (int)(s_cb[sl + 1] - s_cb[sl]);
         nu = nu < cap ? nu : cap;
     };
+    // a row-split slot whose entries fit beside the stage's multi-lookup values keeps its
+    // coalesced values in the stage (entry u, dimension d at column d, index vb0 + u) instead
+    // of the workspace: no HBM round trip for them (the workspace values are then not written)
+    const int vb0 = n - NS;
+    const bool lds_vals = APPLY && !dsplit && vb0 + U <= CE && U <= (int)(s_cb[s + 1] - s_cb[s]);
     int64_t rb = 0, bb = 0, sbb = 0;
     int ua0 = 0, nu0 = 0;
-    float4 wpf[WPF];
-    float bpf[WPF], sbpf[WPF];
+    float4 wpf[WPFA];
+    float bpf[WPFA];
     float otm = 0.0f;
     if constexpr (APPLY) {
         rb = a.meta[t];
@@ -850,17 +859,17 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             s_oq_n = 0;
             s_dirty = 0;
         }
+        // the W rows and block maxima of the entries this workgroup will update, in flight
+        // across the segment phase and the wait for the table's other workgroups
 #pragma unroll
         for (int j = 0; j < WPF; ++j) {
             const int q = tid + TPB * j;
             wpf[j] = make_float4(0.f, 0.f, 0.f, 0.f);
             bpf[j] = 0.0f;
-            sbpf[j] = 0.0f;
             if (q < (nu0 << lpr_sh)) {
                 const int64_t x = r0 + krow(keys[hpos[ua0 + (q >> lpr_sh)]]);
                 wpf[j] = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
                 bpf[j] = la.blkmax[bb + (x >> 8)];
-                sbpf[j] = la.sblkmax[sbb + (x >> 16)];
             }
         }
         otm = la.tmax[t];
@@ -875,7 +884,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             e = s_cb[sl] + (u - s_uf[sl]);
         }
         if (e < s_cb[sl + 1]) {
-            if (APPLY && dsplit) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
+            if (lds_vals) stage[d * SP + vb0 + u] = acc;
+            else if (APPLY && dsplit) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
             else a.ws_vals[e * a.D + q0 * 4 + d] = acc;
             if (q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
         }
@@ -899,17 +909,21 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         };
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
-            float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
-            if (APPLY && dsplit) st4_wt(dst, v);
-            else *dst = v;
+            if (lds_vals) {
+                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - cb_s), v);
+            } else {
+                float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
+                if (APPLY && dsplit) st4_wt(dst, v);
+                else *dst = v;
+            }
             if (q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
             amax = fmaxf(amax, abs_max4(v));
         };
         int q = tid;
         {
-            int de[PFR];
+            int de[PF];
 #pragma unroll
-            for (int f = 0; f < PFR; ++f) {
+            for (int f = 0; f < PF; ++f) {
                 de[f] = -1;
                 if (q + TPB * f < nitems) {  // the STE division only where a value exists
                     pf[f] = finish(pf[f]);
@@ -917,8 +931,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 }
             }
 #pragma unroll
-            for (int f = 0; f < PFR; ++f) store(q + TPB * f, de[f], pf[f]);
-            q += TPB * PFR;
+            for (int f = 0; f < PF; ++f) store(q + TPB * f, de[f], pf[f]);
+            q += TPB * PF;
         }
         for (; q < nitems; q += TPB) {  // beyond the register budget (or no prefetch)
             const int p = pos[q >> lg_sh];
@@ -1035,12 +1049,15 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // stage, free by now): a shrunk block is then re-reduced from the other rows' stored
         // maxima (untouched this launch) and these, with no wait for its own stores
         const bool one_slot = NA == SPLIT;
-        float* s_newrm = stage;                       // [nu0]
-        float* s_blkrm = stage + MAXB;                // [NW][BLK] per-wave block scratch
-        // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk / osb its
-        // block's / superblock's max before this step (a stale-low superblock or table max
-        // only costs a redundant atomicMax: within the launch they only grow)
-        auto update = [&](int ua, int q, float4 w0, float oblk, float osb, float4 v) {
+        // (LDS dead by now: the gather map sdest and the multi-lookup list mlist)
+        float* s_newrm = reinterpret_cast<float*>(sdest);  // [nu0]
+        float* s_blkrm = reinterpret_cast<float*>(mlist);  // [RRW][BLK] per-wave block scratch
+        constexpr int RRW = 8;                             // waves re-reducing blocks at a time
+        static_assert(RRW * BLK * 4 <= (MAXB + 8) * 2, "block scratch in the mlist region");
+        // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk its
+        // block's max before this step (a stale-low superblock or table max only costs a
+        // redundant atomicMax: within the launch they only grow)
+        auto update = [&](int ua, int q, float4 w0, float oblk, float4 v) {
             const int u = ua + (q >> lpr_sh), sub = q & (LPR - 1);
             const int64_t x = r0 + krow(keys[hpos[u]]), grow = rb + x;
             float4 acc;  // + 0.0f: the payload's integer round trip turns -0 into +0
@@ -1059,6 +1076,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             st_wt(la.rowmax + grow, rm);
             if (one_slot) s_newrm[u - ua] = rm;
             const int64_t blk = x >> 8, sb = sbb + (blk >> 8);
+            const float osb = rm > oblk || old_rm == oblk ? la.sblkmax[sb] : 0.0f;  // the superblock's max
             if (rm > oblk) {  // growth: order-free atomicMax on the non-negative float bits
                 atomicMax(reinterpret_cast<unsigned int*>(la.blkmax) + bb + blk, __float_as_uint(rm));
                 if (rm > osb) {
@@ -1082,6 +1100,10 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // a row split reads back its own values (plain loads after the workgroup barrier); a
         // dimension-split table's rows hold the slices of all its workgroups (sc1 loads)
         auto load_val = [&](const float* vb, int q) -> float4 {
+            if (lds_vals) {  // entry q >> lpr_sh, float4 q & (LPR-1), from the stage columns
+                const float* c = stage + (q & (LPR - 1)) * 4 * SP + vb0 + (q >> lpr_sh);
+                return make_float4(c[0], c[SP], c[2 * SP], c[3 * SP]);
+            }
             return dsplit ? ld4_sc1(vb, (uint32_t)q * 16u) : reinterpret_cast<const float4*>(vb)[q];
         };
         for (int sl = s, j0 = 0; sl < SPLIT; sl += NA, j0 = 1) {  // uniform
@@ -1090,32 +1112,37 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const int nit = nu << lpr_sh;
             const float* vb = a.ws_vals + s_cb[sl] * a.D;  // the slot's entries, D floats each
             int q = tid;
-            if (j0 == 0) {  // the prefetched rows: all value loads in flight, then the updates
-                float4 v[WPF];
+            if (j0 == 0) {  // the prefetched rows: value loads two at a time in flight, then the updates
 #pragma unroll
-                for (int j = 0; j < WPF; ++j)
-                    v[j] = q + TPB * j < nit ? load_val(vb, q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int jh = 0; jh < WPF; jh += 2) {
+                    float4 v[2];
 #pragma unroll
-                for (int j = 0; j < WPF; ++j)
-                    if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], sbpf[j], v[j]);
+                    for (int j = jh; j < jh + 2 && j < WPF; ++j)
+                        v[j - jh] = q + TPB * j < nit ? load_val(vb, q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int j = jh; j < jh + 2 && j < WPF; ++j)
+                        if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], v[j - jh]);
+                }
                 q += TPB * WPF;
+                CDIAG(14);
             }
             for (; q < nit; q += TPB) {
                 const int64_t x = r0 + krow(keys[hpos[ua + (q >> lpr_sh)]]);
                 const float4 w0 = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
-                const float ob = la.blkmax[bb + (x >> 8)], osb = la.sblkmax[sbb + (x >> 16)];
-                update(ua, q, w0, ob, osb, load_val(vb, q));
+                const float ob = la.blkmax[bb + (x >> 8)];
+                update(ua, q, w0, ob, load_val(vb, q));
             }
         }
         // owned blocks whose max holder shrank: re-reduce their 256 row maxima
         __syncthreads();
+        CDIAG(15);
         const int nq = s_oq_n < OWN_Q ? s_oq_n : OWN_Q;
         if (nq > 0 && !one_slot) {  // uniform: the stored maxima (write-through), once they have landed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
         const int lane = tid % WAVE;
-        for (int qi = w; qi < nq; qi += NW) {  // one wave per block
+        for (int qi = w; qi < nq && (w < RRW || !one_slot); qi += one_slot ? RRW : NW) {  // one wave per block
             const int64_t blk = s_oq_blk[qi];
             float mv = 0.0f;
             if (one_slot) {

@@ -3051,10 +3051,12 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     uint64_t mk[NPG];
 #pragma unroll
     for (int k = 0; k < NPG; ++k) mk[k] = 0ull;
-    for (int jb = j0; jb < j1; jb += 8) {  // 8 LDS reads in flight, then the compares
+    for (int jb = j0; jb < j1; jb += 8) {  // 8 unconditional LDS reads in flight, then the compares
         int32_t v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = jb + i < j1 ? s_row[jb + i] : -1;
+        for (int i = 0; i < 8; ++i) v[i] = s_row[jb + i < j1 ? jb + i : j1 - 1];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = jb + i < j1 ? v[i] : -1;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -3078,26 +3080,6 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             const uint32_t lo32 = (uint32_t)__shfl((int)(uint32_t)mk[k], gbase + l, WAVE);
             const uint32_t hi32 = (uint32_t)__shfl((int)(uint32_t)(mk[k] >> 32), gbase + l, WAVE);
             uint64_t ml = ((uint64_t)hi32 << 32) | lo32;
-            if (p1) {
-                // Criteo form (position j = bag j): 8 positions at a time, all 8 dy reads in
-                // flight (unmatched ones unused), then the matched FMAs in position order --
-                // a hot row of a tiny table walks ~B/n positions
-                const int jb = l * ch;
-                for (int c8 = 0; c8 < ch && (ml >> c8); c8 += 8) {
-                    const uint32_t bits = (uint32_t)(ml >> c8) & 0xFFu;
-                    if (bits == 0u) continue;
-                    float4 g[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const int j = jb + c8 + i;
-                        g[i] = s_dy[(j < L ? j : L - 1) * LPR + sub];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        if ((bits >> i) & 1u) acc = seg_op4<OP_FMA>(acc, g[i], a.nlr);
-                }
-                ml = 0;
-            }
             while (ml) {
                 const int j = l * ch + __ffsll((long long)ml) - 1;
                 ml &= ml - 1;

@@ -826,8 +826,9 @@ def test_fused_coalesce_apply_matches_two_launches(dq, D, B, dist, bits, repack)
     workgroups meet once for the gradient maxima, then update their row ranges) against
     dqrm_emb_bwd_coalesce + dqrm_apply_local on a copy of the same tables, bit for bit over
     three steps with large updates (block-max holders shrink, other rows grow): W, packed
-    rows, s_avg, rowmax / block / superblock / table maxima and the coalesced workspace; the
-    kept hierarchy equals a rebuild; out-of-range indices raise the same flags."""
+    rows, s_avg, rowmax / block / superblock / table maxima and the workspace's rows, counts
+    and maxima (its values are scratch in the one-launch call); the kept hierarchy equals a
+    rebuild; out-of-range indices raise the same flags."""
     from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
 
     rows = COAL_ROWS
@@ -860,11 +861,10 @@ def test_fused_coalesce_apply_matches_two_launches(dq, D, B, dist, bits, repack)
         assert torch.equal(s_avg[0], s_avg[1])
         assert torch.equal(wss[0].ucount, wss[1].ucount)
         assert torch.equal(wss[0].absmax, wss[1].absmax)
-        for t in range(T):
-            r0, v0 = _table_slots(wss[0], t)
-            r1, v1 = _table_slots(wss[1], t)
+        for t in range(T):  # the one-launch call leaves workspace values scratch (kept on chip)
+            r0, _ = _table_slots(wss[0], t)
+            r1, _ = _table_slots(wss[1], t)
             np.testing.assert_array_equal(r0, r1)
-            np.testing.assert_array_equal(v0, v1)
         for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax") + (("packed",) if repack else ()):
             assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
     inc = [x.clone() for x in (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)]

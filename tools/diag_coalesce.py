@@ -56,6 +56,7 @@ for i in range(NB):  # one launch per batch, read after each
     c = buf.reshape(T, 8, 16).astype(np.int64)
     k0 = c[:, :, 0][c[:, :, 0] > 0].min()
     c = np.where(c >= k0, c - k0, -1)  # -1: not stamped in this launch
+    cs.append(c)
 end = 13 if APPLY else 7
 spans = [c[:, :, end].max() / 100 for c in cs]
 print(f"{cfg} B={B} D={D}: span median {np.median(spans):.1f} us over {NB} launches (min {min(spans):.1f}, "
@@ -88,6 +89,8 @@ if APPLY:
         ps = [slow(c, t, 13) for c in cs]
         if ps[0][11] < 0:
             continue
-        ph = np.median([[p[11] - p[6], p[12] - p[11], p[13] - p[12], p[13]] for p in ps], axis=0) / 100
-        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} {ph[1]:5.1f} {ph[2]:5.1f} || {ph[3]:5.1f}")
+        ph = np.median([[p[11] - p[6], p[12] - p[11], p[13] - p[12], p[13], p[14] - p[11], p[15] - p[14],
+                         p[12] - p[15]] for p in ps], axis=0) / 100
+        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} {ph[1]:5.1f} {ph[2]:5.1f} || {ph[3]:5.1f}   "
+              f"(updated = values+prefetched rows {ph[4]:4.1f} | rest+barrier {ph[5]:4.1f} | re-reduce {ph[6]:4.1f})")
 print("errors", ts.read_errors())
