@@ -403,6 +403,7 @@ def main():
         P = batches[(a.warmup + a.steps - 1) % len(batches)].idx.view(T, -1)
         U = int(sum(torch.unique(P[t]).numel() for t in range(T)))
     alg = alg_bytes(dom, T, B, D, U, world, pool1=True, repack=repack)
+    step_alg = sum(alg_bytes(n, T, B, D, U, world, pool1=True, repack=repack) for n in names)
     achieved = alg / (dom_ms * 1e-3) / 1e9
     err = ts.read_errors()
 
@@ -475,6 +476,11 @@ def main():
                          "traffic_src": traffic,
                          "alg_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 5),
                          "timed_launches": len(sampled)},
+            # the whole step against the same peak: every phase's algorithmic bytes / step time
+            "step_roofline": {"alg_bytes_per_step": step_alg,
+                              "achieved": round(step_alg / (elapsed / a.steps) / 1e9, 1),
+                              "frac": round(step_alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                              "phases": names},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events "
                                "(apply_local and bwd_sgd include the |W| hierarchy finalize launch)",

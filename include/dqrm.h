@@ -337,7 +337,8 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
                      void* stream);
 
 /* World size 1: dqrm_emb_bwd_coalesce followed by dqrm_apply_local, with the same results
- * (W, the |W| hierarchy, s_avg, packed rows, and the coalesced workspace) -- for a
+ * (W, the |W| hierarchy, s_avg, packed rows; the workspace's rows, counts and maxima -- its
+ * values are scratch: a slot that fits keeps them on chip) -- for a
  * Criteo-form batch (DQRM_BATCH_POOLING_ONE, num_bags <= 4096, num_tables <= 32) in ONE
  * launch: each table's workgroups meet once to share their gradient maxima and then
  * update their row ranges, the W rows having been read during the coalesce. Replaces
