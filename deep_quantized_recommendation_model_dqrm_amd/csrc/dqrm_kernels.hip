@@ -255,7 +255,9 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
     const float r = 1.0f / s;
     if (refresh && !full_precision && blockIdx.x == 0 && threadIdx.x == 0) a.scale[t] = s;
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
-    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    // Criteo form: table t's lookups are idx[t*B, (t+1)*B) -- no idx_base round trip in front of the index loads
+    const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
+    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ibase;
     const int64_t B = a.B;
     const int64_t* __restrict__ off = a.off + (int64_t)t * B;
     const int64_t* __restrict__ idx = a.idx + ibase;
@@ -377,7 +379,9 @@ __global__ void __launch_bounds__(256) k_emb_fwd_packed(FwdArgs a) {
     const float r = 1.0f / s;
     const float qlo = -(float)(1 << (a.bits - 1)), qhi = (float)((1 << (a.bits - 1)) - 1);
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
-    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    // Criteo form: table t's lookups are idx[t*B, (t+1)*B) -- no idx_base round trip in front of the index loads
+    const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
+    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ibase;
     const int64_t B = a.B;
     const int64_t* __restrict__ off = a.off + (int64_t)t * B;
     const int64_t* __restrict__ idx = a.idx + ibase;
@@ -3443,7 +3447,9 @@ __global__ void __launch_bounds__(256) k_lookup_grad(LgArgs a) {
     const int D = LPR * 4;
     const float s = a.scale[t];
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
-    const int64_t ibase = a.idx_base[t], L = a.idx_base[t + 1] - ibase;
+    // Criteo form: table t's lookups are idx[t*B, (t+1)*B) -- no idx_base round trip in front of the index loads
+    const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
+    const int64_t L = a.pool1 ? a.B : a.idx_base[t + 1] - ibase;
     const int64_t B = a.B;
     const int64_t* __restrict__ off = a.off + (int64_t)t * B;
     const bool p1 = a.pool1 && L == B;

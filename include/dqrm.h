@@ -117,9 +117,9 @@ typedef struct dqrm_batch {
     uint32_t reserved;
 } dqrm_batch;
 
-/* Criteo form (dlrm_data_pytorch.py:328-345): every table has L_t == B and
- * off[t][b] == b, i.e. bag b is lookup b. The kernels then skip the offsets round trip
- * (a table whose L_t != B is still read through its offsets). */
+/* Criteo form (dlrm_data_pytorch.py:328-345): every table has L_t == B (so idx_base[t] ==
+ * t * B) and off[t][b] == b, i.e. bag b is lookup b. The kernels then read neither the
+ * offsets nor idx_base. */
 #define DQRM_BATCH_POOLING_ONE 1u
 
 /* forward flags */
