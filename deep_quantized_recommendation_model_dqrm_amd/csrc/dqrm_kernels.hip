@@ -2965,6 +2965,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     __shared__ float s_sqo[SG_MAXL];                             // ... their old max
     __shared__ float s_red[NW];
     __shared__ int s_n[3];                                       // queue lengths, rescan flag
+    __shared__ int s_wsc[NW + 1];                                // block scan scratch
     const int t = blockIdx.x;
     DIAG_T(0);
     const Meta m = make_meta(a.meta, a.T);
@@ -3075,12 +3076,61 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
         own[k] = i < L && xk[k] >= 0 && !(__ballot(earlier != 0ull) & gmask);
     }
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    // Criteo form: every owner's matched positions, ascending, as one contiguous run of an LDS
+    // list (s_bag, unused by this form; the runs laid out by a block scan of the owners'
+    // counts), so that its ordered walk below reads 8 positions' dy per LDS round trip --
+    // a hot row of a tiny table has ~B/n of them
+    int rbase[NPG], rcnt[NPG];
+    if (p1) {
+        int pc[NPG], pre[NPG], mine = 0;
+#pragma unroll
+        for (int k = 0; k < NPG; ++k) {
+            pc[k] = (int)__popcll(mk[k]);
+            pre[k] = 0;
+            rcnt[k] = 0;
+#pragma unroll
+            for (int l = 0; l < LPR; ++l) {  // the group's count, and this lane's offset in it
+                const int v = __shfl(pc[k], gbase + l, WAVE);
+                rcnt[k] += v;
+                if (l < sub) pre[k] += v;
+            }
+            if (own[k] && sub == 0) mine += rcnt[k];
+        }
+        int tot;
+        int base = block_scan_excl<SG_TPB>(mine, s_wsc, &tot);
+#pragma unroll
+        for (int k = 0; k < NPG; ++k) {
+            rbase[k] = __shfl(base, gbase, WAVE);  // the group's lane 0 holds the run bases
+            if (own[k] && sub == 0) base += rcnt[k];
+            if (!own[k]) continue;
+            uint64_t m = mk[k];
+            int r = rbase[k] + pre[k];
+            while (m) {  // this lane's matches, ascending
+                s_bag[r++] = j0 + __ffsll((long long)m) - 1;
+                m &= m - 1;
+            }
+        }
+        __syncthreads();
+    }
     DIAG_T(3);
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
         if (!own[k]) continue;  // group-uniform
         float4 acc = w0[k];
-        for (int l = 0; l < LPR; ++l) {  // the row's positions, ascending
+        if (p1) {  // the run: 8 positions and their dy rows in flight, then the FMAs in order
+            for (int i0 = 0; i0 < rcnt[k]; i0 += 8) {
+                int jj[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) jj[q] = s_bag[rbase[k] + (i0 + q < rcnt[k] ? i0 + q : rcnt[k] - 1)];
+                float4 g[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) g[q] = s_dy[jj[q] * LPR + sub];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (i0 + q < rcnt[k]) acc = seg_op4<OP_FMA>(acc, g[q], a.nlr);
+            }
+        }
+        for (int l = 0; l < LPR && !p1; ++l) {  // the row's positions, ascending
             const uint32_t lo32 = (uint32_t)__shfl((int)(uint32_t)mk[k], gbase + l, WAVE);
             const uint32_t hi32 = (uint32_t)__shfl((int)(uint32_t)(mk[k] >> 32), gbase + l, WAVE);
             uint64_t ml = ((uint64_t)hi32 << 32) | lo32;
