@@ -49,7 +49,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CONFIGS = {k: dict(rows=r, dim=d) for k, (r, d) in _CONFIGS.items()}
 # host tables of the PyTorch-CPU baseline: the reference's own TB run stands in for the
 # 773 M-row profile (its 198 GB of FP32 rows exceed one bench run's host-memory budget)
-CPU_TABLES = {"terabyte": "terabyte_ref", "terabyte_ref": "terabyte_ref", "kaggle": "kaggle"}
+CPU_TABLES = {"terabyte": "terabyte_ref", "terabyte_ref": "terabyte_ref", "terabyte_1g": "terabyte_1g",
+              "kaggle": "kaggle"}
 
 
 def parse(argv=None):
@@ -58,13 +59,14 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="terabyte", choices=sorted(CONFIGS))
-    p.add_argument("--mode", default="dp", choices=["dp", "fwd", "sgd", "dropin-sgd", "dropin-dp"],
+    p.add_argument("--mode", default="dp", choices=["dp", "fwd", "sgd", "dropin-sgd", "dropin-dp", "dlrm"],
                    help="dp: data-parallel QAT step; fwd: forward only; sgd: forward + fused sparse SGD; "
                         "dropin-sgd / dropin-dp: the reference drivers' call pattern through the drop-in "
-                        "modules and hooks (see dropin_main)")
+                        "modules and hooks (see dropin_main); dlrm: the whole single-GPU DLRM QAT step "
+                        "(MLPs, interaction, BCE, backward, SGD; see dlrm_main)")
     p.add_argument("--dropin-form", default="list", choices=["list", "collection"],
-                   help="drop-in modes: the unchanged drivers' ModuleList of per-table QuantEmbeddingBagTwo, "
-                        "or one QuantEmbeddingBagCollection replacing apply_emb's loop")
+                   help="drop-in / dlrm modes: the unchanged drivers' ModuleList of per-table "
+                        "QuantEmbeddingBagTwo, or one QuantEmbeddingBagCollection replacing apply_emb's loop")
     p.add_argument("--grad-mode", default="sparse", choices=["sparse", "fused_sgd"],
                    help="dropin-sgd: module grad_mode (sparse = torch.optim.SGD on the per-lookup COO)")
     p.add_argument("--sync-every", type=int, default=0,
@@ -99,6 +101,10 @@ def parse(argv=None):
                    help="nccl (= RCCL on ROCm) for measurements; gloo only to rehearse N>1 on one GPU")
     p.add_argument("--unfused-local", action="store_true",
                    help="N=1: run quant-pack + payload apply instead of the fused dqrm_apply_local")
+    p.add_argument("--force-collectives", action="store_true",
+                   help="run the N>1 exchange (two all-gathers, quantize-pack, payload apply; the MLP "
+                        "exchange's collectives) through the process group at world size 1 too: the RCCL leg "
+                        "on a one-GPU box")
     p.add_argument("--two-launch-local", action="store_true",
                    help="N=1: coalesce + dqrm_apply_local as two launches (not dqrm_emb_bwd_apply_local)")
     p.add_argument("--sample-every", type=int, default=8,
@@ -109,7 +115,7 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
-PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "kaggle": "kaggle"}
+PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "terabyte_1g": "tb1g", "kaggle": "kaggle"}
 KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
     "emb_fwd": "k_emb_fwd<{lpr},",
     "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
@@ -122,14 +128,20 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
 }
 
 
-def pmc_traffic(path, phase, D):
+def pmc_traffic(path, phase, D, workload=None):
     """HBM bytes per launch of the phase's kernel from a committed rocprofv3 PMC summary
-    (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None. The summary must
+    have been profiled on the same workload (tools/prof_summary.py records the profiled bench
+    line's config, batch per GPU, mode and N=1 update form): a summary of another batch
+    size or mode is refused, not rescaled."""
     if not path or not os.path.exists(path) or phase not in KERNEL_SYMBOL:
+        return None
+    summ = json.load(open(path))
+    if workload is not None and summ.get("workload") != workload:
         return None
     sym = KERNEL_SYMBOL[phase]
     prefixes = tuple(p.format(lpr=D // 4) for p in (sym if isinstance(sym, tuple) else (sym,)))
-    kernels = json.load(open(path))["kernels"]
+    kernels = summ["kernels"]
     for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
         if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
             return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
@@ -216,13 +228,20 @@ def main():
     local = local % max(ndev, 1)  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    coll = world > 1 or a.force_collectives  # the exchange runs through the process group
+    if coll:
+        if world == 1:  # a lone rank outside torch.distributed.run
+            for k, v in (("RANK", "0"), ("WORLD_SIZE", "1"), ("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511")):
+                os.environ.setdefault(k, v)
         if a.dist_backend == "nccl":  # RCCL over xGMI, one process per GPU
             dist.init_process_group("nccl", device_id=dev)
         else:  # gloo: functional rehearsal of the N>1 path (e.g. several ranks on one GPU)
             dist.init_process_group("gloo")
     if a.mode.startswith("dropin"):
         dropin_main(a, world, rank, dev)
+        return
+    if a.mode == "dlrm":
+        dlrm_main(a, world, rank, dev)
         return
     cfg = CONFIGS[a.config]
     rows, D = cfg["rows"], cfg["dim"]
@@ -236,7 +255,8 @@ def main():
     batches = make_batches(rows, B_global, rank, world, a.num_batches, a.seed, a.index_dist, dev)
     dy = torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + rank)) * 0.05
     y = torch.empty(T, B, D, device=dev)
-    ex = dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits) if a.mode == "dp" else None
+    ex = (dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits, force_collectives=a.force_collectives)
+          if a.mode == "dp" else None)
     if a.use_packed:
         ts.refresh_scale_and_pack(4)
     torch.cuda.synchronize()
@@ -244,9 +264,10 @@ def main():
 
     # N=1: quantize-pack + apply fused (dqrm_apply_local; same quantize/dequantize/SGD
     # arithmetic, bit-identical W, no payload since nothing is exchanged)
-    fused = world == 1 and not a.unfused_local
+    fused = not coll and not a.unfused_local
     # one launch (dqrm_emb_bwd_apply_local) for Criteo-form batches of <= 4096 lookups, <= 32 tables
-    one_launch = fused and not a.two_launch_local and B <= 4096 and T <= 32
+    # whose grid the device can hold at once (the library decides; asked here for the line)
+    one_launch = fused and not a.two_launch_local and ts.apply_local_is_one_launch(batches[0])
     repack = a.use_packed
     names = phase_names(a.mode, a.use_packed, fused, one_launch)
 
@@ -288,7 +309,7 @@ def main():
             kern.apply_local(ex.ws, a.grad_bits, ex.s_avg, a.lr, repack)
             mark(2, 1)
             return
-        if ex.world == 1:
+        if not ex.coll:
             absmax_all = ex.ws.absmax.view(1, -1)
         else:
             ex._all_gather(ex.absmax_all, ex.ws.absmax)
@@ -296,7 +317,7 @@ def main():
         mark(2, 0)
         kern.quant_pack(ex.ws, absmax_all, ex.world, a.grad_bits, ex.cap_base, ex.cap_total, ex.s_avg, ex.payload)
         mark(2, 1)
-        if ex.world == 1:
+        if not ex.coll:
             gathered = ex.payload.view(1, -1)
         else:
             ex._all_gather(ex.gathered, ex.payload)
@@ -377,7 +398,7 @@ def main():
 
     # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
     # it runs on) on every sample_every-th step, so the events barely perturb the timing
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [timed_events(len(names)) for _ in range(a.steps)]
@@ -385,7 +406,7 @@ def main():
     t_start = time.perf_counter()
     for i in range(a.steps):
         run(a.warmup + i, evs[i] if i in sampled else None)
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
@@ -408,7 +429,7 @@ def main():
     err = ts.read_errors()
 
     gather = gather_phase(a, ts, rows, T, D, dev) if a.gather_batch > 0 else None
-    mlp = dense_phase(a, dev, world, rank) if a.mlp_iters > 0 else None
+    mlp = dense_phase(a, dev, world, rank, coll) if a.mlp_iters > 0 else None
 
     cpu = cpu_c = None  # the CPU baselines are N=1 figures: a single-rank run only
     if world == 1 and a.cpu_baseline:
@@ -426,8 +447,15 @@ def main():
         replicas_match = all(torch.equal(allcs[0], c) for c in allcs)
     else:
         replicas_match = True
+    n1_update = (None if a.mode != "dp" or world > 1 else
+                 "coalesce + quant-pack + payload apply (RCCL at world size 1)" if coll else
+                 "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
+                 "coalesce + dqrm_apply_local" if fused else "coalesce + quant-pack + payload apply")
+    workload = {"config": a.config, "mode": a.mode, "batch_per_gpu": B, "n1_update": n1_update,
+                "index_dist": a.index_dist}
     prof = a.traffic_profile or latest_profile(PROFILE_TAG[a.config])
-    traffic = pmc_traffic(prof, dom, D)
+    traffic = pmc_traffic(prof, dom, D, workload)
+    med_us = traffic["profiled_median_us"] if traffic else None
     if rank == 0:
         value = B_global * a.steps / elapsed
         metric = {
@@ -436,10 +464,10 @@ def main():
             "fwd": "forward samples/sec (INT4 fake-quant EmbeddingBag forward, 26 tables)",
             "sgd": "QAT-step samples/sec (1-GPU embedding QAT step: INT4 fake-quant gather + fused sparse SGD)",
         }[a.mode]
-        coll = None
+        colls = None
         if a.mode == "dp":
-            coll = {"world_size": world, "backend": a.dist_backend if world > 1 else None,
-                    "per_step": 2 if world > 1 else 0,
+            colls = {"world_size": world, "backend": a.dist_backend if coll else None,
+                    "per_step": 2 if coll else 0,
                     "scale_allgather_bytes_per_rank": ex.ws.absmax.numel() * 4,
                     "payload_allgather_bytes_per_rank": int(ex.payload_bytes)}
         line = {
@@ -465,9 +493,7 @@ def main():
                 "grad_bits": a.grad_bits if a.mode == "dp" else None,
                 "scale_period": max(a.scale_period, 1), "packed_int4_forward": a.use_packed,
                 "hip_graph": a.graph, "graph_steps": gs if a.graph else None,
-                "n1_update": (None if a.mode != "dp" or world > 1 else
-                              "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
-                              "coalesce + dqrm_apply_local" if fused else "coalesce + quant-pack + payload apply"),
+                "n1_update": n1_update,
                 "parallelism": f"dp{world} (tables replicated)",
             },
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -475,15 +501,21 @@ def main():
                          "traffic": traffic["bytes"] if traffic else None, "traffic_unit": "bytes/launch",
                          "traffic_src": traffic,
                          "alg_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 5),
-                         "timed_launches": len(sampled)},
+                         "timed_launches": len(sampled),
+                         # the same bytes over rocprofv3's median kernel time of this workload
+                         # (events bracket the launch and read a few us above the kernel)
+                         "frac_rocprof_median": (round(alg / (med_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                                                 if med_us else None),
+                         "workload_profiled": workload},
             # the whole step against the same peak: every phase's algorithmic bytes / step time
             "step_roofline": {"alg_bytes_per_step": step_alg,
                               "achieved": round(step_alg / (elapsed / a.steps) / 1e9, 1),
                               "frac": round(step_alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                               "phases": names},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
-            "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events "
-                               "(apply_local and bwd_sgd include the |W| hierarchy finalize launch)",
+            "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events (the |W| "
+                               "hierarchy is finalized inside the updating launches; apply_sparse_update "
+                               "and apply_local add a short finalize launch)",
             "weight_syncc": ({"every": sync_every, "ms_per_call": round(sync_ms, 3),
                               "amortized_us_per_step": round(sync_ms * 1e3 / sync_every, 2),
                               "in_timed_region": True} if sync_every else None),
@@ -492,7 +524,7 @@ def main():
                                    f"{a.scale_period} steps" if refresh_ms is not None else None),
             "launch_share": (round(max(0.0, 1.0 - sum(kms.values()) / (elapsed / a.steps * 1e3)), 4)
                              if not a.graph else None),
-            "collectives": coll,
+            "collectives": colls,
             "int4_gather": gather,
             "mlp_grad_exchange": mlp,
             "cpu_baseline": cpu,
@@ -502,7 +534,7 @@ def main():
             "setup_s": round(setup_s, 1),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if coll:
         dist.barrier()
         dist.destroy_process_group()
     if err:  # a step that dropped or mis-indexed lookups is not a measurement
@@ -666,6 +698,214 @@ def dropin_main(a, world, rank, dev):
         dist.destroy_process_group()
 
 
+class DLRMNet(torch.nn.Module):
+    """DLRM_Net of the single-GPU driver (dlrm_s_pytorch_single_gpu.py:271-962) at the
+    reference scripts' Kaggle shape: bottom MLP 13-512-256-64-16 (ReLU after every layer),
+    26 embedding tables, dot interaction without self-interaction (:696-801: the 351 pairs
+    j < i of the 27 vectors, concatenated after the bottom output -> 367), top MLP
+    367-512-256-1 (ReLU, ReLU, sigmoid), create_mlp's init (N(0, sqrt(2/(m+n))) weights,
+    N(0, sqrt(1/m)) biases, :293-336). `emb(P)` returns the 26 pooled vectors as [B, T, D]."""
+
+    def __init__(self, bot, top, emb, seed):
+        super().__init__()
+        rs = np.random.RandomState(seed)
+
+        def mlp(dims, sigmoid_last):
+            layers = []
+            for k, (n, m) in enumerate(zip(dims[:-1], dims[1:])):
+                lin = torch.nn.Linear(n, m)
+                with torch.no_grad():
+                    lin.weight.copy_(torch.from_numpy(rs.normal(0.0, np.sqrt(2 / (m + n)), (m, n)).astype(np.float32)))
+                    lin.bias.copy_(torch.from_numpy(rs.normal(0.0, np.sqrt(1 / m), m).astype(np.float32)))
+                layers += [lin, torch.nn.Sigmoid() if sigmoid_last and k == len(dims) - 2 else torch.nn.ReLU()]
+            return torch.nn.Sequential(*layers)
+
+        self.bot_l = mlp(bot, False)
+        self.top_l = mlp(top, True)
+        self.emb = emb
+        self._li = self._lj = None
+
+    def forward(self, X, P):
+        x = self.bot_l(X)
+        ly = self.emb(P)                                           # [B, T, D]
+        Tm = torch.cat([x.unsqueeze(1), ly], dim=1)                # [B, T+1, D]
+        Z = torch.bmm(Tm, Tm.transpose(1, 2))
+        if self._li is None:
+            n = Tm.shape[1]
+            self._li = torch.tensor([i for i in range(n) for j in range(i)], device=X.device)
+            self._lj = torch.tensor([j for i in range(n) for j in range(i)], device=X.device)
+        R = torch.cat([x, Z[:, self._li, self._lj]], dim=1)
+        return self.top_l(R)
+
+
+class _RefEmb(torch.nn.Module):
+    """The reference's embedding layer as PyTorch ops (QuantEmbeddingBagTwo on ATen): per table
+    nn.EmbeddingBag(mode="sum", sparse=True), the full-table aminmax scale every training
+    forward, fake quant + dequant with the STE backward."""
+
+    def __init__(self, rows, D, dev):
+        super().__init__()
+        self.bags = torch.nn.ModuleList()
+        for n in rows:
+            w = torch.empty(n, D, device=dev).uniform_(-float(np.sqrt(1 / n)), float(np.sqrt(1 / n)))
+            self.bags.append(torch.nn.EmbeddingBag(n, D, mode="sum", sparse=True, _weight=w))
+        self.register_buffer("off", torch.zeros(0, dtype=torch.int64, device=dev))
+
+    def forward(self, P):
+        B = P.shape[1]
+        if self.off.numel() != B:
+            self.off = torch.arange(B, dtype=torch.int64, device=P.device)
+        ys = []
+        for t, e in enumerate(self.bags):
+            with torch.no_grad():
+                mn, mx = torch.aminmax(e.weight)
+                s = torch.clamp(torch.maximum(mn.abs(), mx.abs()), min=1e-8) / 7.0
+            ys.append(_FakeQuantSTE.apply(e(P[t], self.off), s, 4))
+        return torch.stack(ys, dim=1)
+
+
+def dlrm_main(a, world, rank, dev):
+    """BASELINE config 3 as SURVEY 8(d) C3 writes it: the single-GPU driver's whole QAT step
+    (dlrm_s_pytorch_single_gpu.py:804-890 forward, :1936-1950 loss / backward / SGD) at the
+    Kaggle shape -- bottom MLP, 26 INT4 fake-quant EmbeddingBag tables, dot interaction, top
+    MLP, BCE, backward, SGD lr 0.1 -- with the embeddings from
+      --dropin-form collection: one QuantEmbeddingBagCollection, grad_mode fused_sgd (the
+                                 sparse SGD runs inside the backward kernel),
+      --dropin-form list:       26 QuantEmbeddingBagTwo modules + torch.optim.SGD on their
+                                 per-lookup COO grads (--grad-mode sparse) or fused_sgd,
+    next to the same model with the reference's modules as PyTorch ops on the same GPU. The
+    MLPs, interaction and loss are PyTorch (hipBLASLt GEMMs): outside the north-star path,
+    inside this measurement. --graph replays whole steps from HIP graphs (one per resident
+    batch); the loss is not copied to the host per step (the driver's E.detach().cpu() is a
+    logging sync)."""
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+
+    if world > 1:
+        print("--mode dlrm is the single-GPU step (config 3)", file=sys.stderr)
+        sys.exit(2)
+    rows, D = CONFIGS[a.config]["rows"], CONFIGS[a.config]["dim"]
+    T = len(rows)
+    B = a.batch_per_gpu
+    bot, top = MLPS[a.config]
+    Q.set_pooling_one_inputs(True)
+    gm = "fused_sgd" if a.dropin_form == "collection" else a.grad_mode
+    g = torch.Generator(device=dev).manual_seed(a.seed)
+    batches = make_batches(rows, B, 0, 1, a.num_batches, a.seed, a.index_dist, dev)
+    Ps = [b.idx.view(T, B) for b in batches]
+    Xs = [torch.rand(B, bot[0], device=dev, generator=g) for _ in range(a.num_batches)]
+    Ys = [torch.round(torch.rand(B, 1, device=dev, generator=g)) for _ in range(a.num_batches)]
+    lS_o = torch.arange(B, dtype=torch.int64, device=dev)
+
+    def build(kind):
+        if kind == "collection":
+            coll = Q.QuantEmbeddingBagCollection(rows, D, 4, init="device", grad_mode="fused_sgd", lr=a.lr, device=dev)
+            emb = lambda P: coll(lS_o.expand(T, B), P, layout="btd")  # noqa: E731
+            holder, emb_params = coll, []
+        elif kind == "list":
+            mods = torch.nn.ModuleList([Q.QuantEmbeddingBagTwo(n, D, 4, embedding_id=i, init="device", grad_mode=gm,
+                                                               lr=a.lr, device=dev) for i, n in enumerate(rows)])
+            emb = lambda P: torch.stack([mods[t](P[t], lS_o) for t in range(T)], dim=1)  # noqa: E731
+            holder = mods
+            emb_params = [] if gm == "fused_sgd" else [m.embedding_bag.weight for m in mods]
+        else:
+            holder = _RefEmb(rows, D, dev)
+            emb, emb_params = holder, list(holder.parameters())
+
+        class _E(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.h = holder
+
+            def forward(self, P):
+                return emb(P)
+
+        net = DLRMNet(bot, top, _E(), a.seed).to(dev)
+        params = list(net.bot_l.parameters()) + list(net.top_l.parameters()) + emb_params
+        opt = torch.optim.SGD(params, lr=a.lr)
+        return net, opt, holder
+
+    loss_fn = torch.nn.BCELoss(reduction="mean")
+
+    def timed(kind, graph):
+        net, opt, holder = build(kind)
+
+        def step(i):
+            k = i % a.num_batches
+            opt.zero_grad(set_to_none=True)
+            E = loss_fn(net(Xs[k], Ps[k]), Ys[k])
+            E.backward()
+            opt.step()
+            return E
+
+        for i in range(a.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        launches = count_launches(lambda: step(0))
+        graphs = None
+        if graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for i in range(3):
+                    step(i)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graphs = []
+            for k in range(a.num_batches):
+                gr = torch.cuda.CUDAGraph()
+                opt.zero_grad(set_to_none=True)
+                with torch.cuda.graph(gr):
+                    E = loss_fn(net(Xs[k], Ps[k]), Ys[k])
+                    E.backward()
+                    opt.step()
+                graphs.append(gr)
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            if graphs is not None:
+                graphs[i % a.num_batches].replay()
+            else:
+                step(a.warmup + i)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) / a.steps * 1e6
+        errs = None
+        if kind == "collection":
+            errs = holder._tset.read_errors()
+        elif kind == "list":
+            errs = 0
+            for m in holder:
+                errs |= m._tset.read_errors()
+        del net, opt, holder, graphs
+        torch.cuda.empty_cache()
+        return us, launches, errs
+
+    us, launches, errs = timed(a.dropin_form, a.graph)
+    ref_us, ref_launches, _ = timed("torch", False)
+    line = {
+        "metric": "DLRM QAT-step samples/sec, 1 GPU (config 3: bottom/top MLP, dot interaction, 26 INT4 "
+                  "fake-quant EmbeddingBag tables, BCE, backward, SGD lr %g)" % a.lr,
+        "value": round(B * a.steps / (us * 1e-6 * a.steps), 1) if not errs else None,
+        "unit": "samples/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(us / 1e3, 4), "us_per_step": round(us, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32 (int4 fake-quant embeddings, fp32 MLP)",
+        "data": "synthetic (uniform-random Criteo-form indices, U[0,1) dense features, Bernoulli labels)",
+        "config": {"workload": f"criteo-{a.config} DLRM QAT step ({a.dropin_form}, {gm})", "tables": T,
+                   "total_rows": sum(rows), "emb_dim": D, "batch_per_gpu": B, "mlp_bot": bot, "mlp_top": top,
+                   "interaction": "dot", "loss": "BCE", "optimizer": "SGD lr %g" % a.lr,
+                   "hip_graph": a.graph, "parallelism": "dp1"},
+        "launches_per_step": launches,
+        "torch_gpu_reference": {"us_per_step": round(ref_us, 2), "launches_per_step": ref_launches,
+                                "speedup": round(ref_us / us, 2),
+                                "what": "the same model and step with the reference's embedding modules as "
+                                        "PyTorch ops on this GPU (nn.EmbeddingBag sparse + per-step full-table "
+                                        "aminmax scale + fake-quant STE, torch.optim.SGD), eager"},
+        "reference_published": "27.6 ms/it on 1x A5000 (bash_scripts/Kaggle/emb_bit_4.txt:49-50; other "
+                               "hardware, loss copied to host every step: context only)",
+        "device_errors": errs,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def torch_reference_gpu(a, rows, D, B, dev, batches, dys, dp, steps=30):
     """The reference's own step as PyTorch ops on this GPU at the drop-in's shape (what a user
     of the reference runs on MI355X without this package): per table nn.EmbeddingBag(mode="sum",
@@ -739,7 +979,7 @@ def gather_phase(a, ts, rows, T, D, dev):
             "bytes_per_lookup": per}
 
 
-def dense_phase(a, dev, world, rank):
+def dense_phase(a, dev, world, rank, coll=False):
     """MLP half of the DP step, outside the timed embedding step:
     per-channel INT8 quantize of every bot_l/top_l gradient, scale all-gather, fp16-wire
     all-reduce (RCCL at N>1), decode, SGD update -- DenseGradExchange.exchange + apply.
@@ -756,14 +996,14 @@ def dense_phase(a, dev, world, rank):
             lin.weight.grad = torch.randn(o, i, device=dev, generator=g) * 1e-3
             lin.bias.grad = torch.randn(o, device=dev, generator=g) * 1e-3
             layers.append(lin)
-    ex = DenseGradExchange(layers, grad_bits=8)
+    ex = DenseGradExchange(layers, grad_bits=8, force_collectives=coll)
     P = ex.channels.total_elems
     wire_b = ex.wire.element_size()
     with torch.no_grad():
         for _ in range(5):
             ex.exchange()
             ex.apply(1e-6)
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize()
         ev = timed_events(a.mlp_iters)
@@ -779,7 +1019,7 @@ def dense_phase(a, dev, world, rank):
     return {"layers": f"bot {'-'.join(map(str, bot))}, top {'-'.join(map(str, top))}", "params": P,
             "channels": ex.channels.num_channels, "wire": str(ex.wire.dtype).replace("torch.", ""),
             "wire_bytes_per_rank": P * wire_b, "ms": round(ms, 4), "alg_bytes": alg,
-            "GBps": round(alg / (ms * 1e-3) / 1e9, 1), "launches": 4, "collectives": 2 if world > 1 else 0,
+            "GBps": round(alg / (ms * 1e-3) / 1e9, 1), "launches": 4, "collectives": 2 if ex.coll else 0,
             "note": "median of per-iteration HIP events; exchange+apply of all layers"}
 
 

@@ -119,12 +119,15 @@ def payload_bytes(num_tables: int, cap_total: int, dim: int, grad_bits: int) -> 
     return a16(4 * num_tables * L.DQRM_TABLE_SPLIT) + a16(4 * cap_total) + a16(cap_total * dim * elem)
 
 
-def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, world: int | None = None) -> None:
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, world: int | None = None,
+                    force: bool = False) -> None:
     """out [N, ...] <- every rank's inp, in rank order. nccl (RCCL on ROCm): one
     all_gather_into_tensor straight into `out` over xGMI; gloo: staged through host memory
-    when the tensors live on the GPU (functional rehearsal only)."""
+    when the tensors live on the GPU (functional rehearsal only). World size 1 is a local
+    copy unless `force` (a process group must exist then): the collective itself runs, as on
+    N > 1 (exercises the RCCL leg on a one-GPU box)."""
     world = world if world is not None else (dist.get_world_size(group) if dist.is_initialized() else 1)
-    if world == 1:
+    if world == 1 and not force:
         out.view(-1)[: inp.numel()].copy_(inp.view(-1))
         return
     backend = dist.get_backend(group)
@@ -160,9 +163,11 @@ class SparseGradExchange:
 
     def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None,
                  kernels: ExchangeKernels | None = None, device=None, absmax_buf: torch.Tensor | None = None,
-                 payload_buf: torch.Tensor | None = None):
+                 payload_buf: torch.Tensor | None = None, force_collectives: bool = False):
         """absmax_buf / payload_buf: caller-owned slices of buffers several sets gather
-        together (MultiSetExchange); the per-set gather buffers are then not allocated."""
+        together (MultiSetExchange); the per-set gather buffers are then not allocated.
+        force_collectives: run the N > 1 step (both all-gathers, quantize-pack, payload
+        decode) at world size 1 too, through the process group's backend."""
         if not (grad_bits == 32 or 2 <= grad_bits <= 16):
             raise ValueError("grad_bits must be 2..16 or 32")
         self.tables = tables
@@ -171,6 +176,10 @@ class SparseGradExchange:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
+        # exchange through the collectives (N > 1, or forced at N = 1)
+        self.coll = self.world > 1 or bool(force_collectives)
+        if self.coll and not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("force_collectives needs an initialised process group")
         dev = torch.device(device if device is not None else tables.device)
         self.device = dev
         self.kernels = kernels if kernels is not None else HipExchangeKernels(tables)
@@ -196,7 +205,7 @@ class SparseGradExchange:
 
     # -------------------------------------------------------------- collectives
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        all_gather_into(out, inp, self.group, self.world)
+        all_gather_into(out, inp, self.group, self.world, force=self.coll)
 
     # -------------------------------------------------------------- the step
     def exchange(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True, layout: str = "tbd") -> torch.Tensor:
@@ -206,13 +215,13 @@ class SparseGradExchange:
         gb = self.grad_bits
         k = self.kernels
         k.coalesce(batch, dy, self.ws, ste, layout)
-        if gb != 32 and self.world > 1:
+        if gb != 32 and self.coll:
             self._all_gather(self.absmax_all, self.ws.absmax)
             absmax_all = self.absmax_all
         else:
             absmax_all = self.ws.absmax.view(1, -1)
         k.quant_pack(self.ws, absmax_all, self.world, gb, self.cap_base, self.cap_total, self.s_avg, self.payload)
-        if self.world > 1:
+        if self.coll:
             self._all_gather(self.gathered, self.payload)
         return self.s_avg
 
@@ -221,7 +230,7 @@ class SparseGradExchange:
         gb = self.grad_bits
         if mode is None:
             mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
-        gathered = self.payload.view(1, -1) if self.world == 1 else self.gathered
+        gathered = self.gathered if self.coll else self.payload.view(1, -1)
         self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, gb, self.s_avg,
                            lr, mode, repack)
 
@@ -233,7 +242,7 @@ class SparseGradExchange:
         one fused kernel (dqrm_apply_local, bit-identical; no payload is produced)."""
         gb = self.grad_bits
         fused = getattr(self.kernels, "apply_local", None)
-        if (fused is not None and self.world == 1 and 2 <= gb <= 16
+        if (fused is not None and not self.coll and 2 <= gb <= 16
                 and (mode is None or mode == L.DQRM_UPD_DP)):
             one = getattr(self.kernels, "coalesce_apply_local", None)
             if one is not None:  # the whole local step in one launch (Criteo-form batches)

@@ -34,6 +34,7 @@
 // dimension-split table come from one L2.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <stdint.h>
 
@@ -410,6 +411,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_ucnt[SPLIT];
     __shared__ float s_red[NW];
     __shared__ float s_am;
+    __shared__ int s_stall;
     __shared__ int s_oq_n;
     __shared__ int s_dirty;
     __shared__ int s_fin;
@@ -1007,20 +1009,29 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if (APPLY && tid < WAVE) {  // wave 0: lane j polls slot j's granule until it shows this launch's epoch
         uint64_t g = 0;
         bool ok = tid >= NA;
+        bool stalled = false;
         for (int spin = 0;; ++spin) {
             if (!ok) {
                 g = __hip_atomic_load(gran + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = (uint32_t)(g >> 32) == epoch;
             }
             if (__all(ok)) break;
-            if (spin > (1 << 20)) {  // the table's workgroups were not all resident: flagged, no hang
+            // the table's workgroups were not all resident (the host checks the device's CUs,
+            // the occupancy and the stream's CU mask before it launches this form; another
+            // stream's kernels can still hold CUs): flagged, no hang -- and this workgroup
+            // does NOT update its rows, since the table scale would come from stale maxima
+            if (spin > (1 << 20)) {
                 if (tid == 0) flag_error(a.err, DQRM_ERRF_STALL);
+                stalled = true;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
         const float am = wave_max(tid < NA ? __uint_as_float((uint32_t)g) : 0.0f);
-        if (tid == 0) s_am = am;
+        if (tid == 0) {
+            s_am = am;
+            s_stall = stalled ? 1 : 0;
+        }
     }
     if (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT)) {
         const int sl = dsplit ? tid : s;
@@ -1039,7 +1050,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // the update of dqrm_apply_local: s = clamp(max|g|, 1e-8) / (2^(bits-1)-1) (* 1/N,
         // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
         const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
-        if (s == 0 && tid == 0) la.s_avg[t] = sv;
+        const bool go = s_stall == 0;  // a stalled workgroup leaves its rows as they were
+        if (go && s == 0 && tid == 0) la.s_avg[t] = sv;
         const float rr = 1.0f / sv;
         const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
@@ -1106,7 +1118,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             }
             return dsplit ? ld4_sc1(vb, (uint32_t)q * 16u) : reinterpret_cast<const float4*>(vb)[q];
         };
-        for (int sl = s, j0 = 0; sl < SPLIT; sl += NA, j0 = 1) {  // uniform
+        for (int sl = s, j0 = 0; go && sl < SPLIT; sl += NA, j0 = 1) {  // uniform
             int ua, nu;
             slot_entries(sl, ua, nu);
             const int nit = nu << lpr_sh;
@@ -1212,10 +1224,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 
 }  // namespace
 
-namespace dqrm_internal {
-
-hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream) {
-    // the attribute is per function, process-wide: set once (thread-safe), re-checked each call
+namespace {
+// the attribute is per function, process-wide: set once (thread-safe), re-checked each call
+hipError_t allow_coalesce_lds() {
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
@@ -1225,10 +1236,57 @@ hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la
             attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1<true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     });
+    return attr;
+}
+}  // namespace
+
+namespace dqrm_internal {
+
+int coalesce_apply_grid(int T) { return (T + 7) / 8 * 64; }
+
+bool coalesce_apply_resident(int T, hipStream_t stream) {
+    if (T <= 0 || T > kCoalesceApplyMaxT) return false;
+    // per device, once: CUs x workgroups of k_coalesce_p1<true> a CU holds (1024 threads,
+    // 156 KiB LDS: one). A query that fails counts as "does not fit".
+    struct Dev { std::once_flag once; int cus = 0, occ = 0; };
+    static Dev devs[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    Dev& d = devs[dev];
+    std::call_once(d.once, [&d, dev] {
+        int cus = 0, occ = 0;
+        if (allow_coalesce_lds() != hipSuccess) return;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_coalesce_p1<true>),
+                                                         TPB, LDS_BYTES) != hipSuccess)
+            return;
+        d.cus = cus;
+        d.occ = occ;
+    });
+    const int grid = coalesce_apply_grid(T);
+    if ((int64_t)d.occ * d.cus < grid) return false;  // e.g. a CPX partition (32 CUs)
+    // the stream's CU mask (hipExtStreamCreateWithCUMask): every CU of the device must be
+    // enabled, since the hardware deals the grid over the XCDs whatever the mask leaves
+    uint32_t mask[32] = {};
+    const int words = (d.cus + 31) / 32;
+    if (words > 32) return false;
+    if (stream == nullptr) {  // the legacy default stream has no mask of its own; a process-wide one
+        const char* g = getenv("ROC_GLOBAL_CU_MASK");  // (HIP's global CU mask) is not assumed full
+        const char* h = getenv("HSA_CU_MASK");
+        return !(g && *g) && !(h && *h);
+    }
+    if (hipExtStreamGetCUMask(stream, (uint32_t)words, mask) != hipSuccess) return false;
+    int on = 0;
+    for (int i = 0; i < words; ++i) on += __builtin_popcount(mask[i]);
+    return on >= d.cus;
+}
+
+hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream) {
+    const hipError_t attr = allow_coalesce_lds();
     if (attr != hipSuccess) return attr;
     const dim3 grid((a.T + 7) / 8 * 64);
     if (la) {
-        if (a.T > kCoalesceApplyMaxT) return hipErrorInvalidValue;  // not all resident at once
+        if (!coalesce_apply_resident(a.T, stream)) return hipErrorInvalidValue;  // not all resident at once
         hipLaunchKernelGGL(k_coalesce_p1<true>, grid, dim3(TPB), LDS_BYTES, stream, a, *la);
     } else {
         hipLaunchKernelGGL(k_coalesce_p1<false>, grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});

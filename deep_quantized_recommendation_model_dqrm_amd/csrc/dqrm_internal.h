@@ -55,8 +55,13 @@ constexpr int64_t kCoalesceMaxB = 4096;
 // workgroups wait for each other's gradient maxima
 constexpr int kCoalesceApplyMaxT = 32;
 
-// launches k_coalesce_p1 (dqrm_coalesce.hip); la != nullptr: the fused update as well.
-// Returns the HIP error of the launch.
+// Whether the fused form's grid of T tables can be resident at once on the current device
+// from `stream`: workgroups per CU (occupancy query) x CUs >= the grid, and the stream's CU
+// mask enables every CU. Device properties are queried once per device.
+bool coalesce_apply_resident(int T, hipStream_t stream);
+
+// launches k_coalesce_p1 (dqrm_coalesce.hip); la != nullptr: the fused update as well
+// (hipErrorInvalidValue if !coalesce_apply_resident). Returns the HIP error of the launch.
 hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream);
 
 }  // namespace dqrm_internal

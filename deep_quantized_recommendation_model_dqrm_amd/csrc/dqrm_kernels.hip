@@ -4153,6 +4153,26 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
     return DQRM_OK;
 }
 
+// dqrm_emb_bwd_apply_local's choice: one launch for Criteo-form batches whose grid can be
+// resident at once (device CUs, occupancy, the stream's CU mask), the two calls otherwise
+static bool apply_local_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, void* stream) {
+    static const bool fused_off = [] {
+        const char* e = getenv("DQRM_LOCAL_FUSED");
+        return e && !strcmp(e, "0");
+    }();
+    return !fused_off && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && (batch->flags & DQRM_BATCH_POOLING_ONE) &&
+           batch->num_bags <= dqrm_internal::kCoalesceMaxB && batch->max_lookups >= batch->num_bags &&
+           set->total_rows <= 0xffffffffll && set->num_tables <= dqrm_internal::kCoalesceApplyMaxT &&
+           dqrm_internal::coalesce_apply_resident(set->num_tables, (hipStream_t)stream);
+}
+
+int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_bwd_apply_local_is_one_launch"))) return rc;
+    return apply_local_one_launch(set, batch, stream) ? 1 : 0;
+}
+
 int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                              int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
                              int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
@@ -4171,13 +4191,7 @@ int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch,
     if (repack_bits && (repack_bits != 4 || !set->packed))
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)",
                          "dqrm_emb_bwd_apply_local", repack_bits);
-    static const bool fused_off = [] {
-        const char* e = getenv("DQRM_LOCAL_FUSED");
-        return e && !strcmp(e, "0");
-    }();
-    if (!fused_off && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && (batch->flags & DQRM_BATCH_POOLING_ONE) &&
-        batch->num_bags <= dqrm_internal::kCoalesceMaxB && batch->max_lookups >= batch->num_bags &&
-        set->total_rows <= 0xffffffffll && set->num_tables <= dqrm_internal::kCoalesceApplyMaxT) {
+    if (apply_local_one_launch(set, batch, stream)) {
         if (batch->num_bags <= 0) return DQRM_OK;
         dqrm_internal::CoalesceArgs ca{};
         ca.meta = set->meta; ca.T = set->num_tables; ca.D = set->dim; ca.B = batch->num_bags; ca.idx = batch->idx;

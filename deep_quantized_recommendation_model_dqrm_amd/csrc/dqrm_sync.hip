@@ -31,7 +31,11 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
     return x ^ (x >> 31);
 }
 
-// out += sum_i mix64(word_i | i << 32): 4 words per thread per pass, one atomic per wave
+// the position term of word i: i * an odd constant (a bijection of the full 64-bit index, so
+// no two positions alias however large the buffer)
+__device__ __forceinline__ uint64_t pos64(uint64_t i) { return i * 0xD1B54A32D192ED03ull; }
+
+// out += sum_i mix64(word_i ^ pos64(i)): 4 words per thread per pass, one atomic per wave
 __global__ void __launch_bounds__(256) k_checksum64(const uint32_t* __restrict__ w, int64_t n,
                                                     unsigned long long* __restrict__ out) {
     uint64_t acc = 0;
@@ -40,11 +44,11 @@ __global__ void __launch_bounds__(256) k_checksum64(const uint32_t* __restrict__
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
         const uint4 v = reinterpret_cast<const uint4*>(w)[q];
         const uint64_t i = (uint64_t)q * 4;
-        acc += mix64(v.x | (i << 32)) + mix64(v.y | ((i + 1) << 32)) + mix64(v.z | ((i + 2) << 32)) +
-               mix64(v.w | ((i + 3) << 32));
+        acc += mix64(v.x ^ pos64(i)) + mix64(v.y ^ pos64(i + 1)) + mix64(v.z ^ pos64(i + 2)) +
+               mix64(v.w ^ pos64(i + 3));
     }
     for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        acc += mix64(w[i] | ((uint64_t)i << 32));
+        acc += mix64(w[i] ^ pos64((uint64_t)i));
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (threadIdx.x % 64 == 0) atomicAdd(out, (unsigned long long)acc);
 }

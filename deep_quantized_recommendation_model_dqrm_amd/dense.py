@@ -162,7 +162,10 @@ class DenseGradExchange:
     """
 
     def __init__(self, layers: Sequence[nn.Module], grad_bits: int = 8, group=None,
-                 kernels: DenseKernels | None = None, device=None, wire_type: int | None = None):
+                 kernels: DenseKernels | None = None, device=None, wire_type: int | None = None,
+                 force_collectives: bool = False):
+        """force_collectives: issue the scale all-gather and the wire all-reduce at world
+        size 1 too, through the process group's backend (the N > 1 code path)."""
         if not (grad_bits == 32 or 2 <= grad_bits <= 16):
             raise ValueError("grad_bits must be 2..16 or 32")
         self.channels = DenseChannels(layers)
@@ -170,6 +173,9 @@ class DenseGradExchange:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.coll = self.world > 1 or bool(force_collectives)
+        if self.coll and not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("force_collectives needs an initialised process group")
         if device is None:
             device = self.channels.layers[0].weight.device if self.channels.layers else "cpu"
         self.device = torch.device(device)
@@ -217,7 +223,7 @@ class DenseGradExchange:
         k.prepare()
         if gb != 32:
             k.scale(gb, self.s_loc)
-            if self.world > 1:
+            if self.coll:
                 self._all_gather_scales()
                 s_all = self.s_all
             else:
@@ -225,7 +231,7 @@ class DenseGradExchange:
         else:
             s_all = None
         k.quant(gb, s_all, self.world, self.s_avg if gb != 32 else None, self.wire_type, self.wire)
-        if self.world > 1:
+        if self.coll:
             self._all_reduce_wire()
         k.decode(self.wire, self.wire_type, self.world)
         if gb != 32:

@@ -50,8 +50,10 @@ def set_error_check_interval(steps: int) -> None:
     training calls -- in the module's forward for grad_mode "sparse" / "fused_sgd", in
     weight_update_parallel_comm for "dp" -- and raise DQRMError when one is set (ATen raises
     on such input). Default 8; 0 = never. A poll never synchronises the host: it reads the
-    last completed asynchronous snapshot of the flag word (EmbeddingTableSet.poll_errors), so
-    a bad batch raises within `steps` + 2 calls after the call that consumed it."""
+    last completed asynchronous snapshot of the flag word (EmbeddingTableSet.poll_errors) and
+    takes the next one, so a flag raised just after a snapshot is read two polls later: a bad
+    batch raises within about 2 * `steps` + 1 calls after the call that consumed it. Calls
+    inside a HIP graph capture do not poll (the capture records device work only)."""
     global _ERROR_CHECK_EVERY
     _ERROR_CHECK_EVERY = max(0, int(steps))
 
@@ -182,7 +184,8 @@ class _QuantEmbeddingBase(nn.Module):
     def _check_errors(self, test_mode: bool) -> None:
         """grad_mode "sparse" / "fused_sgd": flags raised by the previous call's kernels
         surface here, at the next training call (the DP hooks check them for "dp")."""
-        if self.grad_mode != "dp" and not test_mode and error_check_due(self):
+        if (self.grad_mode != "dp" and not test_mode and error_check_due(self)
+                and not torch.cuda.is_current_stream_capturing()):
             poll_device_errors(self._tset)
 
     # ------------------------------------------------------------ scale refresh logic
@@ -319,6 +322,30 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
         return out
 
 
+def can_consolidate(modules) -> bool:
+    """Whether consolidate_tables(modules) would move the tables: at least two single-table
+    modules, not yet one set, alike (device, dim, packed rows), and room on the device for a
+    second copy of the tables while they move. Data-parallel callers agree this over the ranks
+    before consolidating (the payload layout depends on it)."""
+    mods = list(modules)
+    if len(mods) < 2 or any(not isinstance(m, QuantEmbeddingBagTwo) for m in mods):
+        return False
+    first = mods[0]._tset
+    if first.parent is not None and all(m._tset.parent is first.parent for m in mods):
+        return False  # already one set
+    dev, D = first.device, first.D
+    packed = first.packed is not None
+    if any(m._tset.device != dev or m._tset.D != D or (m._tset.packed is not None) != packed for m in mods):
+        return False
+    rows = [m._tset.num_rows[0] for m in mods]
+    need = sum(rows) * (D * 4 + (D // 2 if packed else 0) + 4)  # W, INT4 rows, row maxima
+    if dev.type == "cuda":
+        free, _ = torch.cuda.mem_get_info(dev)
+        if need * 1.1 + (256 << 20) > free:
+            return False
+    return True
+
+
 def consolidate_tables(modules, force: bool = False) -> EmbeddingTableSet | None:
     """Move the tables of several single-table modules (the DP driver's ModuleList of
     QuantEmbeddingBagTwo, dlrm_s_pytorch_tb_dp_one_parallel_comm.py:380) into ONE table set:
@@ -427,4 +454,4 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
 
 
 __all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode",
-           "set_error_check_interval", "set_pooling_one_inputs", "consolidate_tables"]
+           "set_error_check_interval", "set_pooling_one_inputs", "consolidate_tables", "can_consolidate"]

@@ -37,8 +37,8 @@ from torch import nn
 from . import _lib as L
 from .comm import ConsolidatedExchange, MultiSetExchange, SparseGradExchange
 from .dense import DenseGradExchange
-from .quant_modules_not_quantize_grad import (_QuantEmbeddingBase, consolidate_tables, error_check_due,
-                                              poll_device_errors, set_error_check_interval)
+from .quant_modules_not_quantize_grad import (_QuantEmbeddingBase, can_consolidate, consolidate_tables,
+                                              error_check_due, poll_device_errors, set_error_check_interval)
 
 _MLP_PLAIN_LINEAR = False
 
@@ -141,13 +141,28 @@ def _outgrown(need, caps, group) -> bool:
     return True
 
 
-def _consolidated_set(model, mods):
-    """The one set holding every module's table (consolidating on first use), or None."""
+def _all_ranks_agree(ok: bool, group, dev) -> bool:
+    """True only if `ok` holds on every rank of the group (one all-reduce MIN, at setup)."""
+    if _world(group) == 1:
+        return ok
+    on_dev = dist.get_backend(group) == "nccl"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def _consolidated_set(model, mods, group=None):
+    """The one set holding every module's table (consolidating on first use), or None. The
+    choice changes the payload layout (one consolidated set vs one payload section per set),
+    so at N > 1 the tables are consolidated only if EVERY rank can (free device memory may
+    differ between ranks)."""
     big = getattr(model, "_dqrm_consolidated", None)
     if big is None:
         big = False
-        if _CONSOLIDATE and len(mods) > 1:
-            big = consolidate_tables(mods) or False
+        if len(mods) > 1:
+            ok = _all_ranks_agree(_CONSOLIDATE and can_consolidate(mods), group, mods[0]._tset.device)
+            if ok:
+                big = consolidate_tables(mods, force=True) or False
         model._dqrm_consolidated = big
     if big is False:
         first = mods[0]._tset.parent
@@ -166,7 +181,7 @@ def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group)
     sets share one device error word so one read per step covers them all. A ModuleList of
     per-table modules is consolidated into one set (ConsolidatedExchange: one launch per
     phase); otherwise one MultiSetExchange over the modules' sets."""
-    big = _consolidated_set(model, mods) if len(mods) > 1 else None
+    big = _consolidated_set(model, mods, group) if len(mods) > 1 else None
     if big is not None and all(m._pending is not None for m in mods) \
             and len({m._pending[0].num_bags for m in mods}) == 1:
         need = max(max(m._pending[0].max_lookups, 1) for m in mods)

@@ -489,6 +489,15 @@ class EmbeddingTableSet:
             "dqrm_emb_bwd_coalesce",
         )
 
+    def apply_local_is_one_launch(self, batch: LookupBatch) -> bool:
+        """Whether backward_apply_local runs this batch as ONE launch on the current stream
+        (Criteo form, <= 4096 lookups, <= 32 tables, and the grid resident at once: device CUs,
+        occupancy and the stream's CU mask; dqrm_bwd_apply_local_is_one_launch)."""
+        rc = self.lib.dqrm_bwd_apply_local_is_one_launch(C.byref(self._c), C.byref(batch.c), _stream_handle())
+        if rc < 0:
+            L.check(rc, "dqrm_bwd_apply_local_is_one_launch")
+        return rc == 1
+
     def backward_apply_local(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad", grad_bits: int,
                              s_avg: torch.Tensor, lr: float, repack: bool = False, ste: bool = True,
                              layout: str = "tbd") -> None:

@@ -20,10 +20,17 @@ TERABYTE_ROWS = [9980200, 26095, 17224, 7383, 20152, 3, 7112, 1435, 62, 9756762,
 # BASELINE config 5 (~800 M rows): the TB profile with its six >= 1 M-row tables x16 (773,280,534 rows)
 TERABYTE_X16_ROWS = [n * 16 if n >= 1_000_000 else n for n in TERABYTE_ROWS]
 
+# A diagnostic profile, not a BASELINE config: the TB profile with its >= 1 M-row tables cut to
+# 500 k rows (3.8 M rows, 0.98 GB): the same lookups and (uniform) distinct rows per step as
+# "terabyte", on a slab whose pages a TLB can cover -- separates address translation from the
+# rest of the step's cost.
+TERABYTE_1G_ROWS = [500_000 if n >= 1_000_000 else n for n in TERABYTE_ROWS]
+
 # name -> (rows, embedding dim); the bench's --config
 CONFIGS = {
     "terabyte": (TERABYTE_X16_ROWS, 64),   # BASELINE configs[4]
     "terabyte_ref": (TERABYTE_ROWS, 64),   # the reference's own TB run (49.1 M rows)
+    "terabyte_1g": (TERABYTE_1G_ROWS, 64),  # diagnostic (translation A/B), see above
     "kaggle": (KAGGLE_ROWS, 16),           # BASELINE configs[1-3]
 }
 
@@ -33,6 +40,7 @@ CONFIGS = {
 MLPS = {
     "terabyte": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
     "terabyte_ref": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
+    "terabyte_1g": ([13, 512, 256, 64], [64 + 351, 512, 512, 256, 1]),
     "kaggle": ([13, 512, 256, 64, 16], [16 + 351, 512, 256, 1]),
 }
 
@@ -56,4 +64,4 @@ def synthetic_indices(rows, B: int, seed: int, dist: str = "uniform", device="cu
     return torch.stack(cols)
 
 
-__all__ = ["KAGGLE_ROWS", "TERABYTE_ROWS", "TERABYTE_X16_ROWS", "CONFIGS", "MLPS", "synthetic_indices"]
+__all__ = ["KAGGLE_ROWS", "TERABYTE_ROWS", "TERABYTE_X16_ROWS", "TERABYTE_1G_ROWS", "CONFIGS", "MLPS", "synthetic_indices"]

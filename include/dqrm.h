@@ -45,10 +45,12 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 5  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 6  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
-                               5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch) */
+                               5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
+                               6: residency-checked one launch (dqrm_bwd_apply_local_is_one_launch),
+                                  dqrm_checksum64 mixes the full 64-bit position */
 
 /* status codes */
 #define DQRM_OK            0
@@ -345,12 +347,21 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
  * quantize_emb_grad (s_q_g_p_c.py:850-869) + weight_update_parallel_comm (:601-628) at N=1,
  * the order grad_update_parallel_comm -> weight_update_parallel_comm runs them in
  * (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1895-1904). Other batches: the two calls.
- * DQRM_ERRF_STALL flags a launch whose workgroups could not all be resident. */
+ * The one launch needs its grid, (T+7)/8*64 workgroups of 1024 threads, resident at once:
+ * it is taken only when the current device's CUs x the occupancy query cover the grid and
+ * the stream's CU mask (hipExtStreamCreateWithCUMask) enables every CU; otherwise (a CPX
+ * partition, a masked stream) the two calls run. A workgroup that still waits too long (other
+ * streams' kernels holding CUs) does not update its rows and flags DQRM_ERRF_STALL: the update
+ * of that step is then incomplete, never computed from a partial table maximum. */
 int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                              int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
                              int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
                              float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
                              void* workspace, size_t workspace_bytes, void* stream);
+
+/* 1 if dqrm_emb_bwd_apply_local would run this batch as ONE launch on `stream` (the current
+ * device), 0 if as the two calls, <0 on bad arguments. */
+int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, void* stream);
 
 /* Which kernel dqrm_apply_sparse_update launches (process-wide; returns the previous
  * choice, or DQRM_E_INVALID). FLAT: one lane group per payload entry over the whole chip,
@@ -490,7 +501,7 @@ int dqrm_init_uniform(const dqrm_table_set* set, uint64_t seed, void* stream);
  * all_reduce(param, SUM) then param *= 1/N, every 200 iterations of the DP driver,
  * dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1801,1924-1936).
  * ------------------------------------------------------------------------------ */
-/* *out (device u64, caller-zeroed) += sum_i mix64(word_i | i << 32) over num_words 32-bit
+/* *out (device u64, caller-zeroed) += sum_i mix64(word_i ^ i * 0xD1B54A32D192ED03) over num_words 32-bit
  * words of data (16-B aligned): a position-dependent, order-free 64-bit checksum whose
  * all-gather tells whether every rank holds the same bits. */
 int dqrm_checksum64(const void* data, int64_t num_words, uint64_t* out, void* stream);

@@ -53,6 +53,12 @@ def test_pmc_traffic_lookup(bench, tmp_path):
     summ["kernels"]["k_coalesce_p1(CoalesceArgs)"] = {"avg_us": 23.6, "hbm_bytes_per_launch": 2.3e7}
     path.write_text(json.dumps(summ))  # the Criteo-form coalesce kernel is found first
     assert bench.pmc_traffic(str(path), "bwd_coalesce", 64)["bytes"] == 23_000_000
+    wl = {"config": "terabyte", "mode": "dp", "batch_per_gpu": 2048, "n1_update": "x", "index_dist": "uniform"}
+    assert bench.pmc_traffic(str(path), "bwd_coalesce", 64, wl) is None  # no workload recorded: refused
+    summ["workload"] = dict(wl)
+    path.write_text(json.dumps(summ))
+    assert bench.pmc_traffic(str(path), "bwd_coalesce", 64, wl)["bytes"] == 23_000_000
+    assert bench.pmc_traffic(str(path), "bwd_coalesce", 64, dict(wl, batch_per_gpu=128)) is None  # other batch
     for name in sorted(os.listdir(os.path.join(ROOT, "profiles"))):  # committed summaries parse
         if name.startswith("r2_") and name.endswith("_summary.json"):
             for ph in bench.KERNEL_SYMBOL:
@@ -130,3 +136,24 @@ def test_bench_rejects_inconsistent_flags():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--use-packed"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 2 and "--scale-period" in p.stderr
+
+
+def test_dlrm_net_shapes_cpu(bench):
+    """config 3's model (mode dlrm): the Kaggle MLPs, 26 pooled vectors and the dot
+    interaction's 351 pairs give the top MLP its 367 inputs; BCE backward reaches every
+    MLP parameter and the embedding tables' sparse grads."""
+    import torch
+
+    bot, top = bench.MLPS["kaggle"]
+    rows = [50 + 3 * t for t in range(26)]
+    emb = bench._RefEmb(rows, 16, torch.device("cpu"))
+    net = bench.DLRMNet(bot, top, emb, 0)
+    B = 8
+    X = torch.rand(B, 13)
+    P = torch.stack([torch.randint(0, n, (B,)) for n in rows])
+    p = net(X, P)
+    assert p.shape == (B, 1) and bool(((p > 0) & (p < 1)).all())
+    assert net.top_l[0].in_features == 367
+    torch.nn.BCELoss()(p, torch.ones(B, 1)).backward()
+    assert all(q.grad is not None for q in net.bot_l.parameters())
+    assert all(b.weight.grad is not None and b.weight.grad.is_sparse for b in emb.bags)

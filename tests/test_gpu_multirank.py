@@ -203,3 +203,81 @@ def test_weight_syncc_identical_replicas_local(tmp_path, world):
         assert moved > 0  # N = 3 moves about half of the elements by an ulp
     for r in range(world):
         assert bool(got[r]["hier_ok"])
+
+
+HOOK_ROWS, HOOK_D, HOOK_B = [7, 300, 5000, 40000], 16, 256
+
+
+def _hook_rank(rank, world, port, out_dir, veto_rank):
+    """The unchanged DP driver's pattern: a ModuleList of per-table QuantEmbeddingBagTwo
+    (grad_mode "dp") stepped through clear_gradients / backward / grad_update_parallel_comm /
+    weight_update_parallel_comm. veto_rank >= 0: that rank cannot consolidate its tables
+    (e.g. too little free memory), so NO rank may (the payload layouts must agree)."""
+    sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gen_inputs as G
+        from torch import nn
+        from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+        from deep_quantized_recommendation_model_dqrm_amd import sgd_quantized_gradients_parallel_comm as H
+        import deep_quantized_recommendation_model_dqrm_amd as dq
+
+        torch.cuda.set_device(0)
+        if rank == veto_rank:
+            H.can_consolidate = lambda mods: False  # this rank's memory check fails
+        Ws = G.table_weights(HOOK_ROWS, HOOK_D, 77)
+        model = nn.Module()
+        model.emb_l = nn.ModuleList([Q.QuantEmbeddingBagTwo(n, HOOK_D, 4, embedding_id=t, grad_mode="dp",
+                                                            weight=torch.from_numpy(Ws[t]))
+                                     for t, n in enumerate(HOOK_ROWS)])
+        model.bot_l, model.top_l = nn.ModuleList(), nn.ModuleList()
+        sl = dq.get_my_slice(HOOK_B, world, rank)
+        Bl = sl.stop - sl.start
+        off = torch.arange(Bl, dtype=torch.int64, device="cuda")
+        for k in range(2):
+            P = G.pooling_one(HOOK_ROWS, HOOK_B, 90 + k)
+            dy = G.upstream_grad(len(HOOK_ROWS), HOOK_B, HOOK_D, 95 + k)
+            H.clear_gradients(model)
+            ys = [model.emb_l[t](torch.from_numpy(np.ascontiguousarray(P[t, sl])).cuda(), off)
+                  for t in range(len(HOOK_ROWS))]
+            torch.autograd.backward(ys, [torch.from_numpy(np.ascontiguousarray(dy[t, sl])).cuda()
+                                         for t in range(len(HOOK_ROWS))])
+            H.grad_update_parallel_comm(model, world, True, 8)
+            H.weight_update_parallel_comm(model, 0.1, num_gpus=world)
+        torch.cuda.synchronize()
+        consolidated = model._dqrm_consolidated is not False
+        np.savez(os.path.join(out_dir, f"h{rank}.npz"), consolidated=np.array(consolidated),
+                 *[model.emb_l[t].embedding_bag.weight.detach().cpu().numpy() for t in range(len(HOOK_ROWS))])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("veto_rank", [-1, 1])
+def test_two_ranks_modulelist_hooks_consolidation_agreed(tmp_path, veto_rank):
+    """The DP hooks on a ModuleList at N=2: the tables are consolidated into one set only
+    when every rank can (an all-reduce MIN of each rank's check); either way both ranks end
+    bit-identical to oracle.dp_step over the global batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import gen_inputs as G
+    import oracle as O
+    from deep_quantized_recommendation_model_dqrm_amd import get_my_slice
+
+    world = 2
+    mp.spawn(_hook_rank, args=(world, _free_port(), str(tmp_path), veto_rank), nprocs=world, join=True)
+    Ws = G.table_weights(HOOK_ROWS, HOOK_D, 77)
+    sls = [get_my_slice(HOOK_B, world, r) for r in range(world)]
+    for k in range(2):
+        P = G.pooling_one(HOOK_ROWS, HOOK_B, 90 + k)
+        dy = G.upstream_grad(len(HOOK_ROWS), HOOK_B, HOOK_D, 95 + k)
+        s_fwd = [O.table_scale(w, 4) for w in Ws]
+        O.dp_step(Ws, [[(np.ascontiguousarray(P[t, sl]), np.arange(sl.stop - sl.start, dtype=np.int64))
+                        for t in range(len(HOOK_ROWS))] for sl in sls],
+                  [[np.ascontiguousarray(dy[t, sl]) for t in range(len(HOOK_ROWS))] for sl in sls], s_fwd, 0.1,
+                  grad_bits=8)
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, f"h{r}.npz"))
+        assert bool(got["consolidated"]) == (veto_rank < 0)
+        for t in range(len(HOOK_ROWS)):
+            np.testing.assert_array_equal(got[f"arr_{t}"], Ws[t])

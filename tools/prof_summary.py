@@ -58,8 +58,17 @@ def main(src: str, tag: str) -> None:
         v["fetch_size_bytes"] = fe
         v["write_size_bytes"] = wr
         v["hbm_bytes_per_launch"] = (2.0 * fe + wr) if fe is not None and wr is not None else None
+    # the profiled bench line's workload: bench.pmc_traffic only uses a summary of the same one
+    workload = None
+    try:
+        lines = [x for x in open(f"{src}_trace.log") if x.startswith("{")]
+        if lines:
+            roof = json.loads(lines[-1]).get("roofline") or {}
+            workload = roof.get("workload_profiled")
+    except (OSError, ValueError):
+        pass
     json.dump({"source": src, "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)",
-               "kernels": out}, open(f"{tag}_summary.json", "w"), indent=1)
+               "workload": workload, "kernels": out}, open(f"{tag}_summary.json", "w"), indent=1)
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
         hb = v["hbm_bytes_per_launch"]
         print(f"{k:32s} calls={v['calls']:4d} avg={v['avg_us']:10.2f} us  median={v.get('median_us', float('nan')):8.2f}"
