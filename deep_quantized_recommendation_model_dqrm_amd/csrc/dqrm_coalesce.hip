@@ -48,7 +48,7 @@ namespace {
 // workgroup stamps the 100 MHz wall clock at phase boundaries.
 #ifdef DQRM_DIAG_CLOCK
 __device__ unsigned long long g_coal_clk[8192 * 16];
-#define CDIAG(ph) do { if (threadIdx.x == 0) g_coal_clk[k * 16 + (ph)] = wall_clock64(); } while (0)
+#define CDIAG(ph) do { if (threadIdx.x == 0) g_coal_clk[kd * 16 + (ph)] = wall_clock64(); } while (0)
 #define CDIAG_W(ph) do { __builtin_amdgcn_s_waitcnt(0); CDIAG(ph); } while (0)
 #else
 #define CDIAG(k) do { } while (0)
@@ -383,13 +383,54 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
 }
 
 #ifndef DQRM_COAL_WPF
-#define DQRM_COAL_WPF 4
+#define DQRM_COAL_WPF 3
 #endif
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
 constexpr int WPFA = WPF > 0 ? WPF : 1;  // array extent (WPF = 0: no early W loads, an A/B build)
 constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
-constexpr int GRAN_WORD = 32;       // the table's 8 gradient-max granules {max bits, epoch} in its sync words
+constexpr int GRAN_WORD = 32;       // the table's 16 slot granules (8 slots x 2 sub-slots) in its sync words
+static_assert(GRAN_WORD + 2 * SPLIT * 2 <= DQRM_SYNC_STRIDE, "granules fit the table's sync words");
 constexpr uint32_t DIRTY_ONE = 1u << 16;  // arrival counter (sync word 0): arrivals | dirty arrivals << 16
+
+// Sub-slots (APPLY only). The grid has (T+7)/8*8 groups of 8 workgroups (one XCD each); group
+// g < T is table g's 8 row-range slots, and the spare groups g >= T each give one of the
+// largest row-split tables (>= 16 row blocks, ranked by row blocks, ties by index) a SECOND
+// workgroup per slot: slot s's blocks are halved, sub-slot 0 takes the lower half, the spare
+// group's workgroup s (sub-slot 1) the upper. The big tables' slots are bound by the bytes one
+// CU moves (dy rows in, W rows read and written), so halving them shortens the launch; the
+// workspace contract (DQRM_TABLE_SPLIT slots per table) is unchanged: after the rendezvous the
+// sub-slots' counts (carried in their granules) place sub-slot 1's rows after sub-slot 0's.
+// Every wave computes the plan alike from meta (lane = table): returns the eligible tables as
+// a lane mask and this lane's rank among them.
+__device__ __forceinline__ uint64_t sub_slot_rank(const int64_t* meta, int T, int& rank) {
+    const int lane = threadIdx.x % WAVE;
+    const int64_t n = lane < T ? meta[T + lane] : 0;
+    const int64_t nbl = (n + BLK - 1) / BLK;  // row blocks (the ranking key; ties by table index)
+    const int nb = nbl < 0x7fffffff ? (int)nbl : 0x7fffffff;
+    const bool elig = lane < T && nb >= 2 * SPLIT;
+    const uint64_t em = __ballot(elig);
+    int rk = 0;
+    for (int q = 0; q < T; ++q) {  // uniform
+        const int nq = __builtin_amdgcn_readlane(nb, q);
+        rk += ((em >> q) & 1ull) && (nq > nb || (nq == nb && q < lane)) ? 1 : 0;
+    }
+    rank = rk;
+    return em;
+}
+
+// granule of a slot: {max|grad| bits, distinct rows (13 bits), launch epoch (19 bits)}, one 8-B
+// sc1 store (data-tagged: no ordering needed for its contents)
+constexpr uint32_t GR_EPOCH_MASK = (1u << 19) - 1u;
+__device__ __forceinline__ uint32_t gr_epoch(uint64_t g) { return (uint32_t)(g >> 45); }
+__device__ __forceinline__ int gr_count(uint64_t g) { return (int)((g >> 32) & 0x1FFFu); }
+__device__ __forceinline__ uint64_t gr_make(float m, int count, uint32_t epoch) {
+    return (uint64_t)__float_as_uint(m) | ((uint64_t)((uint32_t)count & 0x1FFFu) << 32) |
+           ((uint64_t)(epoch & GR_EPOCH_MASK) << 45);
+}
+static_assert(MAXB < (1 << 13), "distinct-row count field of a granule");
+#ifndef DQRM_COAL_SUBSLOTS
+#define DQRM_COAL_SUBSLOTS 1  // 0: A/B build without sub-slots (the spare groups stay idle)
+#endif
 
 // APPLY (dqrm_emb_bwd_apply_local, world size 1): after the coalesce, the table's workgroups
 // meet once (each publishes its max|grad|, then waits for the table's others: all of them are
@@ -412,6 +453,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ float s_red[NW];
     __shared__ float s_am;
     __shared__ int s_stall;
+    __shared__ int s_upart;
     __shared__ int s_oq_n;
     __shared__ int s_dirty;
     __shared__ int s_fin;
@@ -428,9 +470,21 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // XCD-aware placement: blocks b and b + 8 share an XCD (and its L2), so table t's 8 slots
     // are blocks (t/8)*64 + s*8 + t%8. A dimension-split table's slots read 32-B slices of
     // the same dy lines; on one XCD a line is fetched from HBM once, not once per slot.
-    const int t = (int)(blockIdx.x >> 6) * 8 + (int)(blockIdx.x & 7), s = (int)(blockIdx.x >> 3) & 7;
-    if (t >= a.T) return;
+    const int grp = (int)(blockIdx.x >> 6) * 8 + (int)(blockIdx.x & 7), s = (int)(blockIdx.x >> 3) & 7;
+    const int nextra = APPLY && DQRM_COAL_SUBSLOTS ? (int)(gridDim.x / SPLIT) - a.T : 0;  // spare groups
+    int t = grp, j = 0;
+    if (grp >= a.T) {
+        if (nextra <= 0) return;
+        int rank;
+        const uint64_t em = sub_slot_rank(a.meta, a.T, rank);
+        const uint64_t hit = __ballot(((em >> (threadIdx.x % WAVE)) & 1ull) && rank == grp - a.T);
+        if (hit == 0) return;  // fewer eligible tables than spare groups
+        t = __ffsll((unsigned long long)hit) - 1;
+        j = 1;
+    }
     const int k = t * SPLIT + s;
+    const int kd = k + j * a.T * SPLIT;  // diagnostic stamp row (sub-slot 1 after all of sub-slot 0)
+    (void)kd;
     const int tid = threadIdx.x, w = tid / WAVE;
     // dy float4 prefetched per thread: 4 in the fused kernel (its update needs the registers;
     // a Criteo slot of <= 256 lookups x 16 float4 still lands in one round)
@@ -442,9 +496,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     //    clamped), so the compiler can count them and wait for exactly the one it needs.
     const int64_t nrows = a.meta[a.T + t];
     const float sc = a.scale[t];
-    int64_t cbv[SPLIT + 1];
-#pragma unroll
-    for (int j = 0; j <= SPLIT; ++j) cbv[j] = a.ws_cap_base[t * SPLIT + j];
+    // this slot's workspace region (scalar), and the table's slot bases (lane q < 9) for LDS
+    const int64_t cb_s = a.ws_cap_base[k], cb_e = a.ws_cap_base[k + 1];
+    const int64_t cbl = a.ws_cap_base[t * SPLIT + (tid <= SPLIT ? tid : SPLIT)];
     const int ni = (B + TPB - 1) / TPB;
     int64_t r[MAXI];
     const int64_t* ti = a.idx + (int64_t)t * a.B;
@@ -463,10 +517,22 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     const int SW = LG * 4;                   // dimensions this workgroup owns
     const int sw_sh = lg_sh + 2;
     const int q0 = dsplit ? s * LG : 0;
+    // sub-slots of this table's slots: 2 if a spare group serves it (see sub_slot_rank)
+    int K = j == 1 ? 2 : 1;
+    if (APPLY && j == 0 && nextra > 0 && !dsplit) {
+        int rank;
+        const uint64_t em = sub_slot_rank(a.meta, a.T, rank);
+        if (((em >> t) & 1ull) && __builtin_amdgcn_readlane(rank, t) < nextra) K = 2;
+    }
     int64_t r0 = 0, r1 = nrows;
     if (!dsplit) {
-        r0 = nblk * s / SPLIT * BLK;
-        r1 = nblk * (s + 1) / SPLIT * BLK;
+        int64_t b0 = nblk * s / SPLIT, b1 = nblk * (s + 1) / SPLIT;
+        if (K == 2) {  // halves of the slot's blocks: sub-slot 0 the lower, 1 the upper
+            const int64_t bm = (b0 + b1) / 2;
+            if (j == 0) b1 = bm; else b0 = bm;
+        }
+        r0 = b0 * BLK;
+        r1 = b1 * BLK;
         r1 = r1 < nrows ? r1 : nrows;
     }
     const bool active = dsplit ? s < DS : r0 < r1;
@@ -478,7 +544,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     uint64_t* gran = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + GRAN_WORD);
     uint32_t epoch = 0;
     if (APPLY && tid < WAVE)
-        epoch = (uint32_t)(__hip_atomic_load(gran + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 32) + 1u;
+        epoch = (gr_epoch(__hip_atomic_load(gran + s + SPLIT * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u) &
+                GR_EPOCH_MASK;
     auto fetch = [&](int b, int sub) -> float4 {
         return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
     };
@@ -510,10 +577,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             pf[f] = *src;
         }
     }
-    if (tid == 0) {
-#pragma unroll
-        for (int j = 0; j <= SPLIT; ++j) s_cb[j] = cbv[j];
-    }
+    if (tid <= SPLIT) s_cb[tid] = cbl;
     if (tid < SPLIT) s_ucnt[tid] = 0;
 #pragma unroll
     for (int i = 0; i < MAXI; ++i)
@@ -555,7 +619,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         },
         none);
     CDIAG(9);
-    if (dsplit ? s == 0 : s == SPLIT - 1) {  // out-of-range indices: flagged once per table
+    if (j == 0 && (dsplit ? s == 0 : s == SPLIT - 1)) {  // out-of-range indices: flagged once per table
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < MAXI; ++i)
@@ -575,7 +639,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         }
     }
     CDIAG(2);
-    const int64_t cb_s = cbv[s < SPLIT ? s : 0];
     uint64_t* tmp = reinterpret_cast<uint64_t*>(lds + OFF_SCR);
     int U, NS, M;
     bool counted = false;
@@ -713,7 +776,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                         const int rs = (int)(nblk * sl / SPLIT * BLK);
                         e = (int)(s_cb[sl] + (u - (info[rs] >> 16)));
                     } else {
-                        e = (int)(cb_s + u);
+                        e = (int)((j ? cb_e - (ta >> 16) : cb_s) + u);
                     }
                 }
                 sdest[p] = e;
@@ -800,7 +863,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                     if (dsplit) atomicAdd(&s_ucnt[slot_of_row(krow(keys[p]), nblk)], 1);
                 }
                 const int u = h ? rh : rh - 1;
-                sdest[p] = sg ? (dsplit ? u : (int)(cb_s + u)) : -(p - rs) - 1;
+                sdest[p] = sg ? (dsplit ? u : (int)((j ? cb_e - U : cb_s) + u)) : -(p - rs) - 1;
             }
         }
     }
@@ -835,7 +898,12 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // split table: its rows in that range; a row split: all of the slot's), entry s_cb[sl] +
     // (u - ua). Workgroup s updates slots s, s + NA, ... (NA = the table's active workgroups).
     const int NA = dsplit ? DS : SPLIT;
+    const int NG = NA * K;  // the table's workgroups (granules)
     const int lpr_sh = __ffs(LPR) - 1;
+    // this workgroup's entries in its slot's workspace region: sub-slot 0 (or a whole slot) from
+    // its start, sub-slot 1 packed at its end (its values are scratch; its rows are written at
+    // their final place, after sub-slot 0's, once the rendezvous has told it sub-slot 0's count)
+    const int64_t ebase = j ? s_cb[s + 1] - U : s_cb[s];
     auto slot_entries = [&](int sl, int& ua, int& nu) {
         ua = dsplit ? s_uf[sl] : 0;
         nu = dsplit ? s_uf[sl + 1] - ua : U;
@@ -880,7 +948,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
         const int64_t row = r0 + krow(keys[hpos[u]]);
         int sl = s;
-        int64_t e = s_cb[s] + u;
+        int64_t e = ebase + u;
         if (dsplit) {
             sl = slot_of_row(row, nblk);
             e = s_cb[sl] + (u - s_uf[sl]);
@@ -889,7 +957,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             if (lds_vals) stage[d * SP + vb0 + u] = acc;
             else if (APPLY && dsplit) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
             else a.ws_vals[e * a.D + q0 * 4 + d] = acc;
-            if (q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
+            if (j == 0 && q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
         }
         amax = fmaxf(amax, fabsf(acc));
     };
@@ -912,13 +980,13 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
             if (lds_vals) {
-                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - cb_s), v);
+                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - ebase), v);
             } else {
                 float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
                 if (APPLY && dsplit) st4_wt(dst, v);
                 else *dst = v;
             }
-            if (q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
+            if (j == 0 && q0 == 0 && (q & (LG - 1)) == 0) a.ws_rows[e] = (int32_t)(r0 + krow(keys[pos[q >> lg_sh]]));
             amax = fmaxf(amax, abs_max4(v));
         };
         int q = tid;
@@ -999,21 +1067,21 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if (tid == 0) {
         float m = 0.0f;
         for (int q = 0; q < NW; ++q) m = fmaxf(m, s_red[q]);
-        a.ws_absmax[k] = m;
-        // publish this slot's max|grad| as ONE 8-B sc1 store of {max bits, epoch} (a data-
-        // tagged granule: no counter, no ordering needed for the value itself)
+        if (K == 1) a.ws_absmax[k] = m;  // sub-slots: sub-slot 0 writes the slot's, after the rendezvous
+        // publish this slot's max|grad| (and distinct rows) as ONE 8-B sc1 store (a data-tagged
+        // granule: no counter, no ordering needed for the value itself)
         if constexpr (APPLY)
-            __hip_atomic_store(gran + s, ((uint64_t)epoch << 32) | __float_as_uint(m), __ATOMIC_RELAXED,
+            __hip_atomic_store(gran + s + SPLIT * j, gr_make(m, dsplit ? 0 : U, epoch), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     if (APPLY && tid < WAVE) {  // wave 0: lane j polls slot j's granule until it shows this launch's epoch
         uint64_t g = 0;
-        bool ok = tid >= NA;
+        bool ok = tid >= NG;
         bool stalled = false;
         for (int spin = 0;; ++spin) {
             if (!ok) {
                 g = __hip_atomic_load(gran + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = (uint32_t)(g >> 32) == epoch;
+                ok = gr_epoch(g) == epoch;
             }
             if (__all(ok)) break;
             // the table's workgroups were not all resident (the host checks the device's CUs,
@@ -1027,13 +1095,32 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        const float am = wave_max(tid < NA ? __uint_as_float((uint32_t)g) : 0.0f);
+        const float am = wave_max(tid < NG ? __uint_as_float((uint32_t)g) : 0.0f);
+        if (K == 2) {  // the partner sub-slot's count and maximum (uniform: readlane)
+            const int p = j ? s : SPLIT + s;
+            const int upart = __builtin_amdgcn_readlane(gr_count(g), p);
+            const float mself = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, s + SPLIT * j));
+            const float mpart = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, p));
+            if (tid == 0) {
+                s_upart = upart;
+                if (j == 0) {  // the slot's count and partial maximum, as one workgroup would write them
+                    int c = U + upart;
+                    const int64_t cap = s_cb[s + 1] - s_cb[s];
+                    if (c > cap) {
+                        atomicOr(a.err, DQRM_ERRF_OVERFLOW);
+                        c = (int)cap;
+                    }
+                    a.ws_ucount[k] = c;
+                    a.ws_absmax[k] = fmaxf(mself, mpart);
+                }
+            }
+        }
         if (tid == 0) {
             s_am = am;
             s_stall = stalled ? 1 : 0;
         }
     }
-    if (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT)) {
+    if (K == 1 && (!dsplit ? tid == 0 : (s == 0 && tid < SPLIT))) {
         const int sl = dsplit ? tid : s;
         int c = dsplit ? s_ucnt[sl] : U;
         const int64_t cap = s_cb[sl + 1] - s_cb[sl];
@@ -1051,7 +1138,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
         const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
         const bool go = s_stall == 0;  // a stalled workgroup leaves its rows as they were
-        if (go && s == 0 && tid == 0) la.s_avg[t] = sv;
+        if (go && s == 0 && j == 0 && tid == 0) la.s_avg[t] = sv;
+        if (j == 1) {  // sub-slot 1's rows, at their place after sub-slot 0's entries
+            const int nr = U < (int)(s_cb[s + 1] - s_cb[s]) - s_upart ? U : (int)(s_cb[s + 1] - s_cb[s]) - s_upart;
+            for (int u = tid; u < nr; u += TPB) a.ws_rows[s_cb[s] + s_upart + u] = (int32_t)(r0 + krow(keys[hpos[u]]));
+        }
         const float rr = 1.0f / sv;
         const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
@@ -1122,7 +1213,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             int ua, nu;
             slot_entries(sl, ua, nu);
             const int nit = nu << lpr_sh;
-            const float* vb = a.ws_vals + s_cb[sl] * a.D;  // the slot's entries, D floats each
+            const float* vb = a.ws_vals + (dsplit ? s_cb[sl] : ebase) * a.D;  // the entries, D floats each
             int q = tid;
             if (j0 == 0) {  // the prefetched rows: value loads two at a time in flight, then the updates
 #pragma unroll
@@ -1210,7 +1301,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             uint32_t* cnt = la.sync + (int64_t)t * DQRM_SYNC_STRIDE;
             const uint32_t add = 1u + (s_dirty ? DIRTY_ONE : 0u);
             const uint32_t now = atomicAdd(cnt, add) + add;
-            const bool last = (now & (DIRTY_ONE - 1u)) == (uint32_t)NA;
+            const bool last = (now & (DIRTY_ONE - 1u)) == (uint32_t)NG;
             if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_fin = last && (now >> 16) != 0u;
         }

@@ -1,6 +1,7 @@
 """Per-phase wall-clock breakdown of the Criteo-form coalesce kernel (k_coalesce_p1) on the
 diagnostic build (tools/build_diag_coal.sh). Stamps: 0 start, 1 indices landed, 2 slot
-compacted, 3 sorted, 4 heads, 5 stage landed, 6 segments done (stores issued), 7 end; with
+compacted, 3 sorted, 4 heads, 5 stage landed, 6 segments done (stores issued), 7 end (a
+table's slowest workgroup over its slots and, in the one-launch step, sub-slots); with
 "apply" (the one-launch local step, dqrm_emb_bwd_apply_local): 11 the table's workgroups
 met, 12 rows updated, 13 end (after the table's last-workgroup finalize).
 usage: python tools/diag_coalesce.py [terabyte|terabyte_ref|kaggle] [B] [apply]"""
@@ -50,10 +51,12 @@ for i in range(3 * NB):
 torch.cuda.synchronize()
 cs = []
 for i in range(NB):  # one launch per batch, read after each
-    buf = np.zeros(T * 8 * 16, dtype=np.uint64)
+    buf = np.zeros(2 * T * 8 * 16, dtype=np.uint64)
     run(i)
     lib.dqrm_diag_coal_read(buf.ctypes.data, buf.size)
-    c = buf.reshape(T, 8, 16).astype(np.int64)
+    # rows: sub-slot 0 of every (table, slot), then sub-slot 1 (the spare groups of the
+    # one-launch step); per table 16 "slots": 0-7 sub-slot 0, 8-15 sub-slot 1
+    c = buf.reshape(2, T, 8, 16).transpose(1, 0, 2, 3).reshape(T, 16, 16).astype(np.int64)
     k0 = c[:, :, 0][c[:, :, 0] > 0].min()
     c = np.where(c >= k0, c - k0, -1)  # -1: not stamped in this launch
     cs.append(c)
@@ -78,7 +81,7 @@ for t in order:
     print(f"t{t:2d} n={rows[t]:>10d}: " + " ".join(f"{x / 100:5.1f}" for x in ph)
           + f" || {np.median([p[7] for p in ps]) / 100:5.1f}")
 sub = [(c[t, s, 8] - c[t, s, 1], c[t, s, 9] - c[t, s, 8], c[t, s, 10] - c[t, s, 9], c[t, s, 2] - c[t, s, 10])
-       for c in cs for t in range(T) for s in range(8) if c[t, s, 2] >= 0 and c[t, s, 10] >= 0]
+       for c in cs for t in range(T) for s in range(16) if c[t, s, 2] >= 0 and c[t, s, 10] >= 0]
 sub = np.array(sub) / 100
 print("compact split (median us): idx-wait %.2f  compaction %.2f  report+barrier %.2f  prefetch-issue %.2f" %
       tuple(np.median(sub, axis=0)))
