@@ -120,6 +120,7 @@ class TableSet(C.Structure):
         ("sdirty", C.c_void_p),
         ("bdirty", C.c_void_p),
         ("sync", C.c_void_p),
+        ("num_rows_host", C.c_void_p),  # host int64 [T] (launch planning), nullable
     ]
 
 

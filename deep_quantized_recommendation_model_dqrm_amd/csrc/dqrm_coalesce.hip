@@ -34,7 +34,9 @@
 // dimension-split table come from one L2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <stdint.h>
 
@@ -394,29 +396,13 @@ constexpr uint32_t DIRTY_ONE = 1u << 16;  // arrival counter (sync word 0): arri
 
 // Sub-slots (APPLY only). The grid has (T+7)/8*8 groups of 8 workgroups (one XCD each); group
 // g < T is table g's 8 row-range slots, and the spare groups g >= T each give one of the
-// largest row-split tables (>= 16 row blocks, ranked by row blocks, ties by index) a SECOND
-// workgroup per slot: slot s's blocks are halved, sub-slot 0 takes the lower half, the spare
-// group's workgroup s (sub-slot 1) the upper. The big tables' slots are bound by the bytes one
-// CU moves (dy rows in, W rows read and written), so halving them shortens the launch; the
-// workspace contract (DQRM_TABLE_SPLIT slots per table) is unchanged: after the rendezvous the
-// sub-slots' counts (carried in their granules) place sub-slot 1's rows after sub-slot 0's.
-// Every wave computes the plan alike from meta (lane = table): returns the eligible tables as
-// a lane mask and this lane's rank among them.
-__device__ __forceinline__ uint64_t sub_slot_rank(const int64_t* meta, int T, int& rank) {
-    const int lane = threadIdx.x % WAVE;
-    const int64_t n = lane < T ? meta[T + lane] : 0;
-    const int64_t nbl = (n + BLK - 1) / BLK;  // row blocks (the ranking key; ties by table index)
-    const int nb = nbl < 0x7fffffff ? (int)nbl : 0x7fffffff;
-    const bool elig = lane < T && nb >= 2 * SPLIT;
-    const uint64_t em = __ballot(elig);
-    int rk = 0;
-    for (int q = 0; q < T; ++q) {  // uniform
-        const int nq = __builtin_amdgcn_readlane(nb, q);
-        rk += ((em >> q) & 1ull) && (nq > nb || (nq == nb && q < lane)) ? 1 : 0;
-    }
-    rank = rk;
-    return em;
-}
+// largest row-split tables a SECOND workgroup per slot (la.sub_table / la.sub_mask, planned on
+// the host from the tables' row counts: >= 16 row blocks, by row blocks, ties by index):
+// slot s's blocks are halved, sub-slot 0 takes the lower half, the spare group's workgroup s
+// (sub-slot 1) the upper. The big tables' slots are bound by the bytes one CU moves (dy rows
+// in, W rows read and written), so halving them shortens the launch; the workspace contract
+// (DQRM_TABLE_SPLIT slots per table) is unchanged: after the rendezvous the sub-slots' counts
+// (carried in their granules) place sub-slot 1's rows after sub-slot 0's.
 
 // granule of a slot: {max|grad| bits, distinct rows (13 bits), launch epoch (19 bits)}, one 8-B
 // sc1 store (data-tagged: no ordering needed for its contents)
@@ -428,9 +414,7 @@ __device__ __forceinline__ uint64_t gr_make(float m, int count, uint32_t epoch) 
            ((uint64_t)(epoch & GR_EPOCH_MASK) << 45);
 }
 static_assert(MAXB < (1 << 13), "distinct-row count field of a granule");
-#ifndef DQRM_COAL_SUBSLOTS
-#define DQRM_COAL_SUBSLOTS 1  // 0: A/B build without sub-slots (the spare groups stay idle)
-#endif
+
 
 // APPLY (dqrm_emb_bwd_apply_local, world size 1): after the coalesce, the table's workgroups
 // meet once (each publishes its max|grad|, then waits for the table's others: all of them are
@@ -471,15 +455,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // are blocks (t/8)*64 + s*8 + t%8. A dimension-split table's slots read 32-B slices of
     // the same dy lines; on one XCD a line is fetched from HBM once, not once per slot.
     const int grp = (int)(blockIdx.x >> 6) * 8 + (int)(blockIdx.x & 7), s = (int)(blockIdx.x >> 3) & 7;
-    const int nextra = APPLY && DQRM_COAL_SUBSLOTS ? (int)(gridDim.x / SPLIT) - a.T : 0;  // spare groups
     int t = grp, j = 0;
-    if (grp >= a.T) {
-        if (nextra <= 0) return;
-        int rank;
-        const uint64_t em = sub_slot_rank(a.meta, a.T, rank);
-        const uint64_t hit = __ballot(((em >> (threadIdx.x % WAVE)) & 1ull) && rank == grp - a.T);
-        if (hit == 0) return;  // fewer eligible tables than spare groups
-        t = __ffsll((unsigned long long)hit) - 1;
+    if (grp >= a.T) {  // a spare group: sub-slot 1 of a big table's slots, or idle
+        const int e = grp - a.T;
+        if (!APPLY || e >= dqrm_internal::kSubTables || la.sub_table[e] < 0) return;
+        t = la.sub_table[e];
         j = 1;
     }
     const int k = t * SPLIT + s;
@@ -517,13 +497,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     const int SW = LG * 4;                   // dimensions this workgroup owns
     const int sw_sh = lg_sh + 2;
     const int q0 = dsplit ? s * LG : 0;
-    // sub-slots of this table's slots: 2 if a spare group serves it (see sub_slot_rank)
-    int K = j == 1 ? 2 : 1;
-    if (APPLY && j == 0 && nextra > 0 && !dsplit) {
-        int rank;
-        const uint64_t em = sub_slot_rank(a.meta, a.T, rank);
-        if (((em >> t) & 1ull) && __builtin_amdgcn_readlane(rank, t) < nextra) K = 2;
-    }
+    // sub-slots of this table's slots: 2 if a spare group serves it
+    const int K = (j == 1 || (APPLY && !dsplit && ((la.sub_mask >> t) & 1u))) ? 2 : 1;
     int64_t r0 = 0, r1 = nrows;
     if (!dsplit) {
         int64_t b0 = nblk * s / SPLIT, b1 = nblk * (s + 1) / SPLIT;
@@ -903,7 +878,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // this workgroup's entries in its slot's workspace region: sub-slot 0 (or a whole slot) from
     // its start, sub-slot 1 packed at its end (its values are scratch; its rows are written at
     // their final place, after sub-slot 0's, once the rendezvous has told it sub-slot 0's count)
-    const int64_t ebase = j ? s_cb[s + 1] - U : s_cb[s];
+    auto ebase = [&]() -> int64_t { return j ? s_cb[s + 1] - U : s_cb[s]; };  // (LDS reads, not a live register)
     auto slot_entries = [&](int sl, int& ua, int& nu) {
         ua = dsplit ? s_uf[sl] : 0;
         nu = dsplit ? s_uf[sl + 1] - ua : U;
@@ -948,7 +923,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
         const int64_t row = r0 + krow(keys[hpos[u]]);
         int sl = s;
-        int64_t e = ebase + u;
+        int64_t e = ebase() + u;
         if (dsplit) {
             sl = slot_of_row(row, nblk);
             e = s_cb[sl] + (u - s_uf[sl]);
@@ -980,7 +955,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
             if (lds_vals) {
-                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - ebase), v);
+                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - ebase()), v);
             } else {
                 float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
                 if (APPLY && dsplit) st4_wt(dst, v);
@@ -1139,10 +1114,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
         const bool go = s_stall == 0;  // a stalled workgroup leaves its rows as they were
         if (go && s == 0 && j == 0 && tid == 0) la.s_avg[t] = sv;
-        if (j == 1) {  // sub-slot 1's rows, at their place after sub-slot 0's entries
-            const int nr = U < (int)(s_cb[s + 1] - s_cb[s]) - s_upart ? U : (int)(s_cb[s + 1] - s_cb[s]) - s_upart;
-            for (int u = tid; u < nr; u += TPB) a.ws_rows[s_cb[s] + s_upart + u] = (int32_t)(r0 + krow(keys[hpos[u]]));
-        }
         const float rr = 1.0f / sv;
         const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
@@ -1213,7 +1184,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             int ua, nu;
             slot_entries(sl, ua, nu);
             const int nit = nu << lpr_sh;
-            const float* vb = a.ws_vals + (dsplit ? s_cb[sl] : ebase) * a.D;  // the entries, D floats each
+            const float* vb = a.ws_vals + (dsplit ? s_cb[sl] : ebase()) * a.D;  // the entries, D floats each
             int q = tid;
             if (j0 == 0) {  // the prefetched rows: value loads two at a time in flight, then the updates
 #pragma unroll
@@ -1289,6 +1260,10 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             }
         }
         if (dirty) s_dirty = 1;
+        if (j == 1) {  // sub-slot 1's rows, at their place after sub-slot 0's entries
+            const int nr = U < (int)(s_cb[s + 1] - s_cb[s]) - s_upart ? U : (int)(s_cb[s + 1] - s_cb[s]) - s_upart;
+            for (int u = tid; u < nr; u += TPB) a.ws_rows[s_cb[s] + s_upart + u] = (int32_t)(r0 + krow(keys[hpos[u]]));
+        }
         CDIAG(12);
         // one arrival per workgroup after all its stores landed, carrying whether it flagged
         // a superblock (hand-off row 1 of MI355X_MICROARCH.md: sc1 stores / atomics, vmcnt(0),
@@ -1334,6 +1309,31 @@ hipError_t allow_coalesce_lds() {
 namespace dqrm_internal {
 
 int coalesce_apply_grid(int T) { return (T + 7) / 8 * 64; }
+
+void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la) {
+    static const bool off = [] {
+        const char* e = getenv("DQRM_SUBSLOTS");
+        return e && !strcmp(e, "0");
+    }();
+    la->sub_mask = 0;
+    for (int e = 0; e < kSubTables; ++e) la->sub_table[e] = -1;
+    if (off || !num_rows_host || T <= 0 || T > kCoalesceApplyMaxT) return;
+    const int nextra = coalesce_apply_grid(T) / SPLIT - T;  // spare groups of 8 workgroups
+    // eligible: row-split tables of >= 16 row blocks (each half-slot keeps >= 1 block), by row
+    // blocks descending, ties by table index
+    int order[kCoalesceApplyMaxT];
+    int64_t nb[kCoalesceApplyMaxT];
+    int ne = 0;
+    for (int t = 0; t < T; ++t) {
+        nb[t] = (num_rows_host[t] + BLK - 1) / BLK;
+        if (nb[t] >= 2 * SPLIT) order[ne++] = t;
+    }
+    std::stable_sort(order, order + ne, [&](int x, int y) { return nb[x] > nb[y]; });
+    for (int e = 0; e < nextra && e < ne && e < kSubTables; ++e) {
+        la->sub_table[e] = (int8_t)order[e];
+        la->sub_mask |= 1u << order[e];
+    }
+}
 
 bool coalesce_apply_resident(int T, hipStream_t stream) {
     if (T <= 0 || T > kCoalesceApplyMaxT) return false;

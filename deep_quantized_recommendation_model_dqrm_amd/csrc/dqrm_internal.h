@@ -46,7 +46,12 @@ struct LocalApplyArgs {
     int bits;
     float nlr;                  // -lr
     int repack;
+    // sub-slots (host-planned, dqrm_coalesce.hip): spare group e serves table sub_table[e]
+    // (-1: idle); bit t of sub_mask = table t's slots are halved between two workgroups
+    uint32_t sub_mask;
+    int8_t sub_table[32];
 };
+constexpr int kSubTables = 32;  // LocalApplyArgs::sub_table entries
 
 // largest B the Criteo-form coalesce kernel takes (larger batches use the general kernel)
 constexpr int64_t kCoalesceMaxB = 4096;
@@ -59,6 +64,10 @@ constexpr int kCoalesceApplyMaxT = 32;
 // from `stream`: workgroups per CU (occupancy query) x CUs >= the grid, and the stream's CU
 // mask enables every CU. Device properties are queried once per device.
 bool coalesce_apply_resident(int T, hipStream_t stream);
+
+// Sub-slot plan of the fused form (la->sub_mask / sub_table) from the host row counts
+// (nullable: no sub-slots). DQRM_SUBSLOTS=0 in the environment disables them (A/B).
+void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la);
 
 // launches k_coalesce_p1 (dqrm_coalesce.hip); la != nullptr: the fused update as well
 // (hipErrorInvalidValue if !coalesce_apply_resident). Returns the HIP error of the launch.

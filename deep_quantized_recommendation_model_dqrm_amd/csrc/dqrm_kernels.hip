@@ -4203,6 +4203,7 @@ int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch,
         la.sblkmax = set->sblkmax; la.sdirty = set->sdirty; la.bdirty = set->bdirty; la.tmax = set->tmax;
         la.pscale = set->pscale; la.sync = set->sync; la.s_avg = s_avg; la.bits = grad_bits; la.nlr = -lr;
         la.repack = repack_bits == 4;
+        dqrm_internal::plan_sub_slots(set->num_rows_host, set->num_tables, &la);
         const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, &la, (hipStream_t)stream);
         if (e != hipSuccess)
             return set_error(DQRM_E_HIP, "dqrm_emb_bwd_apply_local: launch failed: %s (%d)", hipGetErrorString(e), (int)e);

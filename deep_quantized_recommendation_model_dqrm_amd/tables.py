@@ -220,11 +220,13 @@ class EmbeddingTableSet:
         self._err_host: torch.Tensor | None = None  # pinned snapshot of the error word (poll_errors)
         self._err_evt = None
         self._err_pending = False
+        self._rows_host = (C.c_int64 * T)(*self.num_rows)  # kept alive with the struct
         self._c = L.TableSet(
             T, D, self.R, NB, NS,
             _ptr(self.W), _ptr(self.packed), _ptr(self.rowmax), _ptr(self.blkmax), _ptr(self.sblkmax),
             _ptr(self.tmax), _ptr(self.scale), _ptr(self.pscale), _ptr(self.meta), _ptr(self.err),
             _ptr(self.tflags), _ptr(self.sdirty), _ptr(self.bdirty), _ptr(self.sync),
+            C.addressof(self._rows_host),
         )
         if weights is not None:
             if len(weights) != T:
@@ -269,11 +271,13 @@ class EmbeddingTableSet:
         v.bdirty = self.bdirty[bb:]
         v.sync = self.sync[t * L.DQRM_SYNC_STRIDE: (t + 1) * L.DQRM_SYNC_STRIDE]
         v._bws, v._err_host, v._err_evt, v._err_pending = None, None, None, False
+        v._rows_host = (C.c_int64 * 1)(n)
         v._c = L.TableSet(
             1, self.D, n, nb, ns,
             _ptr(v.W), _ptr(v.packed), _ptr(v.rowmax), _ptr(v.blkmax), _ptr(v.sblkmax),
             _ptr(v.tmax), _ptr(v.scale), _ptr(v.pscale), _ptr(v.meta), _ptr(v.err),
             _ptr(v.tflags), _ptr(v.sdirty), _ptr(v.bdirty), _ptr(v.sync),
+            C.addressof(v._rows_host),
         )
         return v
 

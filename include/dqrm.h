@@ -50,7 +50,8 @@ extern "C" {
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
                                6: residency-checked one launch (dqrm_bwd_apply_local_is_one_launch),
-                                  dqrm_checksum64 mixes the full 64-bit position */
+                                  dqrm_checksum64 mixes the full 64-bit position,
+                                  dqrm_table_set.num_rows_host */
 
 /* status codes */
 #define DQRM_OK            0
@@ -99,6 +100,9 @@ typedef struct dqrm_table_set {
                                  arrival counters of the updating kernels (the last workgroup
                                  of a table finalizes its |W| hierarchy inside the launch), one
                                  per 256 bytes; library-internal */
+    const int64_t* num_rows_host; /* nullable HOST array [T]: the tables' row counts (meta's
+                                 second row), for host-side launch planning (the one-launch local
+                                 step gives its spare workgroups to the largest tables) */
 } dqrm_table_set;
 
 /* A batch of lookups for all T tables, in the reference's per-table

@@ -41,8 +41,8 @@ def test_payload_bytes_agree(lib):
 
 
 def test_struct_layouts():
-    # dqrm_table_set: 2 x i32 + 3 x i64 + 14 pointers; dqrm_batch: 3 pointers + 2 x i64
-    assert C.sizeof(L.TableSet) == 8 + 24 + 14 * 8
+    # dqrm_table_set: 2 x i32 + 3 x i64 + 15 pointers (the last a host array); dqrm_batch: 3 pointers + 2 x i64
+    assert C.sizeof(L.TableSet) == 8 + 24 + 15 * 8
     assert C.sizeof(L.Batch) == 6 * 8
 
 
