@@ -385,11 +385,17 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
 }
 
 #ifndef DQRM_COAL_WPF
-#define DQRM_COAL_WPF 3
+#define DQRM_COAL_WPF 4
+#endif
+#ifndef DQRM_COAL_WLATE
+#define DQRM_COAL_WLATE 1
 #endif
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
 constexpr int WPFA = WPF > 0 ? WPF : 1;  // array extent (WPF = 0: no early W loads, an A/B build)
 constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
+constexpr int SBC = 256;            // fused update: superblock maxima of the slot's rows cached in LDS
+constexpr int CAND_SLOTS = 2 * (MAXB * 2) / (BLK * 4);  // row-max caches of candidate blocks (pos + mlist regions)
+static_assert(CAND_SLOTS == 16 && CAND_SLOTS <= NW, "one candidate-block cache per wave");
 constexpr int GRAN_WORD = 32;       // the table's 16 slot granules (8 slots x 2 sub-slots) in its sync words
 static_assert(GRAN_WORD + 2 * SPLIT * 2 <= DQRM_SYNC_STRIDE, "granules fit the table's sync words");
 constexpr uint32_t DIRTY_ONE = 1u << 16;  // arrival counter (sync word 0): arrivals | dirty arrivals << 16
@@ -438,6 +444,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ float s_am;
     __shared__ int s_stall;
     __shared__ int s_upart;
+    __shared__ float s_sbm[SBC];            // fused update: sblkmax of the slot's superblocks
+    __shared__ int s_cand_blk[CAND_SLOTS];  // fused update: block cached by wave w's row-max slot (-1: none)
     __shared__ int s_oq_n;
     __shared__ int s_dirty;
     __shared__ int s_fin;
@@ -904,21 +912,36 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             s_oq_n = 0;
             s_dirty = 0;
         }
-        // the W rows and block maxima of the entries this workgroup will update, in flight
-        // across the segment phase and the wait for the table's other workgroups
-#pragma unroll
-        for (int j = 0; j < WPF; ++j) {
-            const int q = tid + TPB * j;
-            wpf[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            bpf[j] = 0.0f;
-            if (q < (nu0 << lpr_sh)) {
-                const int64_t x = r0 + krow(keys[hpos[ua0 + (q >> lpr_sh)]]);
-                wpf[j] = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
-                bpf[j] = la.blkmax[bb + (x >> 8)];
-            }
-        }
         otm = la.tmax[t];
     }
+    // the W rows and block maxima of the entries this workgroup will update, in flight across
+    // the segment phase and the wait for the table's other workgroups: issued once the dy
+    // prefetch registers are free (DQRM_COAL_WLATE, the default: the two register sets are
+    // never live together), or before the land phase
+    auto issue_w = [&]() {
+        if constexpr (APPLY) {
+#pragma unroll
+            for (int jj = 0; jj < WPF; ++jj) {
+                const int q = tid + TPB * jj;
+                wpf[jj] = make_float4(0.f, 0.f, 0.f, 0.f);
+                bpf[jj] = 0.0f;
+                if (q < (nu0 << lpr_sh)) {
+                    const int64_t x = r0 + krow(keys[hpos[ua0 + (q >> lpr_sh)]]);
+                    wpf[jj] = reinterpret_cast<const float4*>(la.W + (rb + x) * a.D)[q & (LPR - 1)];
+                    bpf[jj] = la.blkmax[bb + (x >> 8)];
+                }
+            }
+        }
+    };
+    // the superblock maxima of the slot's rows (a row-split slot spans a few hundred at most),
+    // read by the update's growth / holder checks from LDS instead of a dependent HBM load each.
+    // Read before the update: a stale-low value (another slot's growth) only costs a redundant
+    // atomicMax or superblock re-reduction, never a wrong maximum.
+    const int64_t sb0 = r0 >> 16;
+    const int nsbc = APPLY && !dsplit && r1 > r0 && ((r1 - 1) >> 16) - sb0 < SBC ? (int)(((r1 - 1) >> 16) - sb0 + 1) : 0;
+    float sbv = 0.0f;
+    if (APPLY && tid < nsbc) sbv = la.sblkmax[sbb + sb0 + tid];
+    if (!DQRM_COAL_WLATE || n - NS > CE) issue_w();
     float amax = 0.0f;
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d
         const int64_t row = r0 + krow(keys[hpos[u]]);
@@ -979,6 +1002,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             for (int f = 0; f < PF; ++f) store(q + TPB * f, de[f], pf[f]);
             q += TPB * PF;
         }
+        if (DQRM_COAL_WLATE) issue_w();
         for (; q < nitems; q += TPB) {  // beyond the register budget (or no prefetch)
             const int p = pos[q >> lg_sh];
             if (p == 0xFFFF) continue;
@@ -1048,6 +1072,47 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         if constexpr (APPLY)
             __hip_atomic_store(gran + s + SPLIT * j, gr_make(m, dsplit ? 0 : U, epoch), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if constexpr (APPLY) {
+        if (tid < nsbc) s_sbm[tid] = sbv;
+        // While wave 0 waits for the table's other workgroups, every other wave looks for a block
+        // whose row-max holder is one of its (prefetched) rows -- the blocks the update may have
+        // to re-reduce -- and copies the first such block's 256 stored row maxima into its LDS
+        // cache (the pos / mlist regions, dead by now). Rows of a block are updated only by this
+        // workgroup, so the copy stays exact for the untouched rows.
+        if (!dsplit && w > 0) {
+            int cb = -1;
+#pragma unroll
+            for (int jj = 0; jj < WPF; ++jj) {
+                const int q = tid + TPB * jj;
+                const bool in = q < (nu0 << lpr_sh);
+                float orm = in ? abs_max4(wpf[jj]) : -1.0f;
+                for (int o = 1; o < LPR; o <<= 1) orm = fmaxf(orm, __shfl_xor(orm, o, WAVE));
+                const bool cand = in && (q & (LPR - 1)) == 0 && orm == bpf[jj];
+                const uint64_t cm = __ballot(cand);
+                if (cb < 0 && cm) {
+                    const int l = __ffsll((unsigned long long)cm) - 1;
+                    const int qq = __builtin_amdgcn_readlane(q, l);
+                    cb = (int)((r0 + krow(keys[hpos[ua0 + (qq >> lpr_sh)]])) >> 8);
+                }
+            }
+            const int lane = tid % WAVE;
+            if (cb >= 0) {
+                float* cache = reinterpret_cast<float*>(w < 8 ? (unsigned char*)pos : (unsigned char*)mlist) + (w & 7) * BLK;
+                float v[BLK / WAVE];
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) {
+                    const int64_t r = (int64_t)cb * BLK + lane + i * WAVE;
+                    v[i] = r < nrows ? la.rowmax[rb + r] : 0.0f;
+                }
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) cache[lane + i * WAVE] = v[i];
+            }
+            if (lane == 0) s_cand_blk[w] = cb;
+        }
+        if (w == 0 && tid < CAND_SLOTS) {
+            if (tid == 0 || dsplit) s_cand_blk[tid] = -1;
+        }
     }
     if (APPLY && tid < WAVE) {  // wave 0: lane j polls slot j's granule until it shows this launch's epoch
         uint64_t g = 0;
@@ -1125,9 +1190,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const bool one_slot = NA == SPLIT;
         // (LDS dead by now: the gather map sdest and the multi-lookup list mlist)
         float* s_newrm = reinterpret_cast<float*>(sdest);  // [nu0]
-        float* s_blkrm = reinterpret_cast<float*>(mlist);  // [RRW][BLK] per-wave block scratch
+        float* s_blkrm = stage;  // [RRW][BLK] per-wave block scratch (the update's values are dead by then)
         constexpr int RRW = 8;                             // waves re-reducing blocks at a time
-        static_assert(RRW * BLK * 4 <= (MAXB + 8) * 2, "block scratch in the mlist region");
+        static_assert(RRW * BLK <= STAGE_FLOATS, "block scratch in the stage region");
         // item (entry u - ua, float4 sub) of slot sl: w0 = the row's old values, oblk its
         // block's max before this step (a stale-low superblock or table max only costs a
         // redundant atomicMax: within the launch they only grow)
@@ -1150,7 +1215,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             st_wt(la.rowmax + grow, rm);
             if (one_slot) s_newrm[u - ua] = rm;
             const int64_t blk = x >> 8, sb = sbb + (blk >> 8);
-            const float osb = rm > oblk || old_rm == oblk ? la.sblkmax[sb] : 0.0f;  // the superblock's max
+            const int64_t sbl = (blk >> 8) - sb0;  // superblock index relative to the slot's first
+            const float osb = !(rm > oblk || old_rm == oblk) ? 0.0f  // the superblock's max
+                              : (sbl >= 0 && sbl < nsbc) ? s_sbm[sbl] : la.sblkmax[sb];
             if (rm > oblk) {  // growth: order-free atomicMax on the non-negative float bits
                 atomicMax(reinterpret_cast<unsigned int*>(la.blkmax) + bb + blk, __float_as_uint(rm));
                 if (rm > osb) {
@@ -1223,10 +1290,17 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 // the block's untouched rows keep their stored maxima; its touched rows (the
                 // slot's entries [e0, e1), ascending rows) take their new maxima from LDS
                 float* sc = s_blkrm + w * BLK;
+                int ci = -1;  // a wave's cache holds this block's stored row maxima already
+                for (int c = 1; c < CAND_SLOTS; ++c)
+                    if (ci < 0 && s_cand_blk[c] == (int)blk) ci = c;
+                if (ci >= 0) {
+                    sc = reinterpret_cast<float*>(ci < 8 ? (unsigned char*)pos : (unsigned char*)mlist) + (ci & 7) * BLK;
+                } else {
 #pragma unroll
-                for (int i = 0; i < BLK / WAVE; ++i) {
-                    const int64_t r = blk * BLK + lane + i * WAVE;
-                    sc[lane + i * WAVE] = r < nrows ? la.rowmax[rb + r] : 0.0f;
+                    for (int i = 0; i < BLK / WAVE; ++i) {
+                        const int64_t r = blk * BLK + lane + i * WAVE;
+                        sc[lane + i * WAVE] = r < nrows ? la.rowmax[rb + r] : 0.0f;
+                    }
                 }
                 auto first_at_least = [&](int64_t row) {  // first entry with a row >= `row`
                     int lo = 0, hi = nu0;
