@@ -2925,7 +2925,10 @@ __global__ void __launch_bounds__(FB_TPB) k_bwd_fused(FArgs a) {
 // ascending lookup position j,  W = fma((dy[bag(j)] * s) / s, -lr, W).
 //   1. one round trip: the table's indices, every bag's dy slice (STE applied, staged in
 //      LDS), the offsets (bag form) and, for a narrow table, its rows' |W| maxima;
-//   2. one lane group (LPR lanes) per lookup i: the group's lanes compare x_i with
+//   2. Criteo form: every lookup inserts its row into an LDS hash (row -> bitmask of its
+//      positions, one atomicCAS probe chain + one 64-bit atomicOr); the row's owner is its
+//      lowest position, and the mask IS its positions in ascending order (no scan, no list).
+//      Bag form: one lane group (LPR lanes) per lookup i, the group's lanes compare x_i with
 //      disjoint position ranges (one 64-bit match mask each); i owns its row iff no earlier
 //      position matches;
 //   3. owners load their W row and the old block / superblock / table maxima (one round
@@ -2943,6 +2946,17 @@ constexpr int SG_DY_FLOATS = 16384;    // dy staging, dynamic LDS (64 KiB)
 __host__ __device__ constexpr int sg_maxl(int lpr) {
     return SG_MAXL < 64 * lpr ? (SG_MAXL < 8 * (SG_TPB / lpr) ? SG_MAXL : 8 * (SG_TPB / lpr))
                               : (64 * lpr < 8 * (SG_TPB / lpr) ? 64 * lpr : 8 * (SG_TPB / lpr));
+}
+
+// the Criteo-form row hash of k_sgd_small: 2^sg_hash_log(L) >= 2L slots of {row + 1, [MW]
+// 64-bit position masks} after the dy staging in dynamic LDS
+__host__ __device__ constexpr int sg_hash_log(int L) {
+    int lg = 6;
+    while ((1 << lg) < 2 * L) ++lg;
+    return lg;
+}
+__host__ __device__ constexpr int64_t sg_hash_bytes(int L) {
+    return (int64_t)(1 << sg_hash_log(L)) * (4 + 8 * ((L + 63) / 64));
 }
 
 template <int LPR>
@@ -2965,7 +2979,6 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     __shared__ float s_sqo[SG_MAXL];                             // ... their old max
     __shared__ float s_red[NW];
     __shared__ int s_n[3];                                       // queue lengths, rescan flag
-    __shared__ int s_wsc[NW + 1];                                // block scan scratch
     const int t = blockIdx.x;
     DIAG_T(0);
     const Meta m = make_meta(a.meta, a.T);
@@ -3034,6 +3047,14 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     }
     if (narrow && threadIdx.x < nrows) s_rm[threadIdx.x] = rmv;
     if (threadIdx.x < 3) s_n[threadIdx.x] = 0;
+    // Criteo form: the row hash after the dy staging (sized by the host, sg_hash_bytes)
+    const int MW = (L + 63) >> 6;               // mask words per row
+    const int hs_log = sg_hash_log(L);
+    const int HS = 1 << hs_log;
+    int32_t* s_hk = reinterpret_cast<int32_t*>(lds + (size_t)B * D * 4);           // row + 1, 0 = empty
+    unsigned long long* s_hm = reinterpret_cast<unsigned long long*>(s_hk + HS);  // [HS][MW] positions
+    if (p1)
+        for (int i = threadIdx.x; i < HS * (1 + 2 * MW); i += SG_TPB) s_hk[i] = 0;
     if (!p1 && (int)threadIdx.x < B) s_q[threadIdx.x] = o0 < 0 ? -1 : (o0 > L ? L + 1 : (int32_t)o0);
     if (!p1)
         for (int j = threadIdx.x; j < L; j += SG_TPB) s_bag[j] = -1;
@@ -3050,13 +3071,37 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     }
     if (!p1) __syncthreads();
     DIAG_T(2);
-    // 3. duplicate scan: lane `sub` of a group compares positions [sub*ch, sub*ch + ch)
+    // 3. duplicates. Criteo form: the row hash (see the header); bag form: lane `sub` of a
+    //    group compares positions [sub*ch, sub*ch + ch)
     const int ch = (L + LPR - 1) / LPR;  // <= 64
     const int j0 = sub * ch, j1 = j0 + ch < L ? j0 + ch : L;
     uint64_t mk[NPG];
+    int hslot[NPG];
 #pragma unroll
-    for (int k = 0; k < NPG; ++k) mk[k] = 0ull;
-    for (int jb = j0; jb < j1; jb += 8) {  // 8 unconditional LDS reads in flight, then the compares
+    for (int k = 0; k < NPG; ++k) {
+        mk[k] = 0ull;
+        hslot[k] = -1;
+    }
+    if (p1) {
+#pragma unroll
+        for (int k = 0; k < NPG; ++k) {
+            const int i = grp + k * G;
+            if (sub == 0 && xk[k] >= 0) {
+                const int key = xk[k] + 1;
+                uint32_t h = ((uint32_t)xk[k] * 2654435761u) >> (32 - hs_log);
+                for (;;) {  // linear probing; HS >= 2L, so a free or matching slot exists
+                    const int old = atomicCAS(&s_hk[h], 0, key);
+                    if (old == 0 || old == key) break;
+                    h = (h + 1) & (uint32_t)(HS - 1);
+                }
+                hslot[k] = (int)h;
+                atomicOr(&s_hm[h * MW + (i >> 6)], 1ull << (i & 63));
+            }
+            hslot[k] = __shfl(hslot[k], gbase, WAVE);
+        }
+        __syncthreads();
+    }
+    for (int jb = j0; jb < j1 && !p1; jb += 8) {  // 8 unconditional LDS reads in flight, then the compares
         int32_t v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] = s_row[jb + i < j1 ? jb + i : j1 - 1];
@@ -3071,63 +3116,47 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
         const int i = grp + k * G;
-        const int lo = i - j0;  // positions of this lane's range that precede i
-        const uint64_t earlier = lo <= 0 ? 0ull : (lo >= 64 ? mk[k] : (mk[k] & ((1ull << lo) - 1ull)));
-        own[k] = i < L && xk[k] >= 0 && !(__ballot(earlier != 0ull) & gmask);
+        if (p1) {  // the owner is the row's lowest position: the first set bit of its mask
+            bool first = false;
+            if (hslot[k] >= 0) {
+                const unsigned long long* hm = s_hm + hslot[k] * MW;
+                int wd = 0;
+                unsigned long long m0 = hm[0];
+                while (m0 == 0ull && wd + 1 < MW) m0 = hm[++wd];
+                first = wd * 64 + __ffsll((long long)m0) - 1 == i;
+            }
+            own[k] = i < L && xk[k] >= 0 && first;
+        } else {
+            const int lo = i - j0;  // positions of this lane's range that precede i
+            const uint64_t earlier = lo <= 0 ? 0ull : (lo >= 64 ? mk[k] : (mk[k] & ((1ull << lo) - 1ull)));
+            own[k] = i < L && xk[k] >= 0 && !(__ballot(earlier != 0ull) & gmask);
+        }
     }
     const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
-    // Criteo form: every owner's matched positions, ascending, as one contiguous run of an LDS
-    // list (s_bag, unused by this form; the runs laid out by a block scan of the owners'
-    // counts), so that its ordered walk below reads 8 positions' dy per LDS round trip --
-    // a hot row of a tiny table has ~B/n of them
-    int rbase[NPG], rcnt[NPG];
-    if (p1) {
-        int pc[NPG], pre[NPG], mine = 0;
-#pragma unroll
-        for (int k = 0; k < NPG; ++k) {
-            pc[k] = (int)__popcll(mk[k]);
-            pre[k] = 0;
-            rcnt[k] = 0;
-#pragma unroll
-            for (int l = 0; l < LPR; ++l) {  // the group's count, and this lane's offset in it
-                const int v = __shfl(pc[k], gbase + l, WAVE);
-                rcnt[k] += v;
-                if (l < sub) pre[k] += v;
-            }
-            if (own[k] && sub == 0) mine += rcnt[k];
-        }
-        int tot;
-        int base = block_scan_excl<SG_TPB>(mine, s_wsc, &tot);
-#pragma unroll
-        for (int k = 0; k < NPG; ++k) {
-            rbase[k] = __shfl(base, gbase, WAVE);  // the group's lane 0 holds the run bases
-            if (own[k] && sub == 0) base += rcnt[k];
-            if (!own[k]) continue;
-            uint64_t m = mk[k];
-            int r = rbase[k] + pre[k];
-            while (m) {  // this lane's matches, ascending
-                s_bag[r++] = j0 + __ffsll((long long)m) - 1;
-                m &= m - 1;
-            }
-        }
-        __syncthreads();
-    }
     DIAG_T(3);
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
         if (!own[k]) continue;  // group-uniform
         float4 acc = w0[k];
-        if (p1) {  // the run: 8 positions and their dy rows in flight, then the FMAs in order
-            for (int i0 = 0; i0 < rcnt[k]; i0 += 8) {
-                int jj[8];
+        if (p1) {  // the row's positions, ascending, straight from its mask: 8 dy rows in flight
+            const unsigned long long* hm = s_hm + hslot[k] * MW;
+            for (int wd = 0; wd < MW; ++wd) {
+                unsigned long long mm = hm[wd];
+                while (mm) {
+                    int jj[8], nv = 0;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) jj[q] = s_bag[rbase[k] + (i0 + q < rcnt[k] ? i0 + q : rcnt[k] - 1)];
-                float4 g[8];
+                    for (int q = 0; q < 8; ++q) {
+                        jj[q] = mm ? wd * 64 + __ffsll((long long)mm) - 1 : (q ? jj[q - 1] : 0);
+                        nv += mm ? 1 : 0;
+                        mm &= mm - 1;
+                    }
+                    float4 g[8];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) g[q] = s_dy[jj[q] * LPR + sub];
+                    for (int q = 0; q < 8; ++q) g[q] = s_dy[jj[q] * LPR + sub];
 #pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (i0 + q < rcnt[k]) acc = seg_op4<OP_FMA>(acc, g[q], a.nlr);
+                    for (int q = 0; q < 8; ++q)
+                        if (q < nv) acc = seg_op4<OP_FMA>(acc, g[q], a.nlr);
+                }
             }
         }
         for (int l = 0; l < LPR && !p1; ++l) {  // the row's positions, ascending
@@ -3649,7 +3678,10 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     // SGD of a small batch: one workgroup per table, no sort, no hand-off (k_sgd_small)
     if (MODE == 0 && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && Lc <= sg_maxl(D / 4) &&
         c.batch->num_bags * D <= SG_DY_FLOATS && set->total_rows <= 0x7fffffffll) {
-        const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float);
+        // dy staging, then (Criteo form) the row hash; the kernel reads L = B lookups per table
+        const bool p1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+        const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float) +
+                           (p1 ? (size_t)sg_hash_bytes((int)c.batch->num_bags) : 0);
         DISPATCH_LPR(D, {
             if ((rc = allow_lds(k_sgd_small<LPR>, dyn))) return rc;
             hipLaunchKernelGGL(k_sgd_small<LPR>, dim3(T), dim3(SG_TPB), dyn, st, fa);

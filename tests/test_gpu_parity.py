@@ -871,3 +871,31 @@ def test_fused_coalesce_apply_matches_two_launches(dq, D, B, dist, bits, repack)
     sets[0].refresh_absmax()
     for x, y in zip(inc, (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("B,D,dist", [(128, 16, "uniform"), (128, 16, "zipf"), (256, 16, "zipf"), (64, 64, "uniform"),
+                                      (100, 4, "zipf"), (500, 8, "uniform"), (1, 16, "uniform")])
+def test_sgd_small_criteo_form_matches_oracle(dq, B, D, dist):
+    """The one-workgroup-per-table SGD kernel on Criteo-form batches (config 3: its row hash
+    of position masks replaces the duplicate scan): three steps on tables from 3 rows (~B/3
+    lookups per row, walked in position order) to 2 M rows equal the oracle's per-lookup
+    torch.optim.SGD order bit for bit, in W and in the kept |W| hierarchy."""
+    rows = [3, 4, 10, 27, 305, 3194, 100000, 2_000_000]
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 21 + B)
+    ts = make_set(dq, Ws)
+    for it in range(3):
+        P = G.pooling_one(rows, B, 22 + it, dist=dist)
+        dy = G.upstream_grad(T, B, D, 25 + it) * 5
+        b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+        ts.forward(b)
+        ts.backward_sgd(b, torch.from_numpy(dy).cuda(), lr=0.1)
+        for t in range(T):
+            O.emb_bwd_sgd(Ws[t], P[t], np.arange(B, dtype=np.int64), dy[t], O.table_scale(Ws[t], 4), 0.1)
+    assert ts.read_errors() == 0
+    for t in range(T):
+        np.testing.assert_array_equal(ts.table_weight(t).cpu().numpy(), Ws[t])
+    inc = [x.clone() for x in (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)]
+    ts.refresh_absmax()
+    for x, y in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
+        assert torch.equal(x, y)
