@@ -383,8 +383,11 @@ class ConsolidatedExchange:
     pending (batch, dy) pairs are concatenated on the device (one copy each for the
     indices, offsets and dy) and the step runs as ONE coalesce, ONE quantize-pack and ONE
     apply for all tables (two collectives at N > 1) -- the launch count of a single
-    26-table set. At world size 1 with quantized gradients quantize-pack and apply run
-    fused at apply time (dqrm_apply_local), which also produces the averaged scales."""
+    26-table set. At world size 1 with quantized gradients the whole local step -- coalesce,
+    quantize and apply -- runs at apply time as ONE launch (dqrm_emb_bwd_apply_local), which
+    also produces the averaged scales (emb_scaling_factor holds them from then on; the
+    reference sets them in grad_update_parallel_comm, s_q_g_p_c.py:296, and reads them in
+    weight_update_parallel_comm, :618-622, so the update sees the same values)."""
 
     def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None):
         self.tables = tables
@@ -403,16 +406,23 @@ class ConsolidatedExchange:
         if any(it[2] != ste for it in items):
             raise ValueError("modules differ in full_precision (STE) within one step")
         if self.fused:
-            self.inner.kernels.coalesce(batch, dy, self.inner.ws, ste, "tbd")
-            self._args = (batch, dy)  # keep the inputs alive until the update
+            self._args = (batch, dy, ste)  # the one-launch step runs at apply time
         else:
             self.inner.exchange(batch, dy, ste=ste, layout="tbd")
         return self.scales
 
     def apply(self, lr: float, mode: int | None = None, repack=False) -> None:
         rp = any(repack) if isinstance(repack, (list, tuple)) else bool(repack)
-        if self.fused and (mode is None or mode == L.DQRM_UPD_DP):
-            self.inner.kernels.apply_local(self.inner.ws, self.grad_bits, self.inner.s_avg, lr, rp)
+        if self.fused:
+            if self._args is None:
+                raise RuntimeError("apply() without a preceding exchange()")
+            batch, dy, ste = self._args
+            if mode is None or mode == L.DQRM_UPD_DP:
+                self.inner.kernels.coalesce_apply_local(batch, dy, self.inner.ws, ste, "tbd", self.grad_bits,
+                                                        self.inner.s_avg, lr, rp)
+            else:  # another update rule: the exchange's coalesce, then the payload path
+                self.inner.exchange(batch, dy, ste=ste, layout="tbd")
+                self.inner.apply(lr, mode=mode, repack=rp)
         else:
             self.inner.apply(lr, mode=mode, repack=rp)
         self._args = None

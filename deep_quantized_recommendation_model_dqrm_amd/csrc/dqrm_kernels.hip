@@ -2948,13 +2948,17 @@ __host__ __device__ constexpr int sg_maxl(int lpr) {
                               : (64 * lpr < 8 * (SG_TPB / lpr) ? 64 * lpr : 8 * (SG_TPB / lpr));
 }
 
-// the Criteo-form row hash of k_sgd_small: 2^sg_hash_log(L) >= 2L slots of {row + 1, [MW]
+// the Criteo-form row hash of k_sgd_small: 2^sg_hash_log(L) >= 4L slots of {row + 1, [MW]
 // 64-bit position masks} after the dy staging in dynamic LDS
 __host__ __device__ constexpr int sg_hash_log(int L) {
     int lg = 6;
-    while ((1 << lg) < 2 * L) ++lg;
+    while ((1 << lg) < 4 * L) ++lg;  // load <= 1/4: short probe chains
     return lg;
 }
+#ifndef DQRM_SG_RUN
+#define DQRM_SG_RUN 16
+#endif
+constexpr int SG_RUN = DQRM_SG_RUN;  // positions (dy rows) of an owner's walk in flight
 __host__ __device__ constexpr int64_t sg_hash_bytes(int L) {
     return (int64_t)(1 << sg_hash_log(L)) * (4 + 8 * ((L + 63) / 64));
 }
@@ -3089,7 +3093,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             if (sub == 0 && xk[k] >= 0) {
                 const int key = xk[k] + 1;
                 uint32_t h = ((uint32_t)xk[k] * 2654435761u) >> (32 - hs_log);
-                for (;;) {  // linear probing; HS >= 2L, so a free or matching slot exists
+                for (;;) {  // linear probing; HS >= 4L, so a free or matching slot exists
                     const int old = atomicCAS(&s_hk[h], 0, key);
                     if (old == 0 || old == key) break;
                     h = (h + 1) & (uint32_t)(HS - 1);
@@ -3138,23 +3142,23 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     for (int k = 0; k < NPG; ++k) {
         if (!own[k]) continue;  // group-uniform
         float4 acc = w0[k];
-        if (p1) {  // the row's positions, ascending, straight from its mask: 8 dy rows in flight
+        if (p1) {  // the row's positions, ascending, straight from its mask: SG_RUN dy rows in flight
             const unsigned long long* hm = s_hm + hslot[k] * MW;
             for (int wd = 0; wd < MW; ++wd) {
                 unsigned long long mm = hm[wd];
                 while (mm) {
-                    int jj[8], nv = 0;
+                    int jj[SG_RUN], nv = 0;
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) {
+                    for (int q = 0; q < SG_RUN; ++q) {
                         jj[q] = mm ? wd * 64 + __ffsll((long long)mm) - 1 : (q ? jj[q - 1] : 0);
                         nv += mm ? 1 : 0;
                         mm &= mm - 1;
                     }
-                    float4 g[8];
+                    float4 g[SG_RUN];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) g[q] = s_dy[jj[q] * LPR + sub];
+                    for (int q = 0; q < SG_RUN; ++q) g[q] = s_dy[jj[q] * LPR + sub];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q)
+                    for (int q = 0; q < SG_RUN; ++q)
                         if (q < nv) acc = seg_op4<OP_FMA>(acc, g[q], a.nlr);
                 }
             }
@@ -3460,15 +3464,23 @@ int grid_for(int64_t work_items, int threads, int max_blocks = 2048) {
 // Rows rewritten outside libdqrm (torch.optim.SGD stepping on the grad_mode="sparse" COO):
 // one lane group per listed slab row recomputes its rowmax (and, repack, its INT4 row with
 // the frozen pscale) and flags its block and superblock; the untracked finalize then
-// re-reduces exactly those blocks and every table maximum.
+// re-reduces exactly those blocks and every table maximum -- for a one-table set (the
+// drivers' per-table modules) inside the launch, in its last workgroup (arrival counter in
+// sync word 1; row maxima stored write-through), instead of a second launch.
 // ------------------------------------------------------------------------------------
-template <int LPR>
+struct RcFin {  // the in-launch finalize of a one-table set
+    float* blkmax;
+    float* sblkmax;
+    float* tmax;
+    uint32_t* sync;
+};
+template <int LPR, bool FIN>
 __global__ void __launch_bounds__(256) k_rows_changed(const float* __restrict__ W, float* __restrict__ rowmax,
                                                       uint8_t* __restrict__ bdirty, uint8_t* __restrict__ sdirty,
                                                       uint8_t* __restrict__ packed, const float* __restrict__ pscale,
                                                       const int64_t* __restrict__ meta, int T,
                                                       const int64_t* __restrict__ rows, int64_t n, int64_t total,
-                                                      uint32_t* __restrict__ err) {
+                                                      uint32_t* __restrict__ err, RcFin fin) {
     constexpr int G = 256 / LPR;
     const int lane = threadIdx.x % LPR;
     const Meta m = make_meta(meta, T);
@@ -3486,10 +3498,15 @@ __global__ void __launch_bounds__(256) k_rows_changed(const float* __restrict__ 
         for (int o = 1; o < LPR; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, LPR));
         if (packed) pack_row_int4<LPR>(w, packed, g, lane, 1.0f / pscale[t]);
         if (lane == 0) {
-            rowmax[g] = v;
+            if (FIN) st_wt(rowmax + g, v);
+            else rowmax[g] = v;
             flag_set(bdirty, m.blk_base[t] + r / BLK);
             flag_set(sdirty, m.sblk_base[t] + r / ((int64_t)BLK * SBLK_BLOCKS));
         }
+    }
+    if constexpr (FIN) {
+        if (arrive_last(fin.sync + 1, gridDim.x))
+            finalize_table<true>(m, 0, W, rowmax, fin.blkmax, fin.sblkmax, sdirty, bdirty, fin.tmax, LPR * 4, false);
     }
 }
 
@@ -3885,14 +3902,23 @@ int dqrm_rows_changed(const dqrm_table_set* set, const int64_t* rows, int64_t n,
     if (n == 0) return DQRM_OK;
     hipStream_t st = (hipStream_t)stream;
     uint8_t* pk = repack_bits == 4 ? set->packed : nullptr;
+    // a one-table set finalizes inside the launch (its last workgroup); larger sets launch
+    // the per-table finalize
+    const bool fin = set->num_tables == 1 && finalize_mode() != 1;
+    const RcFin rf{set->blkmax, set->sblkmax, set->tmax, set->sync};
     DISPATCH_LPR(set->dim, {
         constexpr int G = 256 / LPR;
-        hipLaunchKernelGGL(k_rows_changed<LPR>, dim3(grid_for(n, G, 4096)), dim3(256), 0, st, set->W, set->rowmax,
-                           set->bdirty, set->sdirty, pk, set->pscale, set->meta, set->num_tables, rows, n,
-                           set->total_rows, (uint32_t*)set->err);
+        if (fin)
+            hipLaunchKernelGGL((k_rows_changed<LPR, true>), dim3(grid_for(n, G, 4096)), dim3(256), 0, st, set->W,
+                               set->rowmax, set->bdirty, set->sdirty, pk, set->pscale, set->meta, set->num_tables,
+                               rows, n, set->total_rows, (uint32_t*)set->err, rf);
+        else
+            hipLaunchKernelGGL((k_rows_changed<LPR, false>), dim3(grid_for(n, G, 4096)), dim3(256), 0, st, set->W,
+                               set->rowmax, set->bdirty, set->sdirty, pk, set->pscale, set->meta, set->num_tables,
+                               rows, n, set->total_rows, (uint32_t*)set->err, rf);
     });
     LAUNCH_CHECK();
-    return launch_finalize(set, st, false);
+    return fin ? DQRM_OK : launch_finalize(set, st, false);
 }
 
 int dqrm_emb_bwd_lookup_grad(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,

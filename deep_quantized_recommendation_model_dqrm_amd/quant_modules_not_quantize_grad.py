@@ -72,8 +72,9 @@ def _pooling_one_arg():
 
 
 def error_check_due(owner) -> bool:
-    n = getattr(owner, "_dqrm_err_calls", 0) + 1
-    owner._dqrm_err_calls = n
+    d = owner.__dict__  # a plain attribute (nn.Module.__setattr__ is slow on the per-call path)
+    n = d.get("_dqrm_err_calls", 0) + 1
+    d["_dqrm_err_calls"] = n
     return _ERROR_CHECK_EVERY > 0 and n % _ERROR_CHECK_EVERY == 0
 
 
@@ -102,8 +103,17 @@ def set_default_grad_mode(mode: str) -> None:
     _DEFAULT_GRAD_MODE = mode
 
 
+def _on(x: torch.Tensor, device: torch.device) -> bool:
+    d = x.device
+    return d.type == device.type and (device.index is None or d.index == device.index)
+
+
 def _batch_from_input(input: torch.Tensor, offsets: torch.Tensor | None, device) -> LookupBatch:
     """nn.EmbeddingBag input conventions: 1-D input + offsets, or 2-D [B, L] fixed bags."""
+    if (input.dim() == 1 and offsets is not None and offsets.dim() == 1 and _on(input, device)
+            and _on(offsets, device)):  # the drivers' per-table call: one table, no copies
+        p1 = _pooling_one_arg() if input.numel() == offsets.numel() else False
+        return LookupBatch.one_table(input, offsets, pooling_one=p1)
     if input.dim() == 2:
         if offsets is not None:
             raise ValueError("if input is 2D, then offsets has to be None")
@@ -309,8 +319,8 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
         else:
             refresh_in_fwd = refresh
         y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "tbd")
-        if refresh:
-            self.eb_scaling_factor = self._tset.scale.view(())  # 0-d scale, as the reference stores it
+        if refresh:  # 0-d scale, as the reference stores it (the buffer entry, without __setattr__)
+            self._buffers["eb_scaling_factor"] = self._tset.scale.view(())
         return y[0]
 
     def load_state_dict(self, state_dict, strict=True, assign=False):

@@ -47,7 +47,7 @@ _BASE_CACHE: dict = {}
 def _device_base(base: list[int], dev: torch.device) -> torch.Tensor:
     """Device copy of a batch's idx_base, created once per distinct (lookup counts, device):
     steady-state steps reuse it instead of a pageable host-to-device copy per call."""
-    key = (tuple(base), str(dev))
+    key = (tuple(base), dev.type, dev.index)
     t = _BASE_CACHE.get(key)
     if t is None:
         if len(_BASE_CACHE) > 256:
@@ -150,6 +150,31 @@ class LookupBatch:
         for t in range(T):
             idx.append(torch.cat([b.idx[b.idx_base_host[t]: b.idx_base_host[t + 1]] for b in batches]))
         return cls(idx, torch.cat(off, dim=1), pooling_one=all(b.pooling_one for b in batches))
+
+    @classmethod
+    def one_table(cls, idx: torch.Tensor, off: torch.Tensor, pooling_one: bool | None = False) -> "LookupBatch":
+        """A one-table batch from a 1-D index and offsets tensor already on the device (the
+        per-table module call of DLRM_Net.apply_emb): the same fields as the constructor,
+        without its general-case work (no concatenation, no copies of int64 contiguous
+        inputs). pooling_one None is taken as False (device offsets cannot be checked)."""
+        if idx.dtype != torch.int64 or not idx.is_contiguous():
+            idx = idx.to(torch.int64).contiguous()
+        if off.dtype != torch.int64 or not off.is_contiguous():
+            off = off.to(torch.int64).contiguous()
+        b = cls.__new__(cls)
+        n = idx.numel()
+        B = off.numel()
+        if pooling_one and n != B:
+            raise ValueError("pooling_one needs exactly one lookup per bag in every table")
+        b.num_tables, b.num_bags, b.lookups, b.max_lookups = 1, B, [n], n
+        b.idx_base_host = [0, n]
+        b.idx = idx
+        b.off = off.view(1, B)
+        b.idx_base = _device_base(b.idx_base_host, idx.device)
+        b.pooling_one = bool(pooling_one)
+        b._c = L.Batch(idx.data_ptr(), off.data_ptr(), b.idx_base.data_ptr(), B, n,
+                       L.DQRM_BATCH_POOLING_ONE if pooling_one else 0, 0)
+        return b
 
     @classmethod
     def pooling_one(cls, indices: torch.Tensor) -> "LookupBatch":

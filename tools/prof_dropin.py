@@ -1,6 +1,8 @@
-"""Host-side profile (cProfile) of the drop-in call patterns at Kaggle B=128: where the
-per-step host time of the modules + hooks goes (the kernels take ~20 us of it).
-usage: python tools/prof_dropin.py [coll-dp|coll-sgd|list-sgd] [steps]"""
+"""Host-side profile of the drop-in call patterns at Kaggle B=128: where the per-step host
+time of the modules + hooks goes (the kernels take ~20 us of it): per-phase wall time
+(forward / backward / optimizer or hooks, the device synchronised between phases), then
+cProfile.
+usage: python tools/prof_dropin.py [coll-dp|coll-sgd|list-sgd|list-dp] [steps]"""
 import cProfile
 import os
 import pstats
@@ -56,6 +58,30 @@ def step(i):
 for i in range(10):
     step(i)
 torch.cuda.synchronize()
+ph = {"fwd": 0.0, "bwd": 0.0, "opt/hooks": 0.0}
+for i in range(steps):
+    Pi = P[i % 8]
+    t0 = time.perf_counter()
+    if dp:
+        H.clear_gradients(model)
+    ly = [emb[t](Pi[t], lS_o) for t in range(T)] if kind.startswith("list") else emb(lS_o.expand(T, B), Pi)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    torch.autograd.backward(ly, dys)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if dp:
+        H.grad_update_parallel_comm(model, 1, True, 8)
+        H.weight_update_parallel_comm(model, 0.1, num_gpus=1)
+    elif opt is not None:
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    ph["fwd"] += t1 - t0
+    ph["bwd"] += t2 - t1
+    ph["opt/hooks"] += t3 - t2
+print(f"{kind} phases (us/step, synchronised): " + ", ".join(f"{k} {v / steps * 1e6:.1f}" for k, v in ph.items()))
 t0 = time.perf_counter()
 for i in range(steps):
     step(i)
