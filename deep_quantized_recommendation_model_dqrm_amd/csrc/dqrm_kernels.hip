@@ -2956,7 +2956,7 @@ __host__ __device__ constexpr int sg_hash_log(int L) {
     return lg;
 }
 #ifndef DQRM_SG_RUN
-#define DQRM_SG_RUN 16
+#define DQRM_SG_RUN 8
 #endif
 constexpr int SG_RUN = DQRM_SG_RUN;  // positions (dy rows) of an owner's walk in flight
 __host__ __device__ constexpr int64_t sg_hash_bytes(int L) {

@@ -133,8 +133,13 @@ class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, weight, owner, batches, bits, flags_refresh, full_precision, layout):
         tset: EmbeddingTableSet = owner._tset
+        one = layout == "bd"  # one table: its [B, D] output itself (no select node after the Function)
+        layout = "tbd" if one else layout
         y = tset.forward(batches, bits=bits, refresh_scale=flags_refresh, use_packed=owner._use_packed(full_precision),
                          full_precision=full_precision, layout=layout)
+        if one:
+            y = y.view(y.shape[1], y.shape[2])
+        ctx.one = one
         ctx.owner = owner
         ctx.batches = batches
         ctx.ste = not full_precision
@@ -145,6 +150,8 @@ class _EmbeddingFn(torch.autograd.Function):
     def backward(ctx, dy):
         owner = ctx.owner
         dy = dy.contiguous()
+        if ctx.one:
+            dy = dy.view(1, dy.shape[0], dy.shape[1])
         grad_w = owner._backward(ctx.batches, dy, ctx.ste, ctx.layout)
         return grad_w, None, None, None, None, None, None
 
@@ -160,8 +167,20 @@ class _WeightHolder(nn.Module):
         self.sparse = sparse
 
 
+# per-call bookkeeping attributes of the modules: plain instance attributes, written without
+# nn.Module.__setattr__'s parameter / buffer / submodule checks (the drivers call 26 modules a
+# step, and the hooks reset these for every module)
+_PLAIN_ATTRS = frozenset({"_pending", "_ready", "_rr", "_ext_rows", "_counters", "_exchange", "_dqrm_err_calls"})
+
+
 class _QuantEmbeddingBase(nn.Module):
     grad_modes = ("sparse", "fused_sgd", "dp")
+
+    def __setattr__(self, name, value):
+        if name in _PLAIN_ATTRS:
+            self.__dict__[name] = value
+        else:
+            super().__setattr__(name, value)
 
     def _init_common(self, grad_mode, lr, scale_period, use_packed_int4):
         if grad_mode is None:
@@ -318,10 +337,17 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
             refresh_in_fwd = False
         else:
             refresh_in_fwd = refresh
-        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "tbd")
-        if refresh:  # 0-d scale, as the reference stores it (the buffer entry, without __setattr__)
-            self._buffers["eb_scaling_factor"] = self._tset.scale.view(())
-        return y[0]
+        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "bd")
+        if refresh:
+            # 0-d scale, as the reference stores it: a view of the set's scale, which every
+            # refreshing forward rewrites in place (the buffer entry, without __setattr__)
+            sv = self.__dict__.get("_scale0")
+            if sv is None or sv[0] is not self._tset:
+                sv = (self._tset, self._tset.scale.view(()))
+                self.__dict__["_scale0"] = sv
+            if self._buffers["eb_scaling_factor"] is not sv[1]:
+                self._buffers["eb_scaling_factor"] = sv[1]
+        return y
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)

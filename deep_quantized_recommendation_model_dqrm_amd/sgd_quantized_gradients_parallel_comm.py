@@ -55,6 +55,12 @@ def _world(group=None) -> int:
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+def _mset(model, name: str, value) -> None:
+    """The hooks' per-step bookkeeping on the driver's model: a plain instance attribute
+    (nn.Module.__setattr__'s checks are a measurable share of the hooks' host time)."""
+    model.__dict__[name] = value
+
+
 def _emb_modules(model) -> list[_QuantEmbeddingBase]:
     emb = getattr(model, "emb_l", None)
     if emb is None:
@@ -163,7 +169,7 @@ def _consolidated_set(model, mods, group=None):
             ok = _all_ranks_agree(_CONSOLIDATE and can_consolidate(mods), group, mods[0]._tset.device)
             if ok:
                 big = consolidate_tables(mods, force=True) or False
-        model._dqrm_consolidated = big
+        _mset(model, "_dqrm_consolidated", big)
     if big is False:
         first = mods[0]._tset.parent
         if first is not None and len(mods) == first.T and all(
@@ -191,7 +197,7 @@ def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group)
         if fresh or _outgrown([need], ex[1].max_lookups[:1], group):
             cap = _agreed_caps([need if fresh else max(need, ex[1].max_lookups[0])], group, big.device)[0]
             ex = (key, ConsolidatedExchange(big, cap, grad_bits=grad_bits, group=group))
-            model._dqrm_emb_exchange = ex
+            _mset(model, "_dqrm_emb_exchange", ex)
             for t, m in enumerate(mods):  # the modules' emb_scaling_factor: views of the averaged scales
                 m.emb_scaling_factor = ex[1].scales[t]
         return ex[1]
@@ -204,7 +210,7 @@ def _emb_exchange(model, mods: list[_QuantEmbeddingBase], grad_bits: int, group)
                             mods[0]._tset.device)
         ex = (key, MultiSetExchange([m._tset for m in mods], caps, grad_bits=grad_bits, group=group,
                                     device=mods[0]._tset.device))
-        model._dqrm_emb_exchange = ex
+        _mset(model, "_dqrm_emb_exchange", ex)
         word = mods[0]._tset.err
         for m in mods[1:]:
             m._tset.share_error_word(word)
@@ -261,7 +267,7 @@ def grad_update_parallel_comm(model, number_of_gpus, emb_grad_quantized=True, nu
                         m.emb_scaling_factor.copy_(s.view_as(m.emb_scaling_factor))
                     m._pending = None
                     m._ready = bits
-                model._dqrm_emb_ready = (ex, bits, mods)
+                _mset(model, "_dqrm_emb_ready", (ex, bits, mods))
         _mlp_grad_update(model, number_of_gpus, mlp_layer_quantized, group)
 
 
@@ -275,7 +281,7 @@ def _mlp_exchange(model, n: int, quantized: bool, group) -> DenseGradExchange | 
     ex = getattr(model, "_dqrm_dense_exchange", None)
     if ex is None or ex[0] != key:
         ex = (key, DenseGradExchange(layers, grad_bits=bits, group=group))
-        model._dqrm_dense_exchange = ex
+        _mset(model, "_dqrm_dense_exchange", ex)
     return ex[1]
 
 
@@ -291,7 +297,7 @@ def _mlp_grad_update(model, n: int, quantized: bool, group) -> None:
         _detach_grad(l.weight.grad)
         _detach_grad(l.bias.grad)
     ex.exchange()
-    model._dqrm_dense_ready = ex
+    _mset(model, "_dqrm_dense_ready", ex)
 
 
 def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embedding=True, num_gpus=1,
@@ -312,7 +318,7 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
                          repack=[m._use_packed(False) for m in bmods])
             for m in bmods:
                 m._ready = None
-            model._dqrm_emb_ready = None
+            _mset(model, "_dqrm_emb_ready", None)
         for m in mods:
             ready = getattr(m, "_ready", None)
             if ready is None:
@@ -337,12 +343,12 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
             if (ex.grad_bits != 32) != bool(mlp_layer_quantized):
                 raise ValueError("mlp_layer_quantized differs from the one used by grad_update_parallel_comm")
             ex.apply(lr)
-            model._dqrm_dense_ready = None
+            _mset(model, "_dqrm_dense_ready", None)
 
 
 def clear_gradients(model) -> None:
     """s_q_g_p_c.py:714-734, plus dropping any not-yet-exchanged embedding gradient."""
-    model._dqrm_emb_ready = None
+    _mset(model, "_dqrm_emb_ready", None)
     with torch.no_grad():
         for _, param in model.named_parameters():
             if param.grad is not None:
