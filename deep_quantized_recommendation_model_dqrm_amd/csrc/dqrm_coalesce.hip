@@ -1302,17 +1302,24 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                         sc[lane + i * WAVE] = r < nrows ? la.rowmax[rb + r] : 0.0f;
                     }
                 }
-                auto first_at_least = [&](int64_t row) {  // first entry with a row >= `row`
-                    int lo = 0, hi = nu0;
-                    while (lo < hi) {
-                        const int mid = (lo + hi) >> 1;
-                        if (r0 + (int64_t)krow(keys[hpos[ua0 + mid]]) < row) lo = mid + 1; else hi = mid;
+                if (nu0 <= 16 * WAVE) {  // every lane tests its entries (independent LDS reads, no search)
+                    for (int e = lane; e < nu0; e += WAVE) {
+                        const int64_t x = r0 + krow(keys[hpos[ua0 + e]]);
+                        if ((x >> 8) == blk) sc[x & (BLK - 1)] = s_newrm[e];
                     }
-                    return lo;
-                };
-                const int e0 = first_at_least(blk * BLK), e1 = first_at_least((blk + 1) * BLK);
-                for (int e = e0 + lane; e < e1; e += WAVE)
-                    sc[(r0 + krow(keys[hpos[ua0 + e]])) & (BLK - 1)] = s_newrm[e];
+                } else {
+                    auto first_at_least = [&](int64_t row) {  // first entry with a row >= `row`
+                        int lo = 0, hi = nu0;
+                        while (lo < hi) {
+                            const int mid = (lo + hi) >> 1;
+                            if (r0 + (int64_t)krow(keys[hpos[ua0 + mid]]) < row) lo = mid + 1; else hi = mid;
+                        }
+                        return lo;
+                    };
+                    const int e0 = first_at_least(blk * BLK), e1 = first_at_least((blk + 1) * BLK);
+                    for (int e = e0 + lane; e < e1; e += WAVE)
+                        sc[(r0 + krow(keys[hpos[ua0 + e]])) & (BLK - 1)] = s_newrm[e];
+                }
 #pragma unroll
                 for (int i = 0; i < BLK / WAVE; ++i) mv = fmaxf(mv, sc[lane + i * WAVE]);
             } else {
