@@ -119,8 +119,9 @@ PROFILE_TAG = {"terabyte": "tb", "terabyte_ref": "tbref", "terabyte_1g": "tb1g",
 KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 summary)
     "emb_fwd": "k_emb_fwd<{lpr},",
     "emb_fwd_packed": "k_emb_fwd_packed<{lpr},",
-    "bwd_coalesce": ("k_coalesce_p1<false>", "k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),  # Criteo form / general
-    "bwd_apply_local": ("k_coalesce_p1<true>",),  # N=1: coalesce + update in one launch
+    # Criteo form (<APPLY, row-major stage>; round-3 summaries: <APPLY>) / general
+    "bwd_coalesce": ("k_coalesce_p1<false,", "k_coalesce_p1<false>", "k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),
+    "bwd_apply_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),  # N=1: coalesce + update in one launch
     "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "grad_quant_pack": "k_quant_pack<{lpr}>",
     "apply_sparse_update": "k_apply_flat<{lpr},",

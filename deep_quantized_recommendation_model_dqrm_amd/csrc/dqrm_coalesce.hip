@@ -384,11 +384,57 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
     return acc;
 }
 
+// the same sum over a ROW-MAJOR stage: c[p * stride], p in [p, pe), strictly in order, G LDS
+// reads in flight while the previous G are added
+#ifndef DQRM_COAL_RMG
+#define DQRM_COAL_RMG 8
+#endif
+__device__ __forceinline__ float chain_sum_rm(const float* c, int p, int pe, int stride, float acc) {
+    constexpr int G = DQRM_COAL_RMG;
+    if (p + G <= pe) {
+        float x[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) x[j] = c[(p + j) * stride];
+        p += G;
+        while (p + G <= pe) {
+            float y[G];
+#pragma unroll
+            for (int j = 0; j < G; ++j) y[j] = c[(p + j) * stride];
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                acc = acc + x[j];
+                x[j] = y[j];
+            }
+            p += G;
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) acc = acc + x[j];
+    }
+    for (; p < pe; ++p) acc = acc + c[p * stride];
+    return acc;
+}
+
+// Stage layout. Row-major: sorted position / entry p's SW floats contiguous, so a float4 lands
+// with one conflict-free ds_write_b128 and a chain's 64 dimensions are 64 consecutive dwords;
+// dimension-major: column d holds dimension d of every position, so a float4 is 4 stores 4*SP
+// floats apart (8-way bank conflicts at SW = 64) but a chain is read 16 B at a time -- what
+// the long chains of a dimension-split table (a few rows, hundreds of lookups each) want; at
+// SW = 16 the dimension-major stores conflict only 2-way. Measured (same box, bench step):
+// row-major -1.0 us at D = 64 (terabyte), +2 us at D = 16 (kaggle). The layout is a template
+// parameter of the kernel (a per-workgroup runtime choice cost more than either layout):
+// DQRM_COAL_ROWMAJOR 1 (default) row-major for D >= 32; 0 never, 2 always (A/B builds).
+#ifndef DQRM_COAL_ROWMAJOR
+#define DQRM_COAL_ROWMAJOR 1
+#endif
+
 #ifndef DQRM_COAL_WPF
 #define DQRM_COAL_WPF 4
 #endif
 #ifndef DQRM_COAL_WLATE
-#define DQRM_COAL_WLATE 1
+#define DQRM_COAL_WLATE 0  // 1: an A/B build issuing the W prefetch after the land phase
+#endif
+#ifndef DQRM_COAL_CAND
+#define DQRM_COAL_CAND 0  // 1: an A/B build prefetching candidate blocks' row maxima during the rendezvous
 #endif
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
 constexpr int WPFA = WPF > 0 ? WPF : 1;  // array extent (WPF = 0: no early W loads, an A/B build)
@@ -429,7 +475,7 @@ static_assert(MAXB < (1 << 13), "distinct-row count field of a granule");
 // re-reduced here, superblock / table growth by atomicMax, shrunk superblocks flagged for the
 // table's last workgroup. The W rows are loaded before the segment phase, so the update's
 // random-row latency hides behind the coalesce.
-template <bool APPLY>
+template <bool APPLY, bool RM>
 __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs a, dqrm_internal::LocalApplyArgs la) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int s_cnt[MAXI * NW];
@@ -519,8 +565,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         r1 = r1 < nrows ? r1 : nrows;
     }
     const bool active = dsplit ? s < DS : r0 < r1;
-    const int SP = (STAGE_FLOATS / SW) & ~3;  // column pitch (16-B columns)
+    const int SP = (STAGE_FLOATS / SW) & ~3;  // stage entries (dimension-major: the column pitch, 16-B columns)
     const int CE = SP - 4;                    // stage entries per chunk
+    constexpr bool rmaj = RM;
+    // stage index of (entry p, dimension d)
+    auto sx = [&](int p, int d) -> int { return rmaj ? p * SW + d : d * SP + p; };
     const float* dyt = a.dy + (int64_t)t * a.dst_t;
     // fused update: this launch's epoch = this slot's previous granule epoch + 1 (every slot
     // of a table publishes once per launch, so the table's granules always agree)
@@ -915,9 +964,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         otm = la.tmax[t];
     }
     // the W rows and block maxima of the entries this workgroup will update, in flight across
-    // the segment phase and the wait for the table's other workgroups: issued once the dy
-    // prefetch registers are free (DQRM_COAL_WLATE, the default: the two register sets are
-    // never live together), or before the land phase
+    // the land and segment phases and the wait for the table's other workgroups: issued before
+    // the land phase (the default; at WPF = 4 both register sets fit the 128-VGPR budget), or
+    // once the dy prefetch registers are free (DQRM_COAL_WLATE=1, an A/B build)
     auto issue_w = [&]() {
         if constexpr (APPLY) {
 #pragma unroll
@@ -952,15 +1001,24 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             e = s_cb[sl] + (u - s_uf[sl]);
         }
         if (e < s_cb[sl + 1]) {
-            if (lds_vals) stage[d * SP + vb0 + u] = acc;
+            if (lds_vals) stage[sx(vb0 + u, d)] = acc;
             else if (APPLY && dsplit) st_wt(a.ws_vals + e * a.D + q0 * 4 + d, acc);
             else a.ws_vals[e * a.D + q0 * 4 + d] = acc;
             if (j == 0 && q0 == 0 && d == 0) a.ws_rows[e] = (int32_t)row;
         }
         amax = fmaxf(amax, fabsf(acc));
     };
-    auto put = [&](float* col, float4 v) {
-        col[0] = v.x; col[SP] = v.y; col[2 * SP] = v.z; col[3 * SP] = v.w;
+    auto put = [&](int p, int sub, float4 v) {  // entry p, dimensions 4*sub .. 4*sub+3
+        if (rmaj) {
+            *reinterpret_cast<float4*>(stage + p * SW + sub * 4) = v;
+        } else {
+            float* col = stage + (sub * 4) * SP + p;
+            col[0] = v.x; col[SP] = v.y; col[2 * SP] = v.z; col[3 * SP] = v.w;
+        }
+    };
+    // strictly ordered sum of dimension d over entries [p, pe), starting from acc
+    auto chain = [&](int d, int p, int pe, float acc) -> float {
+        return rmaj ? chain_sum_rm(stage + d, p, pe, SW, acc) : chain_sum(stage + d * SP, p, pe, acc);
     };
     if (n - NS <= CE) {
         // 4. one chunk. Every value first goes where it belongs -- a single-lookup segment's
@@ -972,13 +1030,13 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const int p = pos[q >> lg_sh];
             if (p == 0xFFFF) return -1;
             const int e = sdest[p];
-            if (e < 0) put(stage + ((q & (LG - 1)) * 4) * SP + (-e - 1), v);
+            if (e < 0) put(-e - 1, q & (LG - 1), v);
             return e;
         };
         auto store = [&](int q, int e, float4 v) {  // a single-lookup segment's output row
             if (e < 0 || e >= s_cb[SPLIT]) return;
             if (lds_vals) {
-                put(stage + ((q & (LG - 1)) * 4) * SP + vb0 + (int)(e - ebase()), v);
+                put(vb0 + (int)(e - ebase()), q & (LG - 1), v);
             } else {
                 float4* dst = reinterpret_cast<float4*>(a.ws_vals + (int64_t)e * a.D) + q0 + (q & (LG - 1));
                 if (APPLY && dsplit) st4_wt(dst, v);
@@ -1015,8 +1073,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const int u = mlist[i >> sw_sh], d = i & (SW - 1);
             const int h = hpos[u], len = hpos[u + 1] - h;
             const int st = -sdest[h] - 1;  // the segment's first stage entry
-            const float* col = stage + d * SP;
-            emit(u, d, chain_sum(col, st + 1, st + len, col[st]));
+            emit(u, d, chain(d, st + 1, st + len, stage[sx(st, d)]));
         }
     } else {
         // a slot larger than the stage: chunks of CE sorted lookups, loaded after the sort;
@@ -1027,7 +1084,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const int ce = n - c0 < CE ? n - c0 : CE;
             for (int q = tid; q < (ce << lg_sh); q += TPB) {
                 const int p = c0 + (q >> lg_sh), sub = q & (LG - 1);
-                put(stage + (sub * 4) * SP + (p - c0), finish(fetch(kbag(keys[p]), sub)));
+                put(p - c0, sub, finish(fetch(kbag(keys[p]), sub)));
             }
             __syncthreads();
             auto seg_of = [&](int p) {  // segment holding sorted position p
@@ -1043,9 +1100,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             for (int i = first + ((tid - first) % TPB + TPB) % TPB; i < ((ub + 1) << sw_sh); i += TPB) {
                 const int u = i >> sw_sh, d = i & (SW - 1);
                 const int h = hpos[u], e1 = hpos[u + 1];
-                const float* col = stage + d * SP - c0;
                 const int pe = e1 < c0 + ce ? e1 : c0 + ce;
-                const float acc = h >= c0 ? chain_sum(col, h + 1, pe, col[h]) : chain_sum(col, c0, pe, carry);
+                const float acc = h >= c0 ? chain(d, h + 1 - c0, pe - c0, stage[sx(h - c0, d)])
+                                          : chain(d, 0, pe - c0, carry);
                 if (e1 > c0 + ce) {
                     carry = acc;
                     continue;
@@ -1080,7 +1137,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // to re-reduce -- and copies the first such block's 256 stored row maxima into its LDS
         // cache (the pos / mlist regions, dead by now). Rows of a block are updated only by this
         // workgroup, so the copy stays exact for the untouched rows.
-        if (!dsplit && w > 0) {
+        if (DQRM_COAL_CAND && !dsplit && w > 0) {
             int cb = -1;
 #pragma unroll
             for (int jj = 0; jj < WPF; ++jj) {
@@ -1111,7 +1168,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             if (lane == 0) s_cand_blk[w] = cb;
         }
         if (w == 0 && tid < CAND_SLOTS) {
-            if (tid == 0 || dsplit) s_cand_blk[tid] = -1;
+            if (tid == 0 || dsplit || !DQRM_COAL_CAND) s_cand_blk[tid] = -1;
         }
     }
     if (APPLY && tid < WAVE) {  // wave 0: lane j polls slot j's granule until it shows this launch's epoch
@@ -1242,6 +1299,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // dimension-split table's rows hold the slices of all its workgroups (sc1 loads)
         auto load_val = [&](const float* vb, int q) -> float4 {
             if (lds_vals) {  // entry q >> lpr_sh, float4 q & (LPR-1), from the stage columns
+                if (rmaj)
+                    return *reinterpret_cast<const float4*>(stage + (vb0 + (q >> lpr_sh)) * SW + (q & (LPR - 1)) * 4);
                 const float* c = stage + (q & (LPR - 1)) * 4 * SP + vb0 + (q >> lpr_sh);
                 return make_float4(c[0], c[SP], c[2 * SP], c[3 * SP]);
             }
@@ -1377,11 +1436,12 @@ hipError_t allow_coalesce_lds() {
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
-        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1<false>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        if (attr == hipSuccess)
-            attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_coalesce_p1<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        const void* fns[] = {reinterpret_cast<const void*>(k_coalesce_p1<false, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<false, true>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, true>)};
+        for (const void* f : fns)
+            if (attr == hipSuccess) attr = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     });
     return attr;
 }
@@ -1429,9 +1489,12 @@ bool coalesce_apply_resident(int T, hipStream_t stream) {
         int cus = 0, occ = 0;
         if (allow_coalesce_lds() != hipSuccess) return;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k_coalesce_p1<true>),
-                                                         TPB, LDS_BYTES) != hipSuccess)
-            return;
+        for (const void* f : {reinterpret_cast<const void*>(k_coalesce_p1<true, false>),
+                              reinterpret_cast<const void*>(k_coalesce_p1<true, true>)}) {
+            int o = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, TPB, LDS_BYTES) != hipSuccess) return;
+            occ = occ == 0 || o < occ ? o : occ;
+        }
         d.cus = cus;
         d.occ = occ;
     });
@@ -1457,11 +1520,14 @@ hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la
     const hipError_t attr = allow_coalesce_lds();
     if (attr != hipSuccess) return attr;
     const dim3 grid((a.T + 7) / 8 * 64);
+    const bool rm = DQRM_COAL_ROWMAJOR == 2 || (DQRM_COAL_ROWMAJOR == 1 && a.D >= 32);  // stage layout
     if (la) {
         if (!coalesce_apply_resident(a.T, stream)) return hipErrorInvalidValue;  // not all resident at once
-        hipLaunchKernelGGL(k_coalesce_p1<true>, grid, dim3(TPB), LDS_BYTES, stream, a, *la);
+        if (rm) hipLaunchKernelGGL((k_coalesce_p1<true, true>), grid, dim3(TPB), LDS_BYTES, stream, a, *la);
+        else hipLaunchKernelGGL((k_coalesce_p1<true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, *la);
     } else {
-        hipLaunchKernelGGL(k_coalesce_p1<false>, grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
+        if (rm) hipLaunchKernelGGL((k_coalesce_p1<false, true>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
+        else hipLaunchKernelGGL((k_coalesce_p1<false, false>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
     }
     return hipGetLastError();
 }
