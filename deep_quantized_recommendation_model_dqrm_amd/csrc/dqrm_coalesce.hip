@@ -49,8 +49,8 @@ namespace {
 // Diagnostic build only (-DDQRM_DIAG_CLOCK, tools/diag_coalesce.py): thread 0 of every
 // workgroup stamps the 100 MHz wall clock at phase boundaries.
 #ifdef DQRM_DIAG_CLOCK
-__device__ unsigned long long g_coal_clk[8192 * 16];
-#define CDIAG(ph) do { if (threadIdx.x == 0) g_coal_clk[kd * 16 + (ph)] = wall_clock64(); } while (0)
+__device__ unsigned long long g_coal_clk[8192 * 32];
+#define CDIAG(ph) do { if (threadIdx.x == 0) g_coal_clk[kd * 32 + (ph)] = wall_clock64(); } while (0)
 #define CDIAG_W(ph) do { __builtin_amdgcn_s_waitcnt(0); CDIAG(ph); } while (0)
 #else
 #define CDIAG(k) do { } while (0)
@@ -385,7 +385,8 @@ __device__ __forceinline__ float chain_sum(const float* col, int p, int pe, floa
 }
 
 // the same sum over a ROW-MAJOR stage: c[p * stride], p in [p, pe), strictly in order, G LDS
-// reads in flight while the previous G are added
+// reads in flight while the previous G are added (measured: G = 16 / 32, or batches predicated
+// to the chain's end, were slower on the 680-long chains of the 3-row tables)
 #ifndef DQRM_COAL_RMG
 #define DQRM_COAL_RMG 8
 #endif
@@ -434,8 +435,8 @@ __device__ __forceinline__ float chain_sum_rm(const float* c, int p, int pe, int
 #define DQRM_COAL_WLATE 0  // 1: an A/B build issuing the W prefetch after the land phase
 #endif
 #ifndef DQRM_COAL_CAND
-#define DQRM_COAL_CAND 0  // 1: an A/B build prefetching candidate blocks' row maxima during the rendezvous
-#endif
+#define DQRM_COAL_CAND 0  // A/B builds: 1 prefetch candidate blocks' row maxima during the rendezvous,
+#endif                    // 2 the same unless the table already met
 constexpr int WPF = DQRM_COAL_WPF;  // fused update: W float4 per thread loaded during the segment phase
 constexpr int WPFA = WPF > 0 ? WPF : 1;  // array extent (WPF = 0: no early W loads, an A/B build)
 constexpr int OWN_Q = 64;           // fused update: shrunk block-max holders re-reduced in the launch
@@ -490,6 +491,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ float s_am;
     __shared__ int s_stall;
     __shared__ int s_upart;
+    __shared__ uint32_t s_epoch;
     __shared__ float s_sbm[SBC];            // fused update: sblkmax of the slot's superblocks
     __shared__ int s_cand_blk[CAND_SLOTS];  // fused update: block cached by wave w's row-max slot (-1: none)
     __shared__ int s_oq_n;
@@ -578,6 +580,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if (APPLY && tid < WAVE)
         epoch = (gr_epoch(__hip_atomic_load(gran + s + SPLIT * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u) &
                 GR_EPOCH_MASK;
+    if (DQRM_COAL_CAND == 2 && APPLY && tid == 0) s_epoch = epoch;  // (read after the barriers below)
     auto fetch = [&](int b, int sub) -> float4 {
         return reinterpret_cast<const float4*>(dyt + (int64_t)b * a.dst_b)[q0 + sub];
     };
@@ -1073,7 +1076,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const int u = mlist[i >> sw_sh], d = i & (SW - 1);
             const int h = hpos[u], len = hpos[u + 1] - h;
             const int st = -sdest[h] - 1;  // the segment's first stage entry
-            emit(u, d, chain(d, st + 1, st + len, stage[sx(st, d)]));
+            emit(u, d, chain(d, st, st + len, -0.0f));  // -0 + x == x for every x: the first value exactly
         }
     } else {
         // a slot larger than the stage: chunks of CE sorted lookups, loaded after the sort;
@@ -1101,8 +1104,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 const int u = i >> sw_sh, d = i & (SW - 1);
                 const int h = hpos[u], e1 = hpos[u + 1];
                 const int pe = e1 < c0 + ce ? e1 : c0 + ce;
-                const float acc = h >= c0 ? chain(d, h + 1 - c0, pe - c0, stage[sx(h - c0, d)])
-                                          : chain(d, 0, pe - c0, carry);
+                const float acc = h >= c0 ? chain(d, h - c0, pe - c0, -0.0f) : chain(d, 0, pe - c0, carry);
                 if (e1 > c0 + ce) {
                     carry = acc;
                     continue;
@@ -1139,8 +1141,15 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // workgroup, so the copy stays exact for the untouched rows.
         if (DQRM_COAL_CAND && !dsplit && w > 0) {
             int cb = -1;
+            bool met = false;
+            if (DQRM_COAL_CAND == 2) {  // the table already met (this workgroup came last): nothing to hide behind
+                const int l = tid % WAVE;
+                const bool ok = l >= NG || gr_epoch(__hip_atomic_load(gran + l, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT)) == s_epoch;
+                met = __all(ok);
+            }
 #pragma unroll
-            for (int jj = 0; jj < WPF; ++jj) {
+            for (int jj = 0; jj < WPF && !met; ++jj) {
                 const int q = tid + TPB * jj;
                 const bool in = q < (nu0 << lpr_sh);
                 float orm = in ? abs_max4(wpf[jj]) : -1.0f;
@@ -1231,6 +1240,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if constexpr (APPLY) {
         __syncthreads();
         CDIAG(11);
+        CDIAG_W(16);  // (diagnostic build: every load of the workgroup landed, the W prefetch included)
         // the update of dqrm_apply_local: s = clamp(max|g|, 1e-8) / (2^(bits-1)-1) (* 1/N,
         // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
         const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
@@ -1295,17 +1305,25 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 }
             }
         };
-        // a row split reads back its own values (plain loads after the workgroup barrier); a
-        // dimension-split table's rows hold the slices of all its workgroups (sc1 loads)
-        auto load_val = [&](const float* vb, int q) -> float4 {
-            if (lds_vals) {  // entry q >> lpr_sh, float4 q & (LPR-1), from the stage columns
-                if (rmaj)
-                    return *reinterpret_cast<const float4*>(stage + (vb0 + (q >> lpr_sh)) * SW + (q & (LPR - 1)) * 4);
-                const float* c = stage + (q & (LPR - 1)) * 4 * SP + vb0 + (q >> lpr_sh);
-                return make_float4(c[0], c[SP], c[2 * SP], c[3 * SP]);
-            }
+        // the values: from the LDS stage (lds_vals), else a row split reads back its own values
+        // (plain loads after the workgroup barrier) and a dimension-split table's rows hold the
+        // slices of all its workgroups (sc1 loads)
+        auto lds_val = [&](int q) -> float4 {  // entry q >> lpr_sh, float4 q & (LPR-1)
+            if (rmaj)
+                return *reinterpret_cast<const float4*>(stage + (vb0 + (q >> lpr_sh)) * SW + (q & (LPR - 1)) * 4);
+            const float* c = stage + (q & (LPR - 1)) * 4 * SP + vb0 + (q >> lpr_sh);
+            return make_float4(c[0], c[SP], c[2 * SP], c[3 * SP]);
+        };
+        auto mem_val = [&](const float* vb, int q) -> float4 {
             return dsplit ? ld4_sc1(vb, (uint32_t)q * 16u) : reinterpret_cast<const float4*>(vb)[q];
         };
+        auto load_val = [&](const float* vb, int q) -> float4 { return lds_vals ? lds_val(q) : mem_val(vb, q); };
+        // vmcnt counts loads and stores in issue order: a load still pending when the update's
+        // stores have been issued is waited for with vmcnt(0), i.e. after every one of them. So
+        // the prefetched W rows and block maxima (landed during the rendezvous) are waited for
+        // here, once (a real s_waitcnt vmcnt(0) the compiler's wait tracking sees; they landed
+        // during the rendezvous), and values read from memory likewise before their updates.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt / lgkmcnt not waited
         for (int sl = s, j0 = 0; go && sl < SPLIT; sl += NA, j0 = 1) {  // uniform
             int ua, nu;
             slot_entries(sl, ua, nu);
@@ -1316,9 +1334,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 #pragma unroll
                 for (int jh = 0; jh < WPF; jh += 2) {
                     float4 v[2];
+                    if (lds_vals) {
 #pragma unroll
-                    for (int j = jh; j < jh + 2 && j < WPF; ++j)
-                        v[j - jh] = q + TPB * j < nit ? load_val(vb, q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        for (int j = jh; j < jh + 2 && j < WPF; ++j)
+                            v[j - jh] = q + TPB * j < nit ? lds_val(q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    } else {  // landed before the updates' stores (else every later use waits for them too)
+#pragma unroll
+                        for (int j = jh; j < jh + 2 && j < WPF; ++j)
+                            v[j - jh] = q + TPB * j < nit ? mem_val(vb, q + TPB * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        __builtin_amdgcn_s_waitcnt(0x0F70);
+                    }
 #pragma unroll
                     for (int j = jh; j < jh + 2 && j < WPF; ++j)
                         if (q + TPB * j < nit) update(ua, q + TPB * j, wpf[j], bpf[j], v[j - jh]);

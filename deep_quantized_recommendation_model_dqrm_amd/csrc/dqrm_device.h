@@ -112,10 +112,13 @@ DQRM_INLINE void st_w(float* p, float v, bool wt) {
 
 // dirty flags (u8 arrays sdirty / bdirty) are set / cleared by device-scope atomics on their
 // aligned 32-bit word and read with sc1 word loads (the arrays are padded to whole words)
+// (the word pointer is derived from f by pointer arithmetic, not through an integer, so the
+// compiler keeps f's global address space: global atomics, not flat ones -- a pending flat
+// atomic makes every later LDS access wait for all of the wave's stores, vmcnt(0) lgkmcnt(0))
 DQRM_INLINE uint32_t* flag_word(const uint8_t* f, int64_t i, int* sh) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(f + i);
-    *sh = (int)(a & 3u) * 8;
-    return reinterpret_cast<uint32_t*>(a & ~(uintptr_t)3u);
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(f + i) & 3u);
+    *sh = (int)mis * 8;
+    return reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(f + i - mis));
 }
 DQRM_INLINE void flag_set(uint8_t* f, int64_t i) {
     int sh;

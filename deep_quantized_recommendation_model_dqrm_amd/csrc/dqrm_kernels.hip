@@ -270,17 +270,33 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
     const int grp = threadIdx.x / LPR;
     const int D = LPR * 4;
 
+    // Every global load of a phase is issued unconditionally (addresses clamped into the
+    // arrays, the values of invalid bags / lookups dropped afterwards), so the UNR bags' index
+    // loads and then their row loads are in flight together: a per-bag branch around a load
+    // made the compiler wait for each one before the next (one round trip per bag).
+    const bool p1 = a.pool1 && L == B;
     for (int64_t b0 = (int64_t)blockIdx.x * (G * UNR); b0 < B; b0 += (int64_t)gridDim.x * (G * UNR)) {
         int64_t beg[UNR], len[UNR], row[UNR];
         // phase 1: offsets
+        int64_t s0v[UNR], s1v[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            const int64_t b = b0 + k * G + grp;
+            const int64_t bb = b < B ? b : 0;
+            if (p1) {
+                s0v[k] = bb;
+                s1v[k] = bb + 1;
+            } else {
+                s0v[k] = off[bb];
+                s1v[k] = off[bb + 1 < B ? bb + 1 : bb];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
             const int64_t b = b0 + k * G + grp;
             const bool valid = b < B;
-            const int64_t bb = valid ? b : 0;
-            const bool p1 = a.pool1 && L == B;
-            int64_t s0 = p1 ? bb : off[bb];
-            int64_t s1 = p1 ? bb + 1 : ((bb + 1 < B) ? off[bb + 1] : L);
+            int64_t s0 = s0v[k];
+            int64_t s1 = (p1 || b + 1 < B) ? s1v[k] : L;
             if (s0 < 0 || s1 > L || s1 < s0) {
                 if (valid && lane == 0) flag_error(a.err, DQRM_ERRF_OFFSET);
                 s0 = s0 < 0 ? 0 : (s0 > L ? L : s0);
@@ -290,32 +306,44 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
             len[k] = valid ? s1 - s0 : -1;  // -1: no such bag
         }
         // phase 2: single-lookup indices
+        int64_t rv[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) rv[k] = L > 0 ? idx[beg[k] < L ? beg[k] : L - 1] : -1;
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
             row[k] = -1;
             if (len[k] == 1) {
-                int64_t rr = idx[beg[k]];
-                if (rr < 0 || rr >= nrows) {
+                if (rv[k] < 0 || rv[k] >= nrows) {
                     if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
-                    rr = -1;
+                } else {
+                    row[k] = rv[k];
                 }
-                row[k] = rr;
             }
         }
-        // phase 3: row loads for single-lookup bags
+        // phase 3: row loads for single-lookup bags (row 0 of the table for the others, dropped)
         float4 acc[UNR];
         uint32_t pk[UNR];
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             pk[k] = 0x8888u;  // q = 0
-            if (row[k] >= 0) {
-                const int64_t grow = rowbase + row[k];
-                if (use_packed)
-                    pk[k] = reinterpret_cast<const uint16_t*>(a.packed + grow * (D / 2))[lane];
-                else
-                    acc[k] = reinterpret_cast<const float4*>(a.W + grow * D)[lane];
+        }
+        if (nrows > 0) {
+            if (use_packed) {
+#pragma unroll
+                for (int k = 0; k < UNR; ++k)
+                    pk[k] = reinterpret_cast<const uint16_t*>(a.packed + (rowbase + (row[k] >= 0 ? row[k] : 0)) * (D / 2))[lane];
+            } else {
+#pragma unroll
+                for (int k = 0; k < UNR; ++k)
+                    acc[k] = reinterpret_cast<const float4*>(a.W + (rowbase + (row[k] >= 0 ? row[k] : 0)) * D)[lane];
             }
+#pragma unroll
+            for (int k = 0; k < UNR; ++k)
+                if (row[k] < 0) {
+                    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    pk[k] = 0x8888u;
+                }
         }
         // phase 4: pooled sums for multi-lookup bags (bag order, FP32), quantize, store
 #pragma unroll

@@ -3,7 +3,8 @@ diagnostic build (tools/build_diag_coal.sh). Stamps: 0 start, 1 indices landed, 
 compacted, 3 sorted, 4 heads, 5 stage landed, 6 segments done (stores issued), 7 end (a
 table's slowest workgroup over its slots and, in the one-launch step, sub-slots); with
 "apply" (the one-launch local step, dqrm_emb_bwd_apply_local): 11 the table's workgroups
-met, 12 rows updated, 13 end (after the table's last-workgroup finalize).
+met, 16 every load landed (the W prefetch), 14 prefetched rows updated, 15 all rows
+updated, 12 owned blocks re-reduced, 13 end (after the table's last-workgroup finalize).
 usage: python tools/diag_coalesce.py [terabyte|terabyte_ref|kaggle] [B] [apply]"""
 import ctypes as C
 import os
@@ -28,6 +29,7 @@ lib = L.load()
 lib.dqrm_diag_coal_read.argtypes = [C.c_void_p, C.c_int]
 ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
 g = torch.Generator(device="cuda").manual_seed(5)
+NS = 32  # stamp slots per workgroup (dqrm_coalesce.hip g_coal_clk)
 NB = 8  # distinct resident batches cycled, as bench.py (cold rows and translations every launch)
 bs = [dq.LookupBatch.pooling_one(torch.stack([torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows]))
       for _ in range(NB)]
@@ -51,12 +53,12 @@ for i in range(3 * NB):
 torch.cuda.synchronize()
 cs = []
 for i in range(NB):  # one launch per batch, read after each
-    buf = np.zeros(2 * T * 8 * 16, dtype=np.uint64)
+    buf = np.zeros(2 * T * 8 * NS, dtype=np.uint64)
     run(i)
     lib.dqrm_diag_coal_read(buf.ctypes.data, buf.size)
     # rows: sub-slot 0 of every (table, slot), then sub-slot 1 (the spare groups of the
     # one-launch step); per table 16 "slots": 0-7 sub-slot 0, 8-15 sub-slot 1
-    c = buf.reshape(2, T, 8, 16).transpose(1, 0, 2, 3).reshape(T, 16, 16).astype(np.int64)
+    c = buf.reshape(2, T, 8, NS).transpose(1, 0, 2, 3).reshape(T, 16, NS).astype(np.int64)
     k0 = c[:, :, 0][c[:, :, 0] > 0].min()
     c = np.where(c >= k0, c - k0, -1)  # -1: not stamped in this launch
     cs.append(c)
@@ -92,8 +94,9 @@ if APPLY:
         ps = [slow(c, t, 13) for c in cs]
         if ps[0][11] < 0:
             continue
-        ph = np.median([[p[11] - p[6], p[12] - p[11], p[13] - p[12], p[13], p[14] - p[11], p[15] - p[14],
-                         p[12] - p[15]] for p in ps], axis=0) / 100
+        ph = np.median([[p[11] - p[6], p[12] - p[11], p[13] - p[12], p[13], p[16] - p[11], p[14] - p[16],
+                         p[15] - p[14], p[12] - p[15]] for p in ps], axis=0) / 100
         print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} {ph[1]:5.1f} {ph[2]:5.1f} || {ph[3]:5.1f}   "
-              f"(updated = values+prefetched rows {ph[4]:4.1f} | rest+barrier {ph[5]:4.1f} | re-reduce {ph[6]:4.1f})")
+              f"(updated = W landed {ph[4]:4.1f} | prefetched rows {ph[5]:4.1f} | rest+barrier {ph[6]:4.1f} | "
+              f"re-reduce {ph[7]:4.1f})")
 print("errors", ts.read_errors())

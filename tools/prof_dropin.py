@@ -87,11 +87,16 @@ for i in range(steps):
     step(i)
 torch.cuda.synchronize()
 print(f"{kind}: {(time.perf_counter() - t0) / steps * 1e6:.1f} us/step")
+# cProfile sees the calling thread only: run the backward there (not on the autograd engine's
+# device thread), so the backward's Python functions show up under their own names
+torch.autograd.set_multithreading_enabled(False)
 pr = cProfile.Profile()
 pr.enable()
 for i in range(steps):
     step(i)
 torch.cuda.synchronize()
 pr.disable()
+torch.autograd.set_multithreading_enabled(True)
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(25)
+st.sort_stats("tottime").print_stats(30)
+st.sort_stats("cumulative").print_stats(30)
