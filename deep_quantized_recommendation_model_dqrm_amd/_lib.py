@@ -51,7 +51,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 6  # include/dqrm.h
+DQRM_ABI_VERSION = 7  # include/dqrm.h
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_bwd_coalesce_scaled",
     "dqrm_emb_bwd_lookup_grad",
     "dqrm_rows_changed",
+    "dqrm_emb_fwd_after_update",
     "dqrm_payload_bytes",
     "dqrm_grad_quant_pack",
     "dqrm_grad_quant_pack_strided",
@@ -195,6 +196,10 @@ def load(path: str | None = None) -> C.CDLL:
         ),
         "dqrm_emb_bwd_lookup_grad": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P]),
         "dqrm_rows_changed": (C.c_int, [TS, P, C.c_int64, C.c_int, P]),
+        "dqrm_emb_fwd_after_update": (
+            C.c_int,
+            [TS, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P, C.c_int64, C.c_int, P],
+        ),
         "dqrm_payload_bytes": (C.c_size_t, [C.c_int, C.c_int64, C.c_int, C.c_int]),
         "dqrm_grad_quant_pack": (
             C.c_int,

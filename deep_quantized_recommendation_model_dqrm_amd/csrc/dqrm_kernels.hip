@@ -242,18 +242,17 @@ struct FwdArgs {
     int pool1;  // DQRM_BATCH_POOLING_ONE: bag b of every table is lookup b (offsets unread)
 };
 
-template <int LPR, int UNR>
-__global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
-    // grid = (bag chunks, tables): the table index is blockIdx.y, so every per-table value
-    // below is wave-uniform (scalar registers) and no 64-bit division is needed per bag.
-    const int t = blockIdx.y;
+// Table t's bags, workgroup bx of gx (the body of k_emb_fwd; WT: the table max was just
+// written by this workgroup -- k_fwd_after_update -- and is read write-through)
+template <int LPR, int UNR, bool WT>
+__device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t bx, int64_t gx) {
     const bool full_precision = (a.flags & DQRM_FWD_FULL_PRECISION) != 0;
     const bool refresh = (a.flags & DQRM_FWD_REFRESH_SCALE) != 0;
     const bool use_packed = (a.flags & DQRM_FWD_USE_PACKED) != 0 && !full_precision;
     float s = 1.0f;
-    if (!full_precision) s = refresh ? sym_scale(a.tmax[t], a.bits) : a.scale[t];
+    if (!full_precision) s = refresh ? sym_scale(WT ? ld_wt(a.tmax + t) : a.tmax[t], a.bits) : a.scale[t];
     const float r = 1.0f / s;
-    if (refresh && !full_precision && blockIdx.x == 0 && threadIdx.x == 0) a.scale[t] = s;
+    if (refresh && !full_precision && bx == 0 && threadIdx.x == 0) a.scale[t] = s;
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
     // Criteo form: table t's lookups are idx[t*B, (t+1)*B) -- no idx_base round trip in front of the index loads
     const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
@@ -275,7 +274,7 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
     // loads and then their row loads are in flight together: a per-bag branch around a load
     // made the compiler wait for each one before the next (one round trip per bag).
     const bool p1 = a.pool1 && L == B;
-    for (int64_t b0 = (int64_t)blockIdx.x * (G * UNR); b0 < B; b0 += (int64_t)gridDim.x * (G * UNR)) {
+    for (int64_t b0 = bx * (G * UNR); b0 < B; b0 += gx * (G * UNR)) {
         int64_t beg[UNR], len[UNR], row[UNR];
         // phase 1: offsets
         int64_t s0v[UNR], s1v[UNR];
@@ -383,6 +382,13 @@ __global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
             reinterpret_cast<float4*>(out + b * a.ost_b)[lane] = y;
         }
     }
+}
+
+template <int LPR, int UNR>
+__global__ void __launch_bounds__(256) k_emb_fwd(FwdArgs a) {
+    // grid = (bag chunks, tables): the table index is blockIdx.y, so every per-table value
+    // is wave-uniform (scalar registers) and no 64-bit division is needed per bag.
+    emb_fwd_table<LPR, UNR, false>(a, blockIdx.y, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3538,6 +3544,43 @@ __global__ void __launch_bounds__(256) k_rows_changed(const float* __restrict__ 
     }
 }
 
+// One workgroup, a one-table set: k_rows_changed's work and finalize for the rows an optimizer
+// rewrote, then the table's forward with the refreshed scale -- the per-table module's
+// external-update sync and its forward as ONE launch (the drivers call 26 modules a step).
+template <int LPR>
+__global__ void __launch_bounds__(256) k_fwd_after_update(FwdArgs a, float* __restrict__ rowmax,
+                                                          uint8_t* __restrict__ bdirty, uint8_t* __restrict__ sdirty,
+                                                          float* __restrict__ blkmax, float* __restrict__ sblkmax,
+                                                          float* __restrict__ tmax, const int64_t* __restrict__ rows,
+                                                          int64_t n, int64_t total) {
+    constexpr int G = 256 / LPR;
+    const int lane = threadIdx.x % LPR;
+    const Meta m = make_meta(a.meta, 1);
+    for (int64_t i = threadIdx.x / LPR; i < n; i += G) {
+        const int64_t g = rows[i];
+        if (g < 0 || g >= total) {
+            if (lane == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+            continue;
+        }
+        const float4 w = reinterpret_cast<const float4*>(a.W + g * (LPR * 4))[lane];
+        float v = abs_max4(w);
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, LPR));
+        if (lane == 0) {
+            st_wt(rowmax + g, v);
+            flag_set(bdirty, g / BLK);
+            flag_set(sdirty, g / ((int64_t)BLK * SBLK_BLOCKS));
+        }
+    }
+    // the row maxima and flags landed (write-through) before the finalize reads them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    finalize_table<true>(m, 0, a.W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, LPR * 4, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    emb_fwd_table<LPR, 4, true>(a, 0, 0, 1);
+}
+
 // ------------------------------------------------------------------------------------
 // Per-lookup (uncoalesced) sparse gradient, the form nn.EmbeddingBag(sparse=True) hands to
 // autograd (embedding_bag_backward's sparse branch: indices = the input indices, values =
@@ -3839,26 +3882,34 @@ int dqrm_refresh_scale_and_pack(const dqrm_table_set* set, int bits, void* strea
     return DQRM_OK;
 }
 
-int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags,
-                 float* out, int64_t out_stride_t, int64_t out_stride_b, void* stream) {
+// the forward's argument checks and kernel arguments (shared by the two forward entry points)
+static int fwd_args(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags, float* out,
+                    int64_t out_stride_t, int64_t out_stride_b, const char* who, FwdArgs* a) {
     int rc = check_set(set);
     if (rc) return rc;
     if (!batch || !batch->idx || !batch->off || !batch->idx_base || !out)
-        return set_error(DQRM_E_INVALID, "%s: null batch/out pointer", "dqrm_emb_fwd");
+        return set_error(DQRM_E_INVALID, "%s: null batch/out pointer", who);
     if (!(flags & DQRM_FWD_FULL_PRECISION) && (bits < 2 || bits > 16))
-        return set_error(DQRM_E_INVALID, "%s: embedding_bit %d unsupported", "dqrm_emb_fwd", bits);
+        return set_error(DQRM_E_INVALID, "%s: embedding_bit %d unsupported", who, bits);
     if ((flags & DQRM_FWD_USE_PACKED) && (!set->packed || bits != 4))
-        return set_error(DQRM_E_INVALID, "%s: packed path needs packed rows and bits == 4", "dqrm_emb_fwd");
+        return set_error(DQRM_E_INVALID, "%s: packed path needs packed rows and bits == 4", who);
     if ((((uintptr_t)out) & 15) || (out_stride_t & 3) || (out_stride_b & 3))
-        return set_error(DQRM_E_INVALID, "%s: out must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_fwd");
-    if (batch->num_bags <= 0) return DQRM_OK;
+        return set_error(DQRM_E_INVALID, "%s: out must be 16-B aligned with strides %% 4 == 0", who);
+    a->W = set->W; a->packed = set->packed; a->tmax = set->tmax; a->scale = set->scale;
+    a->meta = set->meta; a->err = set->err;
+    a->idx = batch->idx; a->off = batch->off; a->idx_base = batch->idx_base;
+    a->pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    a->out = out; a->B = batch->num_bags; a->ost_t = out_stride_t; a->ost_b = out_stride_b;
+    a->T = set->num_tables; a->bits = bits; a->flags = flags;
+    return DQRM_OK;
+}
+
+int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags,
+                 float* out, int64_t out_stride_t, int64_t out_stride_b, void* stream) {
     FwdArgs a;
-    a.W = set->W; a.packed = set->packed; a.tmax = set->tmax; a.scale = set->scale;
-    a.meta = set->meta; a.err = set->err;
-    a.idx = batch->idx; a.off = batch->off; a.idx_base = batch->idx_base;
-    a.pool1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-    a.out = out; a.B = batch->num_bags; a.ost_t = out_stride_t; a.ost_b = out_stride_b;
-    a.T = set->num_tables; a.bits = bits; a.flags = flags;
+    int rc = fwd_args(set, batch, bits, flags, out, out_stride_t, out_stride_b, "dqrm_emb_fwd", &a);
+    if (rc) return rc;
+    if (batch->num_bags <= 0) return DQRM_OK;
     hipStream_t st = (hipStream_t)stream;
     const int D = set->dim;
     const bool packed_path = (flags & DQRM_FWD_USE_PACKED) && !(flags & DQRM_FWD_FULL_PRECISION) && D >= 8;
@@ -3885,6 +3936,32 @@ int dqrm_emb_fwd(const dqrm_table_set* set, const dqrm_batch* batch, int bits, u
         const int64_t cap = (8192 + a.T - 1) / a.T;  // ~8k workgroups in total, grid-stride beyond
         if (bx > cap) bx = cap;
         hipLaunchKernelGGL((k_emb_fwd<LPR, UNR>), dim3((unsigned)bx, (unsigned)a.T), dim3(256), 0, st, a);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
+int dqrm_emb_fwd_after_update(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags,
+                              float* out, int64_t out_stride_t, int64_t out_stride_b, const int64_t* rows,
+                              int64_t n, int repack_bits, void* stream) {
+    FwdArgs a;
+    int rc = fwd_args(set, batch, bits, flags, out, out_stride_t, out_stride_b, "dqrm_emb_fwd_after_update", &a);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && !rows))
+        return set_error(DQRM_E_INVALID, "%s: bad row list", "dqrm_emb_fwd_after_update");
+    // one workgroup does it all: a one-table set, a small batch and row list, FP32 rows
+    const int lpr = set->dim / 4;
+    const bool one = n > 0 && n <= 4096 && set->num_tables == 1 && repack_bits == 0 &&
+                     !(flags & DQRM_FWD_USE_PACKED) && batch->num_bags > 0 &&
+                     batch->num_bags * (int64_t)lpr <= 16 * 256 && finalize_mode() != 1;
+    if (!one) {  // the two calls
+        if (n > 0 && (rc = dqrm_rows_changed(set, rows, n, repack_bits, stream))) return rc;
+        return dqrm_emb_fwd(set, batch, bits, flags, out, out_stride_t, out_stride_b, stream);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    DISPATCH_LPR(set->dim, {
+        hipLaunchKernelGGL((k_fwd_after_update<LPR>), dim3(1), dim3(256), 0, st, a, set->rowmax, set->bdirty,
+                           set->sdirty, set->blkmax, set->sblkmax, set->tmax, rows, n, set->total_rows);
     });
     LAUNCH_CHECK();
     return DQRM_OK;

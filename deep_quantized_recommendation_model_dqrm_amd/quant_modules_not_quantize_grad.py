@@ -25,6 +25,7 @@ all tables instead of 26.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import numpy as np
@@ -103,6 +104,11 @@ def set_default_grad_mode(mode: str) -> None:
     _DEFAULT_GRAD_MODE = mode
 
 
+# grad_mode "sparse": the rows an optimizer changed are synced by the next forward's own launch
+# (dqrm_emb_fwd_after_update); DQRM_FUSE_SYNC=0 issues dqrm_rows_changed as a call of its own (A/B)
+_FUSE_SYNC = os.environ.get("DQRM_FUSE_SYNC", "1") != "0"
+
+
 def _on(x: torch.Tensor, device: torch.device) -> bool:
     d = x.device
     return d.type == device.type and (device.index is None or d.index == device.index)
@@ -131,12 +137,12 @@ class _EmbeddingFn(torch.autograd.Function):
     """Autograd bridge: forward = dqrm_emb_fwd; backward per the module's grad_mode."""
 
     @staticmethod
-    def forward(ctx, weight, owner, batches, bits, flags_refresh, full_precision, layout):
+    def forward(ctx, weight, owner, batches, bits, flags_refresh, full_precision, layout, changed=None):
         tset: EmbeddingTableSet = owner._tset
         one = layout == "bd"  # one table: its [B, D] output itself (no select node after the Function)
         layout = "tbd" if one else layout
         y = tset.forward(batches, bits=bits, refresh_scale=flags_refresh, use_packed=owner._use_packed(full_precision),
-                         full_precision=full_precision, layout=layout)
+                         full_precision=full_precision, layout=layout, changed_rows=changed)
         if one:
             y = y.view(y.shape[1], y.shape[2])
         ctx.one = one
@@ -153,7 +159,7 @@ class _EmbeddingFn(torch.autograd.Function):
         if ctx.one:
             dy = dy.view(1, dy.shape[0], dy.shape[1])
         grad_w = owner._backward(ctx.batches, dy, ctx.ste, ctx.layout)
-        return grad_w, None, None, None, None, None, None
+        return grad_w, None, None, None, None, None, None, None
 
 
 class _WeightHolder(nn.Module):
@@ -323,7 +329,9 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
     def forward(self, input, offsets=None, per_sample_weights=None, full_precision_flag=False, test_mode=False):
         fp = bool(full_precision_flag or self.full_precision_flag)
         self._check_errors(test_mode)
-        self._sync_external_update()
+        fuse_sync = _FUSE_SYNC and bool(self._ext_rows) and not self._use_packed(False)  # synced by the forward's launch
+        if not fuse_sync:
+            self._sync_external_update()
         if self.quant_mode not in ("symmetric", "speed_symmetric", "asymmetric"):
             raise ValueError("unknown quant mode: {}".format(self.quant_mode))
         refresh = self._refresh_due(fp, test_mode)
@@ -337,7 +345,12 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
             refresh_in_fwd = False
         else:
             refresh_in_fwd = refresh
-        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "bd")
+        changed = None
+        if fuse_sync:
+            changed = self._ext_rows[0] if len(self._ext_rows) == 1 else torch.cat(self._ext_rows)
+            self._ext_rows = []
+        y = _EmbeddingFn.apply(self.embedding_bag.weight, self, batch, self.embedding_bit, refresh_in_fwd, fp, "bd",
+                               changed)
         if refresh:
             # 0-d scale, as the reference stores it: a view of the set's scale, which every
             # refreshing forward rewrites in place (the buffer entry, without __setattr__)

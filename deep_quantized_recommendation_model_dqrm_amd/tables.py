@@ -382,10 +382,14 @@ class EmbeddingTableSet:
         out: torch.Tensor | None = None,
         layout: str = "tbd",
         nt_store: bool | None = None,
+        changed_rows: torch.Tensor | None = None,
     ) -> torch.Tensor:
         """Fused T-table fake-quant EmbeddingBag (q_m_n_q_g.py:317-398 for every table).
 
         layout "tbd" -> out [T, B, D]; "btd" -> out [B, T, D] (DLRM interaction order).
+        changed_rows: slab rows rewritten outside the kernels since the last call (an
+        optimizer's step on the lookup_grad COO): rows_changed(changed_rows) first, in the
+        same launch when the set and batch are small (dqrm_emb_fwd_after_update).
         """
         if batch.num_tables != self.T:
             raise ValueError("batch has %d tables, set has %d" % (batch.num_tables, self.T))
@@ -410,6 +414,16 @@ class EmbeddingTableSet:
             nt_store = B * T * D * 4 > (192 << 20)
         if nt_store:
             flags |= L.DQRM_FWD_NT_STORE
+        if changed_rows is not None and changed_rows.numel() > 0:
+            rows = changed_rows
+            if rows.dtype != torch.int64 or not rows.is_contiguous() or rows.device != self.device:
+                rows = rows.to(device=self.device, dtype=torch.int64).contiguous()
+            L.check(
+                self.lib.dqrm_emb_fwd_after_update(C.byref(self._c), C.byref(batch.c), bits, flags, _ptr(out), st,
+                                                   sb, _ptr(rows), rows.numel(), 0, _stream_handle()),
+                "dqrm_emb_fwd_after_update",
+            )
+            return out
         L.check(
             self.lib.dqrm_emb_fwd(C.byref(self._c), C.byref(batch.c), bits, flags, _ptr(out), st, sb,
                                   _stream_handle()),

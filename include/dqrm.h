@@ -45,13 +45,14 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 6  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 7  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
                                6: residency-checked one launch (dqrm_bwd_apply_local_is_one_launch),
                                   dqrm_checksum64 mixes the full 64-bit position,
-                                  dqrm_table_set.num_rows_host */
+                                  dqrm_table_set.num_rows_host;
+                               7: dqrm_emb_fwd_after_update */
 
 /* status codes */
 #define DQRM_OK            0
@@ -252,6 +253,16 @@ int dqrm_emb_bwd_lookup_grad(const dqrm_table_set* set, const dqrm_batch* batch,
  * max again, quant_utils.py:141-194) and, repack_bits == 4, repack their INT4 rows with the
  * frozen packing scale. rows: slab rows (device i64 [n], duplicates allowed). */
 int dqrm_rows_changed(const dqrm_table_set* set, const int64_t* rows, int64_t n, int repack_bits, void* stream);
+
+/* dqrm_rows_changed(set, rows, n, repack_bits) followed by dqrm_emb_fwd(set, batch, ...),
+ * same results: the per-table module's sync after a torch.optim.SGD step on its COO grad
+ * and its next forward (q_m_n_q_g.py:317-398 with the full-table scale of
+ * quant_utils.py:141-194). A one-table set with a small batch (bags * D/4 <= 4096, n <= 4096,
+ * FP32 rows, no repack) runs both as ONE single-workgroup launch; anything else as the two
+ * calls. n == 0 is dqrm_emb_fwd. */
+int dqrm_emb_fwd_after_update(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags,
+                              float* out, int64_t out_stride_t, int64_t out_stride_b, const int64_t* rows,
+                              int64_t n, int repack_bits, void* stream);
 
 /* Wire payload of one rank (bytes), produced by dqrm_grad_quant_pack:
  *   [counts i32 T*S | pad to 16] [rows i32 CAP | pad to 16] [vals CAP*D elems of
