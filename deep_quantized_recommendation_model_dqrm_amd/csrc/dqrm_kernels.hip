@@ -1744,6 +1744,9 @@ DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
 }
 
 constexpr int FLAT_TPB = 256;
+#ifndef DQRM_FLAT_PRELOAD
+#define DQRM_FLAT_PRELOAD 1  // 0: an A/B build reading the superblock / table max only on growth
+#endif
 
 // SGD of row x (global row grow) by one LPR-lane group with the summed value acc, rowmax,
 // and the exact |W| hierarchy without a per-block pass: growth goes in with an order-free
@@ -1759,6 +1762,11 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
     const int64_t blk = x >> 8;
     const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
     const float old_blk = a.blkmax[bb + blk];
+    // the superblock and table maxima with the row (DQRM_FLAT_PRELOAD): no dependent round trips
+    // on growth, which early in training is every row of a big table; a stale-low value only
+    // costs a redundant atomicMax (within the launch they only grow)
+    const float old_sb = DQRM_FLAT_PRELOAD && nrows > BLK ? a.sblkmax[sbb + (blk >> 8)] : 0.0f;
+    const float old_tm = DQRM_FLAT_PRELOAD ? a.tmax[t] : 0.0f;
     float4 w;
     w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
     w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
@@ -1773,9 +1781,10 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
             const int64_t sb = sbb + (blk >> 8);
             if (rm > old_blk) {
                 atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
-                if (rm > a.sblkmax[sb]) {
+                if (rm > (DQRM_FLAT_PRELOAD ? old_sb : a.sblkmax[sb])) {
                     atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
-                    if (rm > a.tmax[t]) atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
+                    if (rm > (DQRM_FLAT_PRELOAD ? old_tm : a.tmax[t]))
+                        atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
                 }
             }
             if (old_rm == old_blk && rm < old_rm) {
