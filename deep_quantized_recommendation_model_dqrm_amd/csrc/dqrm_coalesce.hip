@@ -993,6 +993,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     const int nsbc = APPLY && !dsplit && r1 > r0 && ((r1 - 1) >> 16) - sb0 < SBC ? (int)(((r1 - 1) >> 16) - sb0 + 1) : 0;
     float sbv = 0.0f;
     if (APPLY && tid < nsbc) sbv = la.sblkmax[sbb + sb0 + tid];
+    CDIAG_W(17);  // (diagnostic build: the dy prefetch landed -- before the W rows are issued)
     if (!DQRM_COAL_WLATE || n - NS > CE) issue_w();
     float amax = 0.0f;
     auto emit = [&](int u, int d, float acc) {  // segment u's sum in dimension q0*4 + d

@@ -30,6 +30,7 @@ lib.dqrm_diag_coal_read.argtypes = [C.c_void_p, C.c_int]
 ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
 g = torch.Generator(device="cuda").manual_seed(5)
 NS = 32  # stamp slots per workgroup (dqrm_coalesce.hip g_coal_clk)
+STE = os.environ.get("DIAG_STE", "1") != "0"  # DIAG_STE=0: without the STE division (a what-if, not the path)
 NB = 8  # distinct resident batches cycled, as bench.py (cold rows and translations every launch)
 bs = [dq.LookupBatch.pooling_one(torch.stack([torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows]))
       for _ in range(NB)]
@@ -42,7 +43,7 @@ def run(i):
     b = bs[i % NB]
     if APPLY:
         ts.forward(b)
-        ts.backward_apply_local(b, dy, ws, 8, s_avg, 0.01)
+        ts.backward_apply_local(b, dy, ws, 8, s_avg, 0.01, ste=STE)
     else:
         ts.backward_coalesce(b, dy, ws)
 
@@ -87,6 +88,12 @@ sub = [(c[t, s, 8] - c[t, s, 1], c[t, s, 9] - c[t, s, 8], c[t, s, 10] - c[t, s, 
 sub = np.array(sub) / 100
 print("compact split (median us): idx-wait %.2f  compaction %.2f  report+barrier %.2f  prefetch-issue %.2f" %
       tuple(np.median(sub, axis=0)))
+lw = [(c[t, s, 17] - c[t, s, 4], c[t, s, 5] - c[t, s, 17]) for c in cs for t in range(T) for s in range(16)
+      if c[t, s, 17] >= 0 and c[t, s, 4] >= 0 and c[t, s, 5] >= 0]
+if lw:
+    lw = np.array(lw) / 100
+    print("land split (median us): dy prefetch still in flight after the heads %.2f  landing + W issue %.2f" %
+          tuple(np.median(lw, axis=0)))
 if APPLY:
     print("apply phases per table, slowest slot, median (us): segments done->met (incl. the wait) | "
           "met->updated | updated->end || end")
