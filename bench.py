@@ -77,6 +77,10 @@ def parse(argv=None):
     p.add_argument("--global-batch", type=int, default=0,
                    help="strong scaling: samples per step over all ranks, each rank taking its "
                         "get_my_slice share (SURVEY 8(d) C5: 2048 over 8 GPUs)")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: --batch-per-gpu samples per rank; strong: --batch-per-gpu is the GLOBAL "
+                        "batch split over the ranks (config 5 as SURVEY 8(d) writes it: "
+                        "--scaling strong = 2048 over N GPUs); --global-batch overrides both")
     p.add_argument("--grad-bits", type=int, default=8)
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--scale-period", type=int, default=0,
@@ -107,8 +111,9 @@ def parse(argv=None):
                         "on a one-GPU box")
     p.add_argument("--two-launch-local", action="store_true",
                    help="N=1: coalesce + dqrm_apply_local as two launches (not dqrm_emb_bwd_apply_local)")
-    p.add_argument("--sample-every", type=int, default=8,
-                   help="bracket the dominant kernel with HIP events on every k-th timed step")
+    p.add_argument("--sample-every", type=int, default=0,
+                   help="bracket the dominant kernel with HIP events on every k-th timed step "
+                        "(0 = auto: at least 16 bracketed launches, at most every 8th step)")
     p.add_argument("--traffic-profile", default=None,
                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; "
                         "default profiles/r2_<config>_summary.json when present")
@@ -221,6 +226,8 @@ def main():
     if a.graph and world > 1:
         print("--graph runs at N=1 only (the collectives stay eager)", file=sys.stderr)
         sys.exit(2)
+    if a.scaling == "strong" and a.global_batch <= 0:
+        a.global_batch = a.batch_per_gpu  # the batch is the global one, split over the ranks
     strong = a.global_batch > 0
     if strong and a.global_batch % world:  # the reference skips such batches (parallel_comm.py:1855-1856)
         print(f"--global-batch {a.global_batch} is not divisible by {world} ranks", file=sys.stderr)
@@ -403,7 +410,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     evs = [timed_events(len(names)) for _ in range(a.steps)]
-    sampled = [] if graphs is not None else [i for i in range(a.steps) if i % a.sample_every == 0]
+    every = a.sample_every if a.sample_every > 0 else max(1, min(8, a.steps // 16))
+    sampled = [] if graphs is not None else [i for i in range(a.steps) if i % every == 0]
     t_start = time.perf_counter()
     for i in range(a.steps):
         run(a.warmup + i, evs[i] if i in sampled else None)
@@ -514,9 +522,11 @@ def main():
                               "frac": round(step_alg / (elapsed / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                               "phases": names},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
-            "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events (the |W| "
-                               "hierarchy is finalized inside the updating launches; apply_sparse_update "
-                               "and apply_local add a short finalize launch)",
+            "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events; " + (
+                "bwd_apply_local is ONE launch (coalesce, quantize, update and the |W| hierarchy)" if one_launch
+                else "apply_local = the fused quantize + update kernel + a short k_table_finalize launch" if fused
+                else "sgd = one launch (|W| hierarchy inside)" if a.mode == "sgd"
+                else "apply_sparse_update = " + L.apply_update_form() if a.mode == "dp" else "forward only"),
             "weight_syncc": ({"every": sync_every, "ms_per_call": round(sync_ms, 3),
                               "amortized_us_per_step": round(sync_ms * 1e3 / sync_every, 2),
                               "in_timed_region": True} if sync_every else None),

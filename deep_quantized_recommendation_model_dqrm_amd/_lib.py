@@ -274,3 +274,9 @@ def check(rc: int, what: str) -> None:
     if rc != DQRM_OK:
         msg = load().dqrm_last_error().decode(errors="replace")
         raise DQRMError(f"{what} failed ({rc}): {msg}")
+
+
+def apply_update_form() -> str:
+    """What dqrm_apply_sparse_update launches (for bench lines): the payload decode + update
+    kernel and where the |W| hierarchy is finalized."""
+    return "the payload decode + update kernel (k_apply_flat) + a short k_table_finalize launch"

@@ -427,8 +427,20 @@ class ConsolidatedExchange:
             self.inner.apply(lr, mode=mode, repack=rp)
         self._args = None
 
+    def discard(self) -> None:
+        """weight_update_parallel_comm(update_embedding=False): no update this step. The fused
+        form deferred the whole step to apply(); its exchange runs now (coalesce + scales, no
+        update) so emb_scaling_factor holds this step's scales as in the reference (set in
+        grad_update_parallel_comm, s_q_g_p_c.py:296), and the pending (batch, dy) is released."""
+        if self.fused and self._args is not None:
+            batch, dy, ste = self._args
+            self.inner.exchange(batch, dy, ste=ste, layout="tbd")
+        self._args = None
+
     @property
     def scales_ready_after_apply(self) -> bool:
+        """True when the scales (emb_scaling_factor) are produced by apply() / discard() rather
+        than by exchange(): the world-size-1 one-launch form computes them with the update."""
         return self.fused
 
 

@@ -1129,9 +1129,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         if (K == 1) a.ws_absmax[k] = m;  // sub-slots: sub-slot 0 writes the slot's, after the rendezvous
         // publish this slot's max|grad| (and distinct rows) as ONE 8-B sc1 store (a data-tagged
         // granule: no counter, no ordering needed for the value itself)
-        if constexpr (APPLY)
+        if constexpr (APPLY) {
             __hip_atomic_store(gran + s + SPLIT * j, gr_make(m, dsplit ? 0 : U, epoch), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+            // a slot served alone this launch also advances its sub-slot-1 granule, so both
+            // sub-slots derive the same epoch in a later launch that splits the slot (a parent
+            // set and a one-table view of it plan sub-slots differently; nobody polls it now)
+            if (K == 1 && !dsplit)
+                __hip_atomic_store(gran + s + SPLIT, gr_make(0.0f, 0, epoch), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if constexpr (APPLY) {
         if (tid < nsbc) s_sbm[tid] = sbv;

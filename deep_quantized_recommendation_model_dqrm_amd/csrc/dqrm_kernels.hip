@@ -3691,6 +3691,25 @@ int allow_lds(K kernel, size_t bytes) {
     return DQRM_OK;
 }
 
+constexpr int LDS_PER_CU = 160 * 1024;  // gfx950: static + dynamic LDS of one workgroup
+
+// a kernel's static LDS bytes (hipFuncGetAttributes, cached per kernel address)
+template <typename K>
+size_t static_lds_bytes(K kernel) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    static const void* seen[64];
+    static size_t seen_bytes[64];
+    static int nseen = 0;
+    const void* f = reinterpret_cast<const void*>(kernel);
+    for (int i = 0; i < nseen; ++i)
+        if (seen[i] == f) return seen_bytes[i];
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, f) != hipSuccess) return (size_t)LDS_PER_CU;  // unknown: treat as full
+    if (nseen < 64) { seen[nseen] = f; seen_bytes[nseen] = at.sharedSizeBytes; ++nseen; }
+    return at.sharedSizeBytes;
+}
+
 // dqrm_emb_bwd_coalesce's kernel choice (dqrm_set_coalesce_kernel)
 std::atomic<int> g_coalesce_kernel{DQRM_COALESCE_AUTO};
 
@@ -3775,16 +3794,22 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     // SGD of a small batch: one workgroup per table, no sort, no hand-off (k_sgd_small)
     if (MODE == 0 && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && Lc <= sg_maxl(D / 4) &&
         c.batch->num_bags * D <= SG_DY_FLOATS && set->total_rows <= 0x7fffffffll) {
-        // dy staging, then (Criteo form) the row hash; the kernel reads L = B lookups per table
+        // dy staging, then (Criteo form) the row hash; the kernel reads L = B lookups per table.
+        // It takes the batch only if that dynamic LDS plus its static LDS fit one CU (else
+        // k_bwd_fused below, which has no per-batch LDS).
         const bool p1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
         const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float) +
                            (p1 ? (size_t)sg_hash_bytes((int)c.batch->num_bags) : 0);
-        DISPATCH_LPR(D, {
-            if ((rc = allow_lds(k_sgd_small<LPR>, dyn))) return rc;
-            hipLaunchKernelGGL(k_sgd_small<LPR>, dim3(T), dim3(SG_TPB), dyn, st, fa);
-        });
-        LAUNCH_CHECK();
-        return DQRM_OK;
+        bool fits = false;
+        DISPATCH_LPR(D, { fits = dyn + static_lds_bytes(k_sgd_small<LPR>) <= (size_t)LDS_PER_CU; });
+        if (fits) {
+            DISPATCH_LPR(D, {
+                if ((rc = allow_lds(k_sgd_small<LPR>, dyn))) return rc;
+                hipLaunchKernelGGL(k_sgd_small<LPR>, dim3(T), dim3(SG_TPB), dyn, st, fa);
+            });
+            LAUNCH_CHECK();
+            return DQRM_OK;
+        }
     }
     DISPATCH_LPR(D, {
         if ((rc = allow_lds(k_bwd_fused<LPR, MODE>, FB_LDS))) return rc;

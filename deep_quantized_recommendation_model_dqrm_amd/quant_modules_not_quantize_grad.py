@@ -110,8 +110,15 @@ _FUSE_SYNC = os.environ.get("DQRM_FUSE_SYNC", "1") != "0"
 
 
 def _on(x: torch.Tensor, device: torch.device) -> bool:
+    """x already lives where the kernels launch: an index-less "cuda" device means the
+    current device (the kernels' stream), so inputs on any other GPU are copied over."""
     d = x.device
-    return d.type == device.type and (device.index is None or d.index == device.index)
+    if d.type != device.type:
+        return False
+    idx = device.index
+    if idx is None and device.type == "cuda":
+        idx = torch.cuda.current_device()
+    return idx is None or d.index == idx
 
 
 def _batch_from_input(input: torch.Tensor, offsets: torch.Tensor | None, device) -> LookupBatch:

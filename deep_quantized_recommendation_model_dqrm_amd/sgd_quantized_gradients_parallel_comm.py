@@ -316,6 +316,8 @@ def weight_update_parallel_comm(model, lr, emb_grad_quantized=True, update_embed
             if update_embedding:
                 ex.apply(lr, mode=L.DQRM_UPD_DP if bits != 32 else L.DQRM_UPD_FP32,
                          repack=[m._use_packed(False) for m in bmods])
+            elif hasattr(ex, "discard"):  # no update: settle the scales, release (batch, dy)
+                ex.discard()
             for m in bmods:
                 m._ready = None
             _mset(model, "_dqrm_emb_ready", None)

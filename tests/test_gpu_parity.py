@@ -873,8 +873,52 @@ def test_fused_coalesce_apply_matches_two_launches(dq, D, B, dist, bits, repack)
         assert torch.equal(x, y)
 
 
+def test_fused_step_alternating_set_and_view(dq):
+    """The one-launch step alternately on an 8-table set (no spare workgroups: no sub-slots)
+    and on a one-table view of its 100 k-row table (the view's spare groups give that table a
+    second workgroup per slot): the two plans share the table's granules, so the sub-slots
+    must agree on the launch epoch whatever ran before. Every step equals the two-launch path
+    on a copy, and no stall is flagged."""
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
+
+    rows = [3, 971, 100000, 2208, 40000, 7, 5000, 300]
+    T, D, B, tv = len(rows), 32, 1024, 2
+    sets = [dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=17) for _ in range(2)]
+    views = [s.view(tv) for s in sets]
+    s_avg = [torch.zeros(T, dtype=torch.float32, device="cuda") for _ in range(2)]
+    sv_avg = [torch.zeros(1, dtype=torch.float32, device="cuda") for _ in range(2)]
+    for it in range(6):
+        P = G.pooling_one(rows, B, 301 + it)
+        dy = torch.from_numpy(G.upstream_grad(T, B, D, 311 + it) * 30).cuda()
+        on_view = it % 2 == 1
+        if on_view:
+            b = dq.LookupBatch.pooling_one(torch.from_numpy(P[tv: tv + 1].copy()).cuda())
+            d = dy[tv: tv + 1].contiguous()
+            targets, avg, nr = views, sv_avg, [rows[tv]]
+        else:
+            b = dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda())
+            d = dy
+            targets, avg, nr = sets, s_avg, rows
+        assert targets[0].apply_local_is_one_launch(b)
+        for j, ts in enumerate(targets):
+            ts.forward(b)
+            ws = dq.CoalescedGrad.allocate(nr, B, D, "cuda")
+            if j == 0:
+                ts.backward_apply_local(b, d, ws, 8, avg[0], 0.5)
+            else:
+                ts.backward_coalesce(b, d, ws)
+                HipExchangeKernels(ts).apply_local(ws, 8, avg[1], 0.5, False)
+        assert [s.read_errors() for s in sets] == [0, 0], it
+        assert torch.equal(avg[0], avg[1]), it
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax"):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
+
+
 @pytest.mark.parametrize("B,D,dist", [(128, 16, "uniform"), (128, 16, "zipf"), (256, 16, "zipf"), (64, 64, "uniform"),
-                                      (100, 4, "zipf"), (500, 8, "uniform"), (1, 16, "uniform")])
+                                      (100, 4, "zipf"), (500, 8, "uniform"), (1, 16, "uniform"),
+                                      # D = 32 at B = 512 / 400: the row hash no longer fits LDS
+                                      # beside the dy stage; the batch takes k_bwd_fused
+                                      (512, 32, "uniform"), (400, 32, "zipf")])
 def test_sgd_small_criteo_form_matches_oracle(dq, B, D, dist):
     """The one-workgroup-per-table SGD kernel on Criteo-form batches (config 3: its row hash
     of position masks replaces the duplicate scan): three steps on tables from 3 rows (~B/3
