@@ -279,9 +279,15 @@ def main():
     repack = a.use_packed
     names = phase_names(a.mode, a.use_packed, fused, one_launch)
 
-    def step(i, ev=None, only=None, refresh=None):
+    # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
+    # (dqrm_exchange_grad: coalesce + both all-gathers + quantize-pack; dqrm_exchange_apply);
+    # the untimed breakdown pass issues the kernels one by one to time each
+    lib_exchange = ex is not None and ex._x is not None
+
+    def step(i, ev=None, only=None, refresh=None, split=False):
         """One step of the selected mode. ev: per-phase (start, end) events; only: bracket
-        just that phase; refresh: refresh the table scales (default: by --scale-period)."""
+        just that phase; refresh: refresh the table scales (default: by --scale-period);
+        split: the library-issued exchange as its separate calls (breakdown pass)."""
         b = batches[i % len(batches)]
         if refresh is None:
             refresh = a.scale_period <= 0 or i % a.scale_period == 0
@@ -306,6 +312,10 @@ def main():
             mark(1, 1)
             return
         kern = ex.kernels
+        if lib_exchange and not split:
+            ex.exchange(b, dy)
+            ex.apply(a.lr, mode=L.DQRM_UPD_DP, repack=repack)
+            return
         if one_launch:
             kern.coalesce_apply_local(b, dy, ex.ws, True, "tbd", a.grad_bits, ex.s_avg, a.lr, repack)
             mark(1, 1)
@@ -343,7 +353,7 @@ def main():
     nb = max(10, min(50, a.steps))
     bev = [timed_events(len(names)) for _ in range(nb)]
     for i in range(nb):
-        step(i, bev[i], refresh=a.scale_period <= 0)
+        step(i, bev[i], refresh=a.scale_period <= 0, split=True)
     torch.cuda.synchronize()
     refresh_ms = None
     if a.use_packed:  # new scales from the |W| hierarchy + INT4 repack of every table whose scale moved
@@ -411,7 +421,8 @@ def main():
     torch.cuda.synchronize()
     evs = [timed_events(len(names)) for _ in range(a.steps)]
     every = a.sample_every if a.sample_every > 0 else max(1, min(8, a.steps // 16))
-    sampled = [] if graphs is not None else [i for i in range(a.steps) if i % every == 0]
+    # (graph replay / the library-issued exchange: the dominant kernel is timed in the breakdown pass)
+    sampled = [] if graphs is not None or lib_exchange else [i for i in range(a.steps) if i % every == 0]
     t_start = time.perf_counter()
     for i in range(a.steps):
         run(a.warmup + i, evs[i] if i in sampled else None)
@@ -424,7 +435,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     dom_ms = (float(np.mean([evs[i][dj][0].elapsed_time(evs[i][dj][1]) for i in sampled])) if sampled
-              else kms[dom])  # graph replay: the eager breakdown's average
+              else kms[dom])  # graph replay / library exchange: the breakdown pass's average (nb launches)
 
     # algorithmic bytes per launch; distinct rows of the last step's batch
     if ex is not None:
@@ -476,6 +487,8 @@ def main():
         colls = None
         if a.mode == "dp":
             colls = {"world_size": world, "backend": a.dist_backend if coll else None,
+                     "issued_by": ("libdqrm (dqrm_comm: RCCL ncclAllGather between the step's kernels)"
+                                   if lib_exchange else "torch.distributed" if coll else None),
                     "per_step": 2 if coll else 0,
                     "scale_allgather_bytes_per_rank": ex.ws.absmax.numel() * 4,
                     "payload_allgather_bytes_per_rank": int(ex.payload_bytes)}
@@ -510,7 +523,7 @@ def main():
                          "traffic": traffic["bytes"] if traffic else None, "traffic_unit": "bytes/launch",
                          "traffic_src": traffic,
                          "alg_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 5),
-                         "timed_launches": len(sampled),
+                         "timed_launches": len(sampled) if sampled else nb,
                          # the same bytes over rocprofv3's median kernel time of this workload
                          # (events bracket the launch and read a few us above the kernel)
                          "frac_rocprof_median": (round(alg / (med_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)

@@ -51,7 +51,8 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 7  # include/dqrm.h
+DQRM_ABI_VERSION = 8  # include/dqrm.h
+DQRM_PRESUM_MAX_LOOKUPS = 2048
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = (
@@ -88,6 +89,13 @@ EXPORTED_SYMBOLS = (
     "dqrm_init_uniform",
     "dqrm_checksum64",
     "dqrm_replica_mean",
+    "dqrm_comm_unique_id",
+    "dqrm_comm_init",
+    "dqrm_comm_destroy",
+    "dqrm_comm_allgather",
+    "dqrm_exchange_grad",
+    "dqrm_exchange_apply",
+    "dqrm_emb_bwd_lookup_grad_presum",
     "dqrm_read_errors",
     "dqrm_last_error",
     "dqrm_set_apply_kernel",
@@ -150,6 +158,32 @@ class DenseSet(C.Structure):
         ("param", C.c_void_p),
         ("len", C.c_void_p),
         ("wire_off", C.c_void_p),
+    ]
+
+
+class Exchange(C.Structure):
+    """Mirror of ``dqrm_exchange`` (include/dqrm.h): one rank's exchange buffers."""
+
+    _fields_ = [
+        ("set", C.POINTER(TableSet)),
+        ("comm", C.c_void_p),
+        ("num_ranks", C.c_int32),
+        ("grad_bits", C.c_int32),
+        ("ws_cap_base", C.c_void_p),
+        ("ws_cap_total", C.c_int64),
+        ("ws_rows", C.c_void_p),
+        ("ws_vals", C.c_void_p),
+        ("ws_ucount", C.c_void_p),
+        ("ws_absmax", C.c_void_p),
+        ("absmax_all", C.c_void_p),
+        ("cap_base", C.c_void_p),
+        ("cap_total", C.c_int64),
+        ("s_avg", C.c_void_p),
+        ("payload", C.c_void_p),
+        ("gathered", C.c_void_p),
+        ("payload_bytes", C.c_size_t),
+        ("workspace", C.c_void_p),
+        ("workspace_bytes", C.c_size_t),
     ]
 
 
@@ -250,6 +284,13 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_init_uniform": (C.c_int, [TS, C.c_uint64, P]),
         "dqrm_checksum64": (C.c_int, [P, C.c_int64, P, P]),
         "dqrm_replica_mean": (C.c_int, [P, C.c_int64, C.c_int, C.c_float, P]),
+        "dqrm_comm_unique_id": (C.c_int, [P]),
+        "dqrm_comm_init": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, P]),
+        "dqrm_comm_destroy": (C.c_int, [P]),
+        "dqrm_comm_allgather": (C.c_int, [P, P, P, C.c_size_t, P]),
+        "dqrm_exchange_grad": (C.c_int, [C.POINTER(Exchange), BA, P, C.c_int64, C.c_int64, C.c_int, P]),
+        "dqrm_exchange_apply": (C.c_int, [C.POINTER(Exchange), C.c_float, C.c_int, C.c_int, P]),
+        "dqrm_emb_bwd_lookup_grad_presum": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P]),
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
         "dqrm_last_error": (C.c_char_p, []),
         "dqrm_set_apply_kernel": (C.c_int, [C.c_int]),

@@ -20,6 +20,7 @@ Kernels: dqrm_emb_bwd_coalesce (K4), dqrm_grad_quant_pack (K5), dqrm_apply_spars
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Protocol
 
 import torch
@@ -151,6 +152,65 @@ def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None, world: int
         dist.all_gather(list(out.unbind(0)), inp, group=group)
 
 
+class DqrmComm:
+    """libdqrm's own RCCL communicator (dqrm_comm) over the ranks of a torch.distributed
+    group: rank 0 draws RCCL's unique id, the group broadcasts it, every rank joins
+    (ncclCommInitRank, collective). The exchange then issues its two all-gathers from C, on
+    the compute stream between its kernels (dqrm_exchange_grad): no Python or c10d work per
+    collective. One per (group, device), shared by every exchange on that group; released at
+    exit or by close()."""
+
+    _cache: dict = {}
+
+    def __init__(self, group=None, device=None):
+        self.lib = L.load()
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        dev = torch.device(device if device is not None else "cuda")
+        idbuf = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            L.check(self.lib.dqrm_comm_unique_id(idbuf.data_ptr()), "dqrm_comm_unique_id")
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        if dist.get_backend(group) == "nccl":  # RCCL broadcasts device tensors
+            t = idbuf.to(dev)
+            dist.broadcast(t, src=src, group=group)
+            idbuf = t.cpu()
+        else:
+            dist.broadcast(idbuf, src=src, group=group)
+        h = C.c_void_p()
+        with torch.cuda.device(dev):
+            L.check(self.lib.dqrm_comm_init(C.byref(h), self.world, self.rank, idbuf.data_ptr()), "dqrm_comm_init")
+        self.handle = h
+
+    @classmethod
+    def get(cls, group=None, device=None) -> "DqrmComm":
+        key = (id(group), str(device))
+        c = cls._cache.get(key)
+        if c is None or c.handle is None:
+            c = cls._cache[key] = cls(group, device)
+        return c
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None:
+            self.lib.dqrm_comm_destroy(self.handle)
+            self.handle = None
+
+    @classmethod
+    def close_all(cls) -> None:
+        for c in cls._cache.values():
+            c.close()
+        cls._cache.clear()
+
+
+def use_library_collectives(group=None) -> bool:
+    """Whether an exchange over `group` issues its collectives from libdqrm (RCCL, nccl
+    backend) rather than through torch.distributed (gloo: host-staged rehearsal). DQRM_C_COMM=0
+    forces the torch.distributed path (A/B)."""
+    if os.environ.get("DQRM_C_COMM", "1") == "0":
+        return False
+    return dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"
+
+
 class SparseGradExchange:
     """Per-step DP embedding update: coalesce -> all-gather of per-slot max|grad| ->
     scale average + quantize-pack -> payload all-gather -> decode + SGD.
@@ -202,6 +262,30 @@ class SparseGradExchange:
                                                           device=dev)
         self.gathered = None if shared else torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8,
                                                         device=dev)
+        # the library-issued step (dqrm_exchange_grad / _apply): RCCL collectives from C on a
+        # dqrm_comm, two host calls per step; only with the HIP kernels and unshared buffers
+        self._x = None
+        if (self.coll and not shared and isinstance(self.kernels, HipExchangeKernels)
+                and use_library_collectives(group)):
+            self.dcomm = DqrmComm.get(group, dev)
+            self._x = self._make_exchange(self.dcomm.handle)
+
+    def _make_exchange(self, comm_handle) -> "L.Exchange":
+        x = L.Exchange()
+        x.set = C.pointer(self.tables.c)
+        x.comm = comm_handle
+        x.num_ranks = self.world
+        x.grad_bits = self.grad_bits
+        ws = self.ws
+        x.ws_cap_base, x.ws_cap_total = _ptr(ws.slot_cap_base), ws.cap_total
+        x.ws_rows, x.ws_vals, x.ws_ucount, x.ws_absmax = _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax)
+        x.absmax_all = _ptr(self.absmax_all)
+        x.cap_base, x.cap_total = _ptr(self.cap_base), self.cap_total
+        x.s_avg, x.payload, x.gathered = _ptr(self.s_avg), _ptr(self.payload), _ptr(self.gathered)
+        x.payload_bytes = self.payload_bytes
+        w = self.tables.bwd_workspace(self.max_lookups)
+        x.workspace, x.workspace_bytes = w.data_ptr(), w.numel()
+        return x
 
     # -------------------------------------------------------------- collectives
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
@@ -213,6 +297,16 @@ class SparseGradExchange:
         coalesce, all-gather the scale inputs, quantize-pack, all-gather the payloads.
         Returns the per-table averaged gradient scale (emb_scaling_factor)."""
         gb = self.grad_bits
+        if self._x is not None:  # one library call: coalesce, all-gather, quantize-pack, all-gather
+            t = self.tables
+            st, sb = t._dy_strides(dy, layout, t.T, batch.num_bags, t.D)
+            w = t.bwd_workspace(batch.max_lookups)
+            x = self._x
+            if x.workspace != w.data_ptr():  # a larger batch grew the scratch
+                x.workspace, x.workspace_bytes = w.data_ptr(), w.numel()
+            L.check(t.lib.dqrm_exchange_grad(C.byref(x), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
+                                             _stream_handle()), "dqrm_exchange_grad")
+            return self.s_avg
         k = self.kernels
         k.coalesce(batch, dy, self.ws, ste, layout)
         if gb != 32 and self.coll:
@@ -230,6 +324,10 @@ class SparseGradExchange:
         gb = self.grad_bits
         if mode is None:
             mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
+        if self._x is not None:
+            L.check(self.tables.lib.dqrm_exchange_apply(C.byref(self._x), float(lr), int(mode), 4 if repack else 0,
+                                                        _stream_handle()), "dqrm_exchange_apply")
+            return
         gathered = self.gathered if self.coll else self.payload.view(1, -1)
         self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, gb, self.s_avg,
                            lr, mode, repack)
@@ -450,5 +548,5 @@ def get_my_slice(n: int, my_size: int, my_rank: int) -> slice:
     return slice(my_rank * k + min(my_rank, m), (my_rank + 1) * k + min(my_rank + 1, m), 1)
 
 
-__all__ = ["SparseGradExchange", "MultiSetExchange", "ConsolidatedExchange", "HipExchangeKernels", "payload_bytes",
+__all__ = ["DqrmComm", "use_library_collectives", "SparseGradExchange", "MultiSetExchange", "ConsolidatedExchange", "HipExchangeKernels", "payload_bytes",
            "get_my_slice", "all_gather_into"]

@@ -347,6 +347,26 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     }
 }
 
+// One rank's wire payload: [counts i32 T*SPLIT][rows i32 cap][values cap x D], 16-B aligned
+// sections (dqrm_payload_bytes); values int8 (bits <= 8), int16 (<= 16) or f32 (32)
+struct PayloadLayout {
+    int64_t rows_off;   // bytes
+    int64_t vals_off;   // bytes
+    int64_t bytes;
+    int elem;           // bytes per value
+};
+
+__host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
+
+__host__ __device__ inline PayloadLayout payload_layout(int T, int64_t cap, int D, int bits) {
+    PayloadLayout p;
+    p.elem = bits <= 8 ? 1 : (bits <= 16 ? 2 : 4);
+    p.rows_off = align16(4 * (int64_t)T * DQRM_TABLE_SPLIT);  // header: entries per (table, slot)
+    p.vals_off = p.rows_off + align16(4 * cap);
+    p.bytes = p.vals_off + align16(cap * (int64_t)D * p.elem);
+    return p;
+}
+
 // dequantize + SGD of one element: update.mul_(1/N), grad * s.item(), W.add_(-lr * .)
 struct ApplyUpdate {
     int mode;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/dqrm.h"
+
 namespace dqrm_internal {
 
 // The coalesce backward of a Criteo-form batch (DQRM_BATCH_POOLING_ONE: table t's lookups
@@ -72,5 +74,48 @@ void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la);
 // launches k_coalesce_p1 (dqrm_coalesce.hip); la != nullptr: the fused update as well
 // (hipErrorInvalidValue if !coalesce_apply_resident). Returns the HIP error of the launch.
 hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la, hipStream_t stream);
+
+// K5 quantize-pack of the N > 1 exchange (dqrm_exchange.hip): the rank's slot workspace ->
+// its wire payload, the table scales averaged over the all-gathered per-slot maxima
+// (dqrm_grad_quant_pack_strided's arguments, validated by the caller).
+struct QuantPackArgs {
+    int T;
+    int D;
+    const int64_t* ws_cap_base;  // [T*S+1]
+    const int32_t* ws_rows;
+    const float* ws_vals;
+    const int32_t* ws_ucount;
+    const float* absmax_all;     // [N][pitch], rank r's per-slot max|grad| at r*pitch + t*S + s
+    int64_t am_pitch;
+    int N;
+    int bits;                    // 2..16 quantized, 32 = FP32 values
+    const int64_t* cap_base;     // [T+1] payload capacity prefix
+    int64_t cap_total;
+    float* s_avg;                // [T]
+    unsigned char* payload;
+};
+hipError_t launch_quant_pack(const QuantPackArgs& a, hipStream_t stream);
+
+// The pre-summed per-lookup gradient (dqrm_lookup.hip, dqrm_emb_bwd_lookup_grad_presum):
+// one workgroup per table of at most kPresumMaxL lookups.
+constexpr int kPresumMaxL = DQRM_PRESUM_MAX_LOOKUPS;
+struct PresumArgs {
+    const int64_t* meta;
+    const float* scale;
+    uint32_t* err;
+    const int64_t* idx;
+    const int64_t* off;
+    const int64_t* idx_base;
+    const float* dy;
+    int64_t dst_t, dst_b;
+    int64_t B;
+    int64_t* rows;
+    float* vals;
+    int T;
+    int D;
+    int ste;
+    int pool1;
+};
+hipError_t launch_lookup_grad_presum(const PresumArgs& a, hipStream_t stream);
 
 }  // namespace dqrm_internal

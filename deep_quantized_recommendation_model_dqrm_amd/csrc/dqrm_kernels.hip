@@ -1265,23 +1265,7 @@ DQRM_INLINE bool narrow_table(int64_t nrows) { return nrows <= BLK; }
 // ------------------------------------------------------------------------------------
 // K5: scale average + quantize-pack (slot workspace -> dense wire payload)
 // ------------------------------------------------------------------------------------
-struct PayloadLayout {
-    int64_t rows_off;   // bytes
-    int64_t vals_off;   // bytes
-    int64_t bytes;
-    int elem;           // bytes per value
-};
-
-__host__ __device__ inline int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
-
-__host__ __device__ inline PayloadLayout payload_layout(int T, int64_t cap, int D, int bits) {
-    PayloadLayout p;
-    p.elem = bits <= 8 ? 1 : (bits <= 16 ? 2 : 4);
-    p.rows_off = align16(4 * (int64_t)T * SPLIT);  // header: entries per (table, slot)
-    p.vals_off = p.rows_off + align16(4 * cap);
-    p.bytes = p.vals_off + align16(cap * (int64_t)D * p.elem);
-    return p;
-}
+// (the wire payload layout, PayloadLayout / payload_layout: dqrm_device.h)
 
 // rank r's local scale from its slots' max |grad| (quant_utils.py:141-194 on the coalesced
 // values), then dist.all_reduce(SUM) + mul_(1./N) (s_q_g_p_c.py:861-866). Gloo's allreduce
@@ -4185,6 +4169,17 @@ int dqrm_grad_quant_pack_strided(int num_tables, int dim, const int64_t* ws_cap_
     if (((uintptr_t)payload) & 15)
         return set_error(DQRM_E_INVALID, "%s: payload must be 16-B aligned", "dqrm_grad_quant_pack");
     hipStream_t st = (hipStream_t)stream;
+    static const bool legacy = [] {  // DQRM_QPACK=legacy: the one-workgroup-per-slot kernel (A/B)
+        const char* e = getenv("DQRM_QPACK");
+        return e && !strcmp(e, "legacy");
+    }();
+    if (!legacy) {
+        dqrm_internal::QuantPackArgs q{num_tables, dim, ws_cap_base, ws_rows, ws_vals, ws_ucount, absmax_all,
+                                       absmax_pitch, num_ranks, grad_bits, cap_base, cap_total, s_avg,
+                                       (unsigned char*)payload};
+        HIP_TRY(dqrm_internal::launch_quant_pack(q, st));
+        return DQRM_OK;
+    }
     DISPATCH_LPR(dim, {
         hipLaunchKernelGGL(k_quant_pack<LPR>, dim3(num_tables * SPLIT), dim3(512), 0, st,
                            num_tables, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, absmax_all,

@@ -13,7 +13,9 @@ state-dict keys (:258-280, :288), and its semantics (:317-398):
   * backward: STE (g*s)/s (quant_utils.py:349-363), then one of
       grad_mode="sparse"    -> the uncoalesced sparse COO ``embedding_bag.weight.grad``
                                nn.EmbeddingBag(sparse=True) produces (one entry per
-                               lookup), for torch.optim.SGD,
+                               lookup), for torch.optim.SGD; by default each row's entries
+                               are pre-summed into its first one so the optimizer's
+                               scatter-add is deterministic (set_sparse_grad_form),
       grad_mode="fused_sgd" -> the update W -= lr * grad is applied inside the backward
                                kernel with torch.optim.SGD's rounding (per lookup, in order),
       grad_mode="dp"        -> the gradient is kept on device for
@@ -92,6 +94,23 @@ def raise_device_errors(flags: int) -> None:
     if flags:
         raise L.DQRMError(f"embedding kernels flagged device errors 0x{flags:x} (1 = index out of range, "
                           "2 = bad offsets, 4 = more lookups than max_lookups)")
+
+
+# grad_mode "sparse": the COO handed to the optimizer -- "presummed" (default: each row's
+# gradient summed in lookup order into its first lookup, zeros after it, so the optimizer's
+# scatter-add is deterministic) or "per_lookup" (one STE'd dy row per lookup, exactly what
+# nn.EmbeddingBag(sparse=True) yields; ATen's atomic scatter-add of duplicate rows then varies
+# in its last bits run to run on the GPU)
+_SPARSE_GRAD_FORM = os.environ.get("DQRM_SPARSE_GRAD", "presummed")
+
+
+def set_sparse_grad_form(form: str) -> None:
+    """The COO form of grad_mode="sparse" modules: "presummed" (deterministic optimizer step;
+    default) or "per_lookup" (nn.EmbeddingBag's own per-lookup entries)."""
+    global _SPARSE_GRAD_FORM
+    if form not in ("presummed", "per_lookup"):
+        raise ValueError("form must be 'presummed' or 'per_lookup'")
+    _SPARSE_GRAD_FORM = form
 
 
 def set_default_grad_mode(mode: str) -> None:
@@ -275,10 +294,13 @@ class _QuantEmbeddingBase(nn.Module):
         return self._sparse_grad(batch, dy, ste, layout)
 
     def _sparse_grad(self, batch, dy, ste, layout):
-        """The uncoalesced COO nn.EmbeddingBag(sparse=True) yields: one (row, STE'd dy row)
-        entry per lookup, in lookup order (one libdqrm launch, no host sync). torch.optim.SGD
-        then adds it to W exactly as it adds the reference's own embedding gradient."""
-        rows, vals = self._tset.lookup_grad(batch, dy, ste=ste, layout=layout)
+        """The uncoalesced COO nn.EmbeddingBag(sparse=True) yields: one entry per lookup, in
+        lookup order (one libdqrm launch, no host sync), which torch.optim.SGD adds to W as it
+        adds the reference's own embedding gradient. Form "presummed" (default): each row's
+        entries summed into its first one (the others +0.0), so that add is deterministic;
+        "per_lookup": one STE'd dy row per lookup (set_sparse_grad_form)."""
+        rows, vals = self._tset.lookup_grad(batch, dy, ste=ste, layout=layout,
+                                            presum=_SPARSE_GRAD_FORM == "presummed")
         self._ext_rows.append(rows)
         return torch.sparse_coo_tensor(rows.view(1, -1), vals, (self._tset.R, self._tset.D), is_coalesced=False)
 
@@ -509,5 +531,5 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         return out
 
 
-__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode",
+__all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode", "set_sparse_grad_form",
            "set_error_check_interval", "set_pooling_one_inputs", "consolidate_tables", "can_consolidate"]

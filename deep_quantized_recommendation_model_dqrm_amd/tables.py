@@ -501,10 +501,24 @@ class EmbeddingTableSet:
         )
 
     def lookup_grad(self, batch: LookupBatch, dy: torch.Tensor, ste: bool = True,
-                    layout: str = "tbd") -> tuple[torch.Tensor, torch.Tensor]:
+                    layout: str = "tbd", presum: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
         """Uncoalesced per-lookup sparse gradient (dqrm_emb_bwd_lookup_grad): slab rows
         i64 [L] and STE'd dy rows f32 [L, D], in lookup order -- the COO that
-        nn.EmbeddingBag(sparse=True)'s backward yields."""
+        nn.EmbeddingBag(sparse=True)'s backward yields. presum: the same rows with each row's
+        gradient summed (lookup order) into its first lookup and zeros after it
+        (dqrm_emb_bwd_lookup_grad_presum) -- an optimizer's scatter-add of it is deterministic;
+        batches of more than DQRM_PRESUM_MAX_LOOKUPS lookups per table take the per-lookup form."""
+        if presum and 0 < batch.max_lookups <= L.DQRM_PRESUM_MAX_LOOKUPS and batch.num_bags > 0:
+            st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
+            Lk = int(batch.idx.numel())
+            rows = torch.empty(Lk, dtype=torch.int64, device=self.device)
+            vals = torch.empty(Lk, self.D, dtype=torch.float32, device=self.device)
+            L.check(
+                self.lib.dqrm_emb_bwd_lookup_grad_presum(C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb,
+                                                         int(ste), _ptr(rows), _ptr(vals), _stream_handle()),
+                "dqrm_emb_bwd_lookup_grad_presum",
+            )
+            return rows, vals
         st, sb = self._dy_strides(dy, layout, self.T, batch.num_bags, self.D)
         Lk = int(batch.idx.numel())
         if batch.num_bags <= 0:  # no bag covers any lookup: an all-zero gradient on row 0

@@ -45,14 +45,16 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 7  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 8  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
                                6: residency-checked one launch (dqrm_bwd_apply_local_is_one_launch),
                                   dqrm_checksum64 mixes the full 64-bit position,
                                   dqrm_table_set.num_rows_host;
-                               7: dqrm_emb_fwd_after_update */
+                               7: dqrm_emb_fwd_after_update;
+                               8: dqrm_comm (RCCL communicator owned by libdqrm), dqrm_exchange
+                                  (the N > 1 exchange as two calls), dqrm_emb_bwd_lookup_grad_presum */
 
 /* status codes */
 #define DQRM_OK            0
@@ -527,6 +529,75 @@ int dqrm_checksum64(const void* data, int64_t num_words, uint64_t* out, void* st
  * with that all-reduce when every rank holds x; the identity for num_replicas 1, 2 and 4
  * with inv_n = 1/num_replicas (barring overflow of num_replicas * x), not for 3 or 8. */
 int dqrm_replica_mean(float* data, int64_t n, int num_replicas, float inv_n, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * The N > 1 exchange over RCCL (xGMI), issued from the library: the reference's 52 blocking
+ * Gloo collectives per step (2 per table, sgd_quantized_gradients_parallel_comm.py:865,878)
+ * become two ncclAllGather calls per step on a communicator libdqrm owns, each stream-ordered
+ * between the step's kernels, with no host round trip in between.
+ * ------------------------------------------------------------------------------ */
+typedef struct dqrm_comm dqrm_comm;
+
+/* RCCL's unique id (128 bytes) for dqrm_comm_init; called by one rank, which hands it to
+ * the others (the Python layer broadcasts it over the torch.distributed process group). The
+ * RCCL library is the one already loaded in the process (PyTorch's), else librccl.so.1. */
+int dqrm_comm_unique_id(void* id128);
+
+/* Collective over the `nranks` processes (one per GPU, each with the same id): creates this
+ * rank's communicator on the current HIP device. nranks == 1 is allowed (local copies). */
+int dqrm_comm_init(dqrm_comm** comm, int nranks, int rank, const void* id128);
+int dqrm_comm_destroy(dqrm_comm* comm);
+
+/* recv[r * bytes, (r+1) * bytes) <- rank r's send[0, bytes), in rank order, on `stream`
+ * (ncclAllGather of bytes uint8). */
+int dqrm_comm_allgather(dqrm_comm* comm, const void* send, void* recv, size_t bytes, void* stream);
+
+/* One rank's exchange state, all device buffers caller-owned and reused every step (the
+ * Python SparseGradExchange builds it once). */
+typedef struct dqrm_exchange {
+    const dqrm_table_set* set;
+    dqrm_comm* comm;            /* NULL: world size 1, no collective (num_ranks must be 1) */
+    int32_t num_ranks;          /* the communicator's size */
+    int32_t grad_bits;          /* 2..16 quantized, 32 = the unquantized FP32 path */
+    const int64_t* ws_cap_base; /* the coalesced-gradient workspace (dqrm_emb_bwd_coalesce) */
+    int64_t ws_cap_total;
+    int32_t* ws_rows;
+    float* ws_vals;
+    int32_t* ws_ucount;
+    float* ws_absmax;           /* [T*S] this rank's per-slot max|grad| */
+    float* absmax_all;          /* [num_ranks][T*S] gathered maxima (world size 1 without comm: ws_absmax) */
+    const int64_t* cap_base;    /* [T+1] payload capacity prefix */
+    int64_t cap_total;
+    float* s_avg;               /* [T] the averaged gradient scale (emb_scaling_factor) */
+    void* payload;              /* this rank's wire payload, dqrm_payload_bytes */
+    void* gathered;             /* [num_ranks][payload_bytes] (world size 1 without comm: payload) */
+    size_t payload_bytes;
+    void* workspace;            /* backward scratch, dqrm_bwd_workspace_bytes(T, max_lookups) */
+    size_t workspace_bytes;
+} dqrm_exchange;
+
+/* grad_update_parallel_comm's embedding branch for all tables (s_q_g_p_c.py:257-317 via
+ * quantize_emb_grad :850-890) in one call: dqrm_emb_bwd_coalesce -> all-gather of the per-slot
+ * maxima -> dqrm_grad_quant_pack_strided (rank scales averaged in Gloo's order) -> all-gather
+ * of the payloads. Same results as those calls made one by one. */
+int dqrm_exchange_grad(const dqrm_exchange* x, const dqrm_batch* batch, const float* dy,
+                       int64_t dy_stride_t, int64_t dy_stride_b, int ste, void* stream);
+
+/* weight_update_parallel_comm's embedding branch (s_q_g_p_c.py:601-628): decode the gathered
+ * payloads and apply (dqrm_apply_sparse_update_strided with mode / repack_bits). */
+int dqrm_exchange_apply(const dqrm_exchange* x, float lr, int mode, int repack_bits, void* stream);
+
+/* dqrm_emb_bwd_lookup_grad with duplicate rows pre-summed: same rows[], but vals[j] is the
+ * sum, in lookup order, of the STE'd dy rows of every lookup of row idx[j] when j is the
+ * row's FIRST lookup, and +0.0 for its later lookups. Handed to torch.optim.SGD
+ * (dlrm_s_pytorch_single_gpu.py:1943-1950) the scatter-add then adds one value per row
+ * (a zero entry adds -lr * 0 = -0.0, the identity), so W is bit-identical run to run;
+ * the COO sums to the same per-row gradient. Tables of more than DQRM_PRESUM_MAX_LOOKUPS
+ * lookups: DQRM_E_CAPACITY (nothing written). */
+#define DQRM_PRESUM_MAX_LOOKUPS 2048
+int dqrm_emb_bwd_lookup_grad_presum(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                                    int64_t dy_stride_t, int64_t dy_stride_b, int ste, int64_t* rows,
+                                    float* vals, void* stream);
 
 /* Synchronises `stream`, returns the accumulated DQRM_ERRF_* flags in *flags and
  * clears them (if clear != 0). */

@@ -32,7 +32,7 @@ def test_header_declares_what_binding_expects():
 def test_library_exports_every_header_symbol(lib):
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 7
+    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 8
 
 
 def test_payload_bytes_agree(lib):
@@ -44,6 +44,8 @@ def test_struct_layouts():
     # dqrm_table_set: 2 x i32 + 3 x i64 + 15 pointers (the last a host array); dqrm_batch: 3 pointers + 2 x i64
     assert C.sizeof(L.TableSet) == 8 + 24 + 15 * 8
     assert C.sizeof(L.Batch) == 6 * 8
+    # dqrm_exchange: 2 pointers + 2 x i32 + 15 eight-byte fields
+    assert C.sizeof(L.Exchange) == 2 * 8 + 8 + 15 * 8
 
 
 def test_invalid_arguments_rejected_without_device(lib):
@@ -55,6 +57,22 @@ def test_invalid_arguments_rejected_without_device(lib):
     assert b"dim" in lib.dqrm_last_error()
     assert lib.dqrm_grad_quant_pack(0, 16, None, 0, None, None, None, None, 1, 8, None, 0, None, None, None) == L.DQRM_E_INVALID
     assert lib.dqrm_grad_quant_pack(2, 16, None, 0, None, None, None, None, 1, 37, None, 0, None, None, None) == L.DQRM_E_INVALID
+
+
+def test_exchange_and_comm_reject_bad_arguments_without_device(lib):
+    """The N > 1 exchange entry points validate before touching RCCL or a device."""
+    assert lib.dqrm_exchange_grad(None, None, None, 0, 0, 1, None) == L.DQRM_E_INVALID
+    assert b"null exchange" in lib.dqrm_last_error()
+    x = L.Exchange()
+    ts = L.TableSet()
+    x.set = C.pointer(ts)
+    x.num_ranks = 2  # no communicator: only world size 1 is valid
+    assert lib.dqrm_exchange_apply(C.byref(x), 0.1, L.DQRM_UPD_DP, 0, None) == L.DQRM_E_INVALID
+    assert b"num_ranks" in lib.dqrm_last_error()
+    assert lib.dqrm_comm_init(None, 1, 0, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_comm_allgather(None, None, None, 0, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_comm_destroy(None) == L.DQRM_OK
+    assert lib.dqrm_emb_bwd_lookup_grad_presum(None, None, None, 0, 0, 1, None, None, None) == L.DQRM_E_INVALID
 
 
 def test_apply_kernel_selector(lib):

@@ -43,7 +43,16 @@ def _qebt(n, D, W, **kw):
     return QuantEmbeddingBagTwo(n, D, embedding_bit=4, embedding_id=0, weight=torch.from_numpy(W), **kw)
 
 
-def test_quant_embedding_bag_two_forward_and_sparse_grad(dq):
+@pytest.fixture
+def per_lookup_grads():
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+
+    Q.set_sparse_grad_form("per_lookup")
+    yield
+    Q.set_sparse_grad_form("presummed")
+
+
+def test_quant_embedding_bag_two_forward_and_sparse_grad(dq, per_lookup_grads):
     n, D = 5000, 16
     W = G.table_weights([n], D, 3)[0]
     (idx,), (off,) = G.random_bags([n], 64, 4, num_indices_per_lookup=5)
@@ -116,6 +125,82 @@ def test_sparse_grad_sgd_step_matches_kaggle_pool1(dq, golden_dir):
         total += got.size
     assert exact > total // 2  # most elements still agree to the bit
     assert all(m._tset.read_errors() == 0 for m in mods)
+
+
+@pytest.mark.parametrize("form", ["bags", "criteo"])
+def test_presummed_sparse_grad_is_the_coalesced_gradient(dq, form):
+    """The default grad_mode="sparse" COO (dqrm_emb_bwd_lookup_grad_presum): the reference's
+    shape -- one entry per lookup, indices = the lookups' rows, in lookup order -- with each
+    row's whole STE'd gradient, summed in lookup order, on its FIRST lookup and +0.0 on the
+    later ones: bit-exact against the oracle's ordered coalesce (s_q_g_p_c.py:859's
+    grad.coalesce() of the per-lookup COO), on bags (C1-style, duplicates within and across
+    bags) and on Criteo-form batches of a 3-row and a 40-row table (~700 / ~50 lookups per row)."""
+    D = 16
+    if form == "bags":
+        n = 50
+        W = G.table_weights([n], D, 3)[0]
+        (idx,), (off,) = G.random_bags([n], 128, 4, num_indices_per_lookup=10)
+    else:
+        n = 3
+        W = G.table_weights([n], D, 3)[0]
+        idx = G.pooling_one([n], 2048, 7)[0]
+        off = np.arange(2048, dtype=np.int64)
+    m = _qebt(n, D, W)
+    x, o = torch.from_numpy(idx).cuda(), torch.from_numpy(off).cuda()
+    y = m(x, o)
+    s = O.table_scale(W, 4)
+    dy = G.upstream_grad(1, len(off), D, 5)[0]
+    y.backward(torch.from_numpy(dy).cuda())
+    g = m.embedding_bag.weight.grad
+    assert g.is_sparse and not g.is_coalesced()
+    gi, gv = g._indices()[0].cpu().numpy(), g._values().cpu().numpy()
+    np.testing.assert_array_equal(gi, idx)
+    r_o, v_o, _ = O.emb_bwd_coalesce(n, idx, off, dy, s)
+    first = {}
+    for j, r in enumerate(idx):
+        first.setdefault(int(r), j)
+    for r, v in zip(r_o, v_o):
+        np.testing.assert_array_equal(gv[first[int(r)]], v)
+    later = np.array([first[int(r)] != j for j, r in enumerate(idx)])
+    assert later.any() and not gv[later].any()
+    assert not np.signbit(gv[later]).any()  # +0.0: the optimizer adds -lr * +0 = -0.0 (identity)
+    np.testing.assert_array_equal(g.coalesce().values().cpu().numpy(), v_o)
+    assert m._tset.read_errors() == 0
+
+
+def test_sparse_sgd_default_is_deterministic(dq):
+    """The unchanged single-GPU driver (26-style per-table modules + torch.optim.SGD on their
+    COO grads, dlrm_s_pytorch_single_gpu.py:1943-1950) with the default presummed COO: two
+    identical runs give bit-identical W over 4 steps on tables of 3..100k rows with heavy
+    duplicates (ATen's scatter-add of the per-lookup form varies there), and W stays within
+    1e-5 of the per-lookup (reference) form's result."""
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+
+    rows, D, B = [3, 10, 27, 5000, 100000], 16, 2048
+    Ws = G.table_weights(rows, D, 41)
+    P = [G.pooling_one(rows, B, 50 + k, dist="zipf") for k in range(4)]
+    dys = [G.upstream_grad(len(rows), B, D, 60 + k) * 10 for k in range(4)]
+
+    def run(form):
+        Q.set_sparse_grad_form(form)
+        try:
+            mods = nn.ModuleList([_qebt(n, D, w, grad_mode="sparse") for n, w in zip(rows, Ws)])
+            opt = torch.optim.SGD([m.embedding_bag.weight for m in mods], lr=0.1)
+            off = torch.arange(B, device="cuda")
+            for k in range(4):
+                opt.zero_grad()
+                ys = [m(torch.from_numpy(P[k][t]).cuda(), off) for t, m in enumerate(mods)]
+                torch.autograd.backward(ys, [torch.from_numpy(dys[k][t]).cuda() for t in range(len(rows))])
+                opt.step()
+            assert all(m._tset.read_errors() == 0 for m in mods)
+            return [m.embedding_bag.weight.detach().clone() for m in mods]
+        finally:
+            Q.set_sparse_grad_form("presummed")
+
+    a, b, ref = run("presummed"), run("presummed"), run("per_lookup")
+    for x, y, z in zip(a, b, ref):
+        assert torch.equal(x, y)
+        torch.testing.assert_close(x, z, rtol=0, atol=1e-5)
 
 
 def test_quant_embedding_bag_two_fused_sgd(dq):

@@ -4,15 +4,15 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $R && mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 120 --timeout-method thread \
-    -k "alternating or sgd_small_criteo" > gpurun_out/r5b_tests.log 2>&1 || { tail -n 30 gpurun_out/r5b_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/r5b_tests.log 2>&1 || { tail -n 30 gpurun_out/r5b_tests.log; exit 1; }
 tail -n 2 gpurun_out/r5b_tests.log
 for B in 2048 256; do
   timeout -k 10 300 python -u tools/prof_exchange.py terabyte_ref $B 200 > gpurun_out/r5b_host_$B.log 2>&1 || { tail -n 20 gpurun_out/r5b_host_$B.log; exit 1; }
   tail -n 1 gpurun_out/r5b_host_$B.log
 done
 A="--steps 200 --warmup 20 --force-collectives --cpu-baseline 0 --gather-batch 0 --mlp-iters 0"
-for v in "flat|" "slot|DQRM_APPLY=slot" "inline|DQRM_FINALIZE=inline"; do
+for v in "flat|" "qlegacy|DQRM_QPACK=legacy" "slot|DQRM_APPLY=slot" "inline|DQRM_FINALIZE=inline"; do
   lab=${v%%|*}; envs=${v#*|}
   env $envs timeout -k 10 300 python -u bench.py $A > gpurun_out/r5b_ab_$lab.log 2>&1 || { tail -n 20 gpurun_out/r5b_ab_$lab.log; exit 1; }
   tail -n 1 gpurun_out/r5b_ab_$lab.log | python3 -c "

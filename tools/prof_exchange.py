@@ -37,9 +37,24 @@ kern = ex.kernels
 names = ["forward", "coalesce", "allgather_scales", "quant_pack", "allgather_payload", "apply"]
 
 
+LIB = ex._x is not None and os.environ.get("PROF_SPLIT", "0") != "1"
+if LIB:
+    names = ["forward", "exchange_grad", "exchange_apply"]
+
+
 def step(i, clk=None):
     b = batches[i % 8]
     t = [time.perf_counter()]
+    if LIB:  # the library-issued exchange: two host calls
+        ts.forward(b, bits=4, refresh_scale=True, out=y)
+        t.append(time.perf_counter())
+        ex.exchange(b, dy)
+        t.append(time.perf_counter())
+        ex.apply(0.1, mode=L.DQRM_UPD_DP)
+        t.append(time.perf_counter())
+        if clk is not None:
+            clk.append(np.diff(t))
+        return
     ts.forward(b, bits=4, refresh_scale=True, out=y)
     t.append(time.perf_counter())
     kern.coalesce(b, dy, ex.ws, True, "tbd")
@@ -77,7 +92,7 @@ torch.cuda.synchronize()
 wall = (time.perf_counter() - t0) / steps * 1e6
 # host issue rate with the device never waited on (bounded by the device when it is slower)
 per = {n: (round(float(np.median(c[:, j])), 2), round(float(np.mean(c[:, j])), 2)) for j, n in enumerate(names)}
-print({"config": cfg, "batch_per_gpu": B, "host_us_median_mean": per,
+print({"config": cfg, "batch_per_gpu": B, "library_exchange": LIB, "host_us_median_mean": per,
        "host_issue_us_per_step_median": round(float(np.median(c.sum(1))), 2),
        "synced_us_per_step": round(wall, 2)})
 dist.destroy_process_group()
