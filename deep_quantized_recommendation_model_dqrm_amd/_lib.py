@@ -40,6 +40,7 @@ DQRM_UPD_FP32 = 2
 DQRM_APPLY_AUTO = 0
 DQRM_APPLY_FLAT = 1
 DQRM_APPLY_SLOT = 2
+DQRM_APPLY_RANGES = 3
 DQRM_COALESCE_AUTO = 0
 DQRM_COALESCE_GENERAL = 1
 

@@ -118,4 +118,35 @@ struct PresumArgs {
 };
 hipError_t launch_lookup_grad_presum(const PresumArgs& a, hipStream_t stream);
 
+// K6 with row ranges owned per workgroup (dqrm_apply.hip, DQRM_APPLY_RANGES): the gathered
+// payloads decoded, summed over ranks, applied, and the |W| hierarchy finalized in-launch.
+struct RangeApplyArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    uint8_t* sdirty;
+    uint8_t* bdirty;
+    float* tmax;
+    uint32_t* sync;
+    const float* pscale;
+    const int64_t* meta;
+    uint32_t* err;
+    const int64_t* cap_base;
+    int64_t cap_total;
+    const unsigned char* payloads;  // rank r's payload at payloads + r * rank_pitch
+    int64_t rank_pitch;
+    int N;
+    int T;
+    int D;
+    int bits;
+    const float* s_avg;
+    float nlr;
+    int mode;
+    int repack;
+    int K;                          // chunks per row-range slot
+};
+hipError_t launch_apply_ranges(const RangeApplyArgs& a, hipStream_t stream);
+
 }  // namespace dqrm_internal

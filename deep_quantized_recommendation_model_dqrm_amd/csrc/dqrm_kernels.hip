@@ -3704,7 +3704,8 @@ int apply_kernel_kind() {
     int k = g_apply_kernel.load();
     if (k < 0) {
         const char* e = getenv("DQRM_APPLY");
-        k = (e && !strcmp(e, "flat")) ? DQRM_APPLY_FLAT : (e && !strcmp(e, "slot")) ? DQRM_APPLY_SLOT : DQRM_APPLY_AUTO;
+        k = (e && !strcmp(e, "flat")) ? DQRM_APPLY_FLAT : (e && !strcmp(e, "slot")) ? DQRM_APPLY_SLOT
+            : (e && !strcmp(e, "ranges")) ? DQRM_APPLY_RANGES : DQRM_APPLY_AUTO;
         int expect = -1;
         g_apply_kernel.compare_exchange_strong(expect, k);
         k = g_apply_kernel.load();
@@ -3832,8 +3833,8 @@ int dqrm_set_coalesce_kernel(int kind) {
 }
 
 int dqrm_set_apply_kernel(int kind) {
-    if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_SLOT)
-        return set_error(DQRM_E_INVALID, "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat) or 2 (slot)");
+    if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_RANGES)
+        return set_error(DQRM_E_INVALID, "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat), 2 (slot) or 3 (ranges)");
     const int prev = apply_kernel_kind();
     g_apply_kernel.store(kind);
     return prev;
@@ -4264,6 +4265,19 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
     const int D = set->dim;
     const int kind = apply_kernel_kind();
     bool flat = false;
+    if (kind == DQRM_APPLY_RANGES) {
+        // chunks per slot: the payload capacity of all ranks spread over the slots, ~48
+        // entries per workgroup (at least 1, at most 64)
+        const int64_t slots = (int64_t)a.T * SPLIT;
+        int64_t K = ((int64_t)num_ranks * cap_total + slots * 48 - 1) / (slots * 48);
+        K = K < 1 ? 1 : (K > 64 ? 64 : K);
+        dqrm_internal::RangeApplyArgs r{a.W, a.packed, a.rowmax, a.blkmax, a.sblkmax, a.sdirty, a.bdirty, a.tmax,
+                                        a.sync, a.pscale, a.meta, a.err, cap_base, cap_total, a.payloads,
+                                        (int64_t)rank_pitch, num_ranks, a.T, D, grad_bits, s_avg, -lr, mode,
+                                        a.repack, (int)K};
+        HIP_TRY(dqrm_internal::launch_apply_ranges(r, st));
+        return DQRM_OK;  // the |W| hierarchy is finalized inside the launch
+    }
     // AUTO: flat while each lane of a row's group searches at most one other rank
     // (num_ranks < D/4), slot beyond (tools/bench_apply_ranks.py)
     if (kind == DQRM_APPLY_SLOT || (kind == DQRM_APPLY_AUTO && num_ranks > 1 && num_ranks >= D / 4)) {

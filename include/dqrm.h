@@ -390,6 +390,11 @@ int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_bat
 #define DQRM_APPLY_AUTO 0
 #define DQRM_APPLY_FLAT 1
 #define DQRM_APPLY_SLOT 2
+/* RANGES: one workgroup per block-aligned row range (a row-range slot cut in chunks) with
+ * every rank's entries of it, rows owned: shrunk block maxima re-reduced in the workgroup,
+ * the table's last workgroup re-reduces flagged superblocks -- no finalize launch
+ * (DQRM_APPLY=ranges) */
+#define DQRM_APPLY_RANGES 3
 int dqrm_set_apply_kernel(int kind);
 
 /* Which backward kernels dqrm_emb_bwd_coalesce and dqrm_emb_bwd_sgd launch (process-wide;

@@ -79,7 +79,9 @@ def test_apply_kernel_selector(lib):
     prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_SLOT)
     try:
         assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_SLOT
-        assert lib.dqrm_set_apply_kernel(3) == L.DQRM_E_INVALID
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_RANGES) == L.DQRM_APPLY_FLAT
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_RANGES
+        assert lib.dqrm_set_apply_kernel(4) == L.DQRM_E_INVALID
         assert b"kind" in lib.dqrm_last_error()
         assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_AUTO) == L.DQRM_APPLY_FLAT
     finally:

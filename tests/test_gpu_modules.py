@@ -173,7 +173,7 @@ def test_sparse_sgd_default_is_deterministic(dq):
     COO grads, dlrm_s_pytorch_single_gpu.py:1943-1950) with the default presummed COO: two
     identical runs give bit-identical W over 4 steps on tables of 3..100k rows with heavy
     duplicates (ATen's scatter-add of the per-lookup form varies there), and W stays within
-    1e-5 of the per-lookup (reference) form's result."""
+    1e-5 (relative) of the per-lookup (reference) form's result."""
     from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
 
     rows, D, B = [3, 10, 27, 5000, 100000], 16, 2048
@@ -200,7 +200,7 @@ def test_sparse_sgd_default_is_deterministic(dq):
     a, b, ref = run("presummed"), run("presummed"), run("per_lookup")
     for x, y, z in zip(a, b, ref):
         assert torch.equal(x, y)
-        torch.testing.assert_close(x, z, rtol=0, atol=1e-5)
+        torch.testing.assert_close(x, z, rtol=1e-5, atol=1e-5)  # |W| reaches ~7 here (dy x 10)
 
 
 def test_quant_embedding_bag_two_fused_sgd(dq):

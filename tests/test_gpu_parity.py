@@ -29,12 +29,13 @@ def dq():
     return d
 
 
-@pytest.fixture(params=["flat", "slot"])
+@pytest.fixture(params=["flat", "slot", "ranges"])
 def apply_kernel(request, dq):
     """Run the test once per dqrm_apply_sparse_update kernel (the AUTO choice depends on N)."""
     L = dq._lib
     lib = L.load()
-    prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT if request.param == "flat" else L.DQRM_APPLY_SLOT)
+    kind = {"flat": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT, "ranges": L.DQRM_APPLY_RANGES}[request.param]
+    prev = lib.dqrm_set_apply_kernel(kind)
     yield request.param
     lib.dqrm_set_apply_kernel(prev)
 
