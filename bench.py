@@ -128,8 +128,8 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "bwd_coalesce": ("k_coalesce_p1<false,", "k_coalesce_p1<false>", "k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),
     "bwd_apply_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),  # N=1: coalesce + update in one launch
     "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
-    "grad_quant_pack": "k_quant_pack<{lpr}>",
-    "apply_sparse_update": "k_apply_flat<{lpr},",
+    "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
+    "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_ranges<{lpr}>"),
     "apply_local": "k_apply_local<{lpr},",
 }
 
@@ -473,7 +473,8 @@ def main():
                  "coalesce + dqrm_apply_local" if fused else "coalesce + quant-pack + payload apply")
     workload = {"config": a.config, "mode": a.mode, "batch_per_gpu": B, "n1_update": n1_update,
                 "index_dist": a.index_dist}
-    prof = a.traffic_profile or latest_profile(PROFILE_TAG[a.config])
+    # (the forced-collectives N > 1 form is profiled under its own tag, e.g. r5_tbforced)
+    prof = a.traffic_profile or latest_profile(PROFILE_TAG[a.config] + ("forced" if coll and world == 1 else ""))
     traffic = pmc_traffic(prof, dom, D, workload)
     med_us = traffic["profiled_median_us"] if traffic else None
     if rank == 0:

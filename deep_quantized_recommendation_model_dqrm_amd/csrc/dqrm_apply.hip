@@ -55,24 +55,22 @@ __global__ void __launch_bounds__(AR_TPB) k_apply_ranges(dqrm_internal::RangeApp
     const int tid = threadIdx.x, lane = tid % WAVE, w = tid / WAVE;
     const int T = a.T, N = a.N;
     const int64_t rb = a.meta[t], nrows = a.meta[T + t], bb = a.meta[2 * T + t], sbb = a.meta[3 * T + t];
-    const int64_t nblk = (nrows + BLK - 1) / BLK;
+    const uint32_t nblk = (uint32_t)((nrows + BLK - 1) / BLK);
     // this workgroup's blocks: the slot's (dqrm_emb_bwd_coalesce's row-range slots) cut in K
-    auto chunk = [&](int ss, int kk, int64_t& c0, int64_t& c1) {
-        const int64_t s0 = nblk * ss / SPLIT, s1 = nblk * (ss + 1) / SPLIT;
-        c0 = s0 + (s1 - s0) * kk / K;
-        c1 = s0 + (s1 - s0) * (kk + 1) / K;
-    };
-    int64_t b0, b1;
-    chunk(s, k, b0, b1);
+    // (32-bit arithmetic: a slot has < 2^26 blocks, K <= 64)
+    auto slot0 = [&](int ss) { return (uint32_t)(((uint64_t)nblk * (uint32_t)ss) >> 3); };
+    static_assert(SPLIT == 8, "slot bounds by shifts");
+    const uint32_t s0 = slot0(s), nb = slot0(s + 1) - s0;
+    const uint32_t b0 = s0 + nb * (uint32_t)k / (uint32_t)K, b1 = s0 + nb * (uint32_t)(k + 1) / (uint32_t)K;
     if (b0 >= b1) return;  // no rows (and no arrival: not counted below)
-    uint32_t expected = 0;  // the table's workgroups with rows
-    for (int ss = 0; ss < SPLIT; ++ss)
-        for (int kk = 0; kk < K; ++kk) {
-            int64_t c0, c1;
-            chunk(ss, kk, c0, c1);
-            expected += c0 < c1 ? 1u : 0u;
-        }
-    const int64_t row_lo = b0 * BLK, row_hi = b1 * BLK < nrows ? b1 * BLK : nrows;
+    // the table's workgroups with rows: a slot of nb blocks has min(nb, K) non-empty chunks
+    uint32_t expected = 0;
+#pragma unroll
+    for (int ss = 0; ss < SPLIT; ++ss) {
+        const uint32_t n_s = slot0(ss + 1) - slot0(ss);
+        expected += n_s < (uint32_t)K ? n_s : (uint32_t)K;
+    }
+    const int64_t row_lo = (int64_t)b0 * BLK, row_hi = (int64_t)b1 * BLK < nrows ? (int64_t)b1 * BLK : nrows;
     const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
     const int64_t cb = a.cap_base[t], cap = a.cap_base[t + 1] - cb;
     auto rows_of = [&](int r) {
@@ -104,15 +102,19 @@ __global__ void __launch_bounds__(AR_TPB) k_apply_ranges(dqrm_internal::RangeApp
     __syncthreads();
     // 2. K > 1: the chunk's run in each rank = [#rows < row_lo, #rows < row_hi) of the slot's
     //    ascending rows (every rank's slot rows loaded once, counted with LDS adds)
-    if (K > 1) {
-        int tot = 0;
-        for (int r = 0; r < N; ++r) tot += s_cnt[r];
-        for (int i = tid; i < tot; i += AR_TPB) {
-            int r = 0, base = 0;
-            while (i >= base + s_cnt[r]) { base += s_cnt[r]; ++r; }
-            const int32_t x = rows_of(r)[s_pre[r] + (i - base)];
-            if (x < row_lo) atomicAdd(&s_lo[r], 1);
-            if (x < row_hi) atomicAdd(&s_hi[r], 1);
+    if (K > 1) {  // per rank: wave ballots, one LDS add per wave
+        for (int r = 0; r < N; ++r) {
+            const int32_t* rows = rows_of(r) + s_pre[r];
+            const int n = s_cnt[r];
+            for (int i0 = w * WAVE; i0 < n; i0 += AR_TPB) {
+                const int i = i0 + lane;
+                const int32_t x = i < n ? rows[i] : 0x7fffffff;
+                const int nlo = __popcll(__ballot(x < row_lo)), nhi = __popcll(__ballot(x < row_hi));
+                if (lane == 0) {
+                    if (nlo) atomicAdd(&s_lo[r], nlo);
+                    if (nhi) atomicAdd(&s_hi[r], nhi);
+                }
+            }
         }
         __syncthreads();
     }

@@ -469,6 +469,102 @@ __device__ __forceinline__ uint64_t gr_make(float m, int count, uint32_t epoch) 
 static_assert(MAXB < (1 << 13), "distinct-row count field of a granule");
 
 
+constexpr int STALL_WORD = 3;  // a table's sync word: bit (s + 8 j) = workgroup (slot s, sub-slot j) stalled
+
+// The table's last-arriving workgroup, when some of the table's workgroups gave up waiting at
+// the rendezvous (stall_mask): every workgroup published its granule before it arrived, so the
+// table scale is known now; the stalled workgroups' entries (left in the workspace: rows, and
+// values the stalled workgroup spilled or a dimension-split table's workgroups stored) are
+// quantized and applied here with dqrm_apply_local's arithmetic, their blocks flagged for the
+// finalize that follows (the rows are not this workgroup's). The table's update is then
+// complete -- never half-applied; DQRM_ERRF_STALL still reports the stall.
+__device__ __forceinline__ void recover_stalled(const dqrm_internal::CoalesceArgs& a, const dqrm_internal::LocalApplyArgs& la,
+                                             int t, uint32_t stall_mask, const uint64_t* gran, int NG, int K,
+                                             bool dsplit, int NA, int64_t nblk, const int64_t* s_cb) {
+    __shared__ float s_sv;
+    __shared__ int s_cnt_g[2 * SPLIT];
+    const int tid = threadIdx.x;
+    if (tid < WAVE) {  // the table scale from every granule (all published by now)
+        const uint64_t g = tid < NG ? __hip_atomic_load(gran + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const float am = wave_max(tid < NG ? __uint_as_float((uint32_t)g) : 0.0f);
+        if (tid < NG) s_cnt_g[tid] = gr_count(g);
+        if (tid == 0) {
+            s_sv = sym_scale(am, la.bits) * (float)(1.0 / 1.0);
+            la.s_avg[t] = s_sv;
+        }
+        if (K == 2 && tid < SPLIT && ((stall_mask >> tid) & 1u)) {  // sub-slot 0 stalled: its slot's count / max
+            const uint64_t g1 = __hip_atomic_load(gran + SPLIT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int c = gr_count(g) + gr_count(g1);
+            const int64_t cap = s_cb[tid + 1] - s_cb[tid];
+            c = c < cap ? c : (int)cap;
+            a.ws_ucount[t * SPLIT + tid] = c;
+            a.ws_absmax[t * SPLIT + tid] = fmaxf(__uint_as_float((uint32_t)g), __uint_as_float((uint32_t)g1));
+        }
+    }
+    __syncthreads();
+    const float sv = s_sv, rr = 1.0f / sv;
+    const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
+    const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
+    const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
+    const int D = a.D, LPR = D / 4, lpr_sh = __ffs(LPR) - 1;
+    const int64_t rb = a.meta[t], nrows = a.meta[a.T + t], bb = a.meta[2 * a.T + t], sbb = a.meta[3 * a.T + t];
+    (void)nblk;
+    auto apply_range = [&](int64_t e0, int64_t e1) {  // workspace entries [e0, e1)
+        for (int64_t q = tid; q < ((e1 - e0) << lpr_sh); q += TPB) {
+            const int64_t e = e0 + (q >> lpr_sh);
+            const int sub = (int)(q & (LPR - 1));
+            const int64_t x = (int64_t)(int32_t)ld_wt(reinterpret_cast<const uint32_t*>(a.ws_rows + e));
+            const float4 v = ld4_sc1(a.ws_vals + e * D, (uint32_t)sub * 16u);
+            const bool ok = x >= 0 && x < nrows;
+            const int64_t grow = rb + (ok ? x : 0);
+            const float4 w0 = reinterpret_cast<const float4*>(la.W + grow * D)[sub];
+            float4 acc, wn;
+            acc.x = fake_quant(v.x, rr, qlo, qhi) + 0.0f; acc.y = fake_quant(v.y, rr, qlo, qhi) + 0.0f;
+            acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
+            wn.x = upd(w0.x, acc.x); wn.y = upd(w0.y, acc.y); wn.z = upd(w0.z, acc.z); wn.w = upd(w0.w, acc.w);
+            if (ok) {
+                reinterpret_cast<float4*>(la.W + grow * D)[sub] = wn;
+                if (la.repack) pack4_row(wn, la.packed + grow * (D / 2), sub, r_pack);
+            }
+            float old_rm = abs_max4(w0), rm = abs_max4(wn);
+            for (int o = 1; o < LPR; o <<= 1) {
+                old_rm = fmaxf(old_rm, __shfl_xor(old_rm, o, WAVE));
+                rm = fmaxf(rm, __shfl_xor(rm, o, WAVE));
+            }
+            if (sub != 0 || !ok) continue;
+            st_wt(la.rowmax + grow, rm);
+            const int64_t blk = x >> 8, sb = sbb + (blk >> 8);
+            const float oblk = la.blkmax[bb + blk];
+            if (rm > oblk) {
+                atomicMax(reinterpret_cast<unsigned int*>(la.blkmax) + bb + blk, __float_as_uint(rm));
+                atomicMax(reinterpret_cast<unsigned int*>(la.sblkmax) + sb, __float_as_uint(rm));
+                atomicMax(reinterpret_cast<unsigned int*>(la.tmax) + t, __float_as_uint(rm));
+            }
+            if (old_rm == oblk && rm < old_rm) {  // held its block's max: the finalize re-reduces it
+                flag_set(la.bdirty, bb + blk);
+                flag_set(la.sdirty, sb);
+            }
+        }
+    };
+    for (uint32_t m = stall_mask; m; m &= m - 1) {  // uniform
+        const int gi = __ffs((int)m) - 1, sg = gi % SPLIT, jg = gi / SPLIT;
+        if (dsplit) {  // the row-range slots this workgroup would have updated
+            for (int sl = sg; sl < SPLIT; sl += NA) {
+                int c = (int)ld_wt(reinterpret_cast<const uint32_t*>(a.ws_ucount + t * SPLIT + sl));
+                const int64_t cap = s_cb[sl + 1] - s_cb[sl];
+                c = c < 0 ? 0 : (c > cap ? (int)cap : c);
+                apply_range(s_cb[sl], s_cb[sl] + c);
+            }
+        } else {
+            int c = s_cnt_g[gi];
+            const int64_t cap = s_cb[sg + 1] - s_cb[sg];
+            c = c < cap ? c : (int)cap;
+            if (K == 1 || jg == 0) apply_range(s_cb[sg], s_cb[sg] + c);
+            else apply_range(s_cb[sg + 1] - c, s_cb[sg + 1]);
+        }
+    }
+}
+
 // APPLY (dqrm_emb_bwd_apply_local, world size 1): after the coalesce, the table's workgroups
 // meet once (each publishes its max|grad|, then waits for the table's others: all of them are
 // resident, one per CU), and each updates the rows of its row-range slot exactly as
@@ -497,6 +593,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_oq_n;
     __shared__ int s_dirty;
     __shared__ int s_fin;
+    __shared__ int s_stallmask;
     __shared__ uint32_t s_oq_blk[OWN_Q];
     __shared__ float s_oq_old[OWN_Q];
     __shared__ float s_oq_sold[OWN_Q];
@@ -1200,9 +1297,11 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             if (__all(ok)) break;
             // the table's workgroups were not all resident (the host checks the device's CUs,
             // the occupancy and the stream's CU mask before it launches this form; another
-            // stream's kernels can still hold CUs): flagged, no hang -- and this workgroup
-            // does NOT update its rows, since the table scale would come from stale maxima
-            if (spin > (1 << 20)) {
+            // stream's kernels can still hold CUs): flagged, no hang -- this workgroup does
+            // not update its rows itself (the table scale would come from stale maxima); it
+            // leaves them in the workspace for the table's last-arriving workgroup, which has
+            // every slot's maximum by then (all-or-nothing per table)
+            if (spin > (int)la.spin_limit) {
                 if (tid == 0) flag_error(a.err, DQRM_ERRF_STALL);
                 stalled = true;
                 break;
@@ -1217,7 +1316,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const float mpart = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, p));
             if (tid == 0) {
                 s_upart = upart;
-                if (j == 0) {  // the slot's count and partial maximum, as one workgroup would write them
+                if (j == 0 && !stalled) {  // the slot's count and partial maximum, as one workgroup would write them
                     int c = U + upart;
                     const int64_t cap = s_cb[s + 1] - s_cb[s];
                     if (c > cap) {
@@ -1252,7 +1351,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // the update of dqrm_apply_local: s = clamp(max|g|, 1e-8) / (2^(bits-1)-1) (* 1/N,
         // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
         const float sv = sym_scale(s_am, la.bits) * (float)(1.0 / 1.0);
-        const bool go = s_stall == 0;  // a stalled workgroup leaves its rows as they were
+        const bool go = s_stall == 0;  // a stalled workgroup leaves its rows to the last arriver
         if (go && s == 0 && j == 0 && tid == 0) la.s_avg[t] = sv;
         const float rr = 1.0f / sv;
         const float qlo = -(float)(1 << (la.bits - 1)), qhi = (float)((1 << (la.bits - 1)) - 1);
@@ -1326,6 +1425,26 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             return dsplit ? ld4_sc1(vb, (uint32_t)q * 16u) : reinterpret_cast<const float4*>(vb)[q];
         };
         auto load_val = [&](const float* vb, int q) -> float4 { return lds_vals ? lds_val(q) : mem_val(vb, q); };
+        if (!go && !dsplit) {
+            // a row-split slot's entries [ebase, ebase + nu0) re-stored write-through (sc1: the
+            // last arriver may run on another XCD, whose L2 never saw this one's plain stores):
+            // values from the LDS stage or back from this workgroup's own workspace stores, rows
+            // from its keys (a dimension-split table's values are stored write-through already,
+            // its workgroups' hand-off; they share one XCD with their rows' writer)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            for (int q = tid; q < (nu0 << lpr_sh); q += TPB) {
+                const int u = q >> lpr_sh, sub = q & (LPR - 1);
+                const int64_t e = ebase() + u;
+                float4* dst = reinterpret_cast<float4*>(a.ws_vals + e * a.D) + sub;
+                st4_wt(dst, lds_vals ? lds_val(q) : *dst);
+                if (sub == 0)
+                    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.ws_rows + e),
+                                       (uint32_t)(r0 + krow(keys[hpos[u]])), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (!go && tid == 0)  // recorded before this workgroup's arrival (ordered by its vmcnt(0))
+            atomicOr(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + STALL_WORD, 1u << (s + SPLIT * j));
         // vmcnt counts loads and stores in issue order: a load still pending when the update's
         // stores have been issued is waited for with vmcnt(0), i.e. after every one of them. So
         // the prefetched W rows and block maxima (landed during the rendezvous) are waited for
@@ -1433,7 +1552,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             }
         }
         if (dirty) s_dirty = 1;
-        if (j == 1) {  // sub-slot 1's rows, at their place after sub-slot 0's entries
+        if (j == 1 && go) {  // sub-slot 1's rows, at their place after sub-slot 0's entries (stalled: left for the recovery)
             const int nr = U < (int)(s_cb[s + 1] - s_cb[s]) - s_upart ? U : (int)(s_cb[s + 1] - s_cb[s]) - s_upart;
             for (int u = tid; u < nr; u += TPB) a.ws_rows[s_cb[s] + s_upart + u] = (int32_t)(r0 + krow(keys[hpos[u]]));
         }
@@ -1450,10 +1569,22 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const uint32_t add = 1u + (s_dirty ? DIRTY_ONE : 0u);
             const uint32_t now = atomicAdd(cnt, add) + add;
             const bool last = (now & (DIRTY_ONE - 1u)) == (uint32_t)NG;
-            if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_fin = last && (now >> 16) != 0u;
+            uint32_t sm = 0u;
+            if (last) {
+                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sm = ld_wt(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + STALL_WORD);
+                if (sm) __hip_atomic_store(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + STALL_WORD, 0u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_stallmask = (int)sm;
+            s_fin = last && ((now >> 16) != 0u || sm != 0u);
         }
         __syncthreads();
+        if (s_stallmask) {  // uniform, rare: apply the stalled workgroups' rows (then finalize)
+            recover_stalled(a, la, t, (uint32_t)s_stallmask, gran, NG, K, dsplit, NA, nblk, s_cb);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         if (s_fin)
             finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
                                  la.bdirty, la.tmax, a.D, true, false);
@@ -1556,8 +1687,14 @@ hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la
     const bool rm = DQRM_COAL_ROWMAJOR == 2 || (DQRM_COAL_ROWMAJOR == 1 && a.D >= 32);  // stage layout
     if (la) {
         if (!coalesce_apply_resident(a.T, stream)) return hipErrorInvalidValue;  // not all resident at once
-        if (rm) hipLaunchKernelGGL((k_coalesce_p1<true, true>), grid, dim3(TPB), LDS_BYTES, stream, a, *la);
-        else hipLaunchKernelGGL((k_coalesce_p1<true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, *la);
+        static const uint32_t spin = [] {  // DQRM_STALL_SPIN: rendezvous polls before a stall (tests)
+            const char* e = getenv("DQRM_STALL_SPIN");
+            return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 20);
+        }();
+        LocalApplyArgs l2 = *la;
+        l2.spin_limit = spin;
+        if (rm) hipLaunchKernelGGL((k_coalesce_p1<true, true>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
+        else hipLaunchKernelGGL((k_coalesce_p1<true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
     } else {
         if (rm) hipLaunchKernelGGL((k_coalesce_p1<false, true>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
         else hipLaunchKernelGGL((k_coalesce_p1<false, false>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});

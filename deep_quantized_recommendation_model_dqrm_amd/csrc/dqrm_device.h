@@ -136,6 +136,15 @@ DQRM_INLINE bool flag_get(const uint8_t* f, int64_t i) {
     return ((ld_wt(w) >> sh) & 0xFFu) != 0u;
 }
 
+// Word FLAG_WORD of a table's sync words: set (atomicOr) by the flat apply kernels whenever
+// they flag a block / superblock of the table; the finalize launch that follows them skips a
+// table whose word is clear (its |W| maxima are exact already: growth went in by atomicMax)
+// and clears it otherwise.
+constexpr int FLAG_WORD = 2;
+DQRM_INLINE void mark_table_flagged(uint32_t* sync, int t) {
+    atomicOr(sync + (int64_t)t * DQRM_SYNC_STRIDE + FLAG_WORD, 1u);
+}
+
 // loads of the finalize: sc1 inside the updating launch (WT), plain in a launch of its own
 template <bool WT> DQRM_INLINE float ld_h(const float* p) { if constexpr (WT) return ld_wt(p); else return *p; }
 template <bool WT> DQRM_INLINE uint32_t ld_h(const uint32_t* p) { if constexpr (WT) return ld_wt(p); else return *p; }

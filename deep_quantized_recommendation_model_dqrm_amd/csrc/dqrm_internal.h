@@ -52,6 +52,9 @@ struct LocalApplyArgs {
     // (-1: idle); bit t of sub_mask = table t's slots are halved between two workgroups
     uint32_t sub_mask;
     int8_t sub_table[32];
+    // rendezvous polls before a workgroup gives up (DQRM_ERRF_STALL; its rows are then applied
+    // by the table's last-arriving workgroup); the host sets it (DQRM_STALL_SPIN, default 2^20)
+    uint32_t spin_limit;
 };
 constexpr int kSubTables = 32;  // LocalApplyArgs::sub_table entries
 

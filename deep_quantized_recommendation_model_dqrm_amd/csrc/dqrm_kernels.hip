@@ -1149,14 +1149,24 @@ DQRM_INLINE void maintain_blocks(const Meta& m, int t, const SlotLds& sl, int U,
 // One workgroup per table after the slot kernels (a kernel boundary is the cheap way to
 // make the slots' writes visible here: an agent-scope fence inside the slot kernel, e.g. a
 // "last workgroup finalizes" counter, writes back the XCD's L2 and measured 2x slower).
+// flagged (after the flat apply kernels, which keep every table's maxima -- narrow ones
+// included -- exact but for the blocks / superblocks they flagged, and mark such tables in
+// FLAG_WORD): a table that flagged nothing is skipped after one load.
 __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict__ W, float* __restrict__ rowmax,
                                                          float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                                          uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty,
                                                          float* __restrict__ tmax,
                                                          const int64_t* __restrict__ meta, int T, int D,
-                                                         int tracked) {
+                                                         int tracked, uint32_t* __restrict__ sync, int flagged) {
     const Meta m = make_meta(meta, T);
-    finalize_table<false>(m, blockIdx.x, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0);
+    const int t = blockIdx.x;
+    if (flagged) {
+        uint32_t* fw = sync + (int64_t)t * DQRM_SYNC_STRIDE + FLAG_WORD;
+        if (*fw == 0u) return;  // uniform
+        __syncthreads();  // every thread has read the word before it is cleared
+        if (threadIdx.x == 0) *fw = 0u;
+    }
+    finalize_table<false>(m, t, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0, flagged == 0);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -1749,7 +1759,7 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
     // the superblock and table maxima with the row (DQRM_FLAT_PRELOAD): no dependent round trips
     // on growth, which early in training is every row of a big table; a stale-low value only
     // costs a redundant atomicMax (within the launch they only grow)
-    const float old_sb = DQRM_FLAT_PRELOAD && nrows > BLK ? a.sblkmax[sbb + (blk >> 8)] : 0.0f;
+    const float old_sb = DQRM_FLAT_PRELOAD ? a.sblkmax[sbb + (blk >> 8)] : 0.0f;
     const float old_tm = DQRM_FLAT_PRELOAD ? a.tmax[t] : 0.0f;
     float4 w;
     w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
@@ -1760,27 +1770,28 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
     const float old_rm = group_max<LPR>(abs_max4(w0));
     const float rm = group_max<LPR>(abs_max4(w));
     if (sub == 0) {
+        // every table, narrow ones (<= 256 rows: one block, one superblock) included: growth by
+        // atomicMax, a shrunk block-max holder re-reduced by its owner or flagged
         st_w(a.rowmax + grow, rm, a.wt);
-        if (nrows > BLK) {
-            const int64_t sb = sbb + (blk >> 8);
-            if (rm > old_blk) {
-                atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
-                if (rm > (DQRM_FLAT_PRELOAD ? old_sb : a.sblkmax[sb])) {
-                    atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
-                    if (rm > (DQRM_FLAT_PRELOAD ? old_tm : a.tmax[t]))
-                        atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
-                }
+        const int64_t sb = sbb + (blk >> 8);
+        if (rm > old_blk) {
+            atomicMax(reinterpret_cast<unsigned int*>(a.blkmax) + bb + blk, __float_as_uint(rm));
+            if (rm > (DQRM_FLAT_PRELOAD ? old_sb : a.sblkmax[sb])) {
+                atomicMax(reinterpret_cast<unsigned int*>(a.sblkmax) + sb, __float_as_uint(rm));
+                if (rm > (DQRM_FLAT_PRELOAD ? old_tm : a.tmax[t]))
+                    atomicMax(reinterpret_cast<unsigned int*>(a.tmax) + t, __float_as_uint(rm));
             }
-            if (old_rm == old_blk && rm < old_rm) {
-                int p = OWN_QCAP;
-                if (owned && oq) {  // the workgroup holds every touched row of this block: it re-reduces it
-                    p = atomicAdd(oq->cnt, 1);
-                    if (p < OWN_QCAP) { oq->blk[p] = (uint32_t)blk; oq->old[p] = old_blk; }
-                }
-                if (p >= OWN_QCAP) {  // the finalize launch re-reduces the block
-                    flag_set(a.bdirty, bb + blk);
-                    flag_set(a.sdirty, sb);
-                }
+        }
+        if (old_rm == old_blk && rm < old_rm) {
+            int p = OWN_QCAP;
+            if (owned && oq) {  // the workgroup holds every touched row of this block: it re-reduces it
+                p = atomicAdd(oq->cnt, 1);
+                if (p < OWN_QCAP) { oq->blk[p] = (uint32_t)blk; oq->old[p] = old_blk; }
+            }
+            if (p >= OWN_QCAP) {  // the finalize re-reduces the block
+                flag_set(a.bdirty, bb + blk);
+                flag_set(a.sdirty, sb);
+                mark_table_flagged(a.sync, t);
             }
         }
     }
@@ -1883,7 +1894,10 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_local(ApplyArgs a, const int
                 if (lane == 0) {
                     a.blkmax[bb + blk] = mv;
                     const int64_t sb = sbb + (blk >> 8);
-                    if (mv < s_oq_old[q] && s_oq_old[q] == a.sblkmax[sb]) flag_set(a.sdirty, sb);  // held the superblock max
+                    if (mv < s_oq_old[q] && s_oq_old[q] == a.sblkmax[sb]) {  // held the superblock max
+                        flag_set(a.sdirty, sb);
+                        mark_table_flagged(a.sync, t);
+                    }
                 }
             }
         }
@@ -3471,11 +3485,18 @@ int check_set(const dqrm_table_set* s) {
 }
 
 // tracked: the preceding kernel raised tmax for every grown row (the flat apply kernels)
-int launch_finalize(const dqrm_table_set* set, hipStream_t st, bool tracked = false) {
+// flagged: after the flat apply kernels (k_apply_flat / k_apply_local), which mark the tables
+// they flagged (FLAG_WORD) and keep narrow tables' maxima themselves
+int launch_finalize(const dqrm_table_set* set, hipStream_t st, bool tracked = false, bool flagged = false) {
     static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
+    static const bool no_skip = [] {  // DQRM_FIN_FLAGGED=0: finalize every table (A/B)
+        const char* e = getenv("DQRM_FIN_FLAGGED");
+        return e && !strcmp(e, "0");
+    }();
+    if (no_skip) flagged = false;
     hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
                        set->blkmax, set->sblkmax, set->sdirty, set->bdirty, set->tmax, set->meta, set->num_tables,
-                       set->dim, tracked ? 1 : 0);
+                       set->dim, tracked ? 1 : 0, set->sync, flagged ? 1 : 0);
     LAUNCH_CHECK();
     return DQRM_OK;
 }
@@ -4307,7 +4328,7 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
         });
     }
     LAUNCH_CHECK();  // both kernels finalize the |W| hierarchy inside the launch
-    if (a.fin_launch) return launch_finalize(set, st, flat);
+    if (a.fin_launch) return launch_finalize(set, st, flat, flat);
     return DQRM_OK;
 }
 
@@ -4355,7 +4376,7 @@ int dqrm_apply_local(const dqrm_table_set* set, const int64_t* ws_cap_base, int6
                                a, ws_cap_base, ws_rows, ws_vals, ws_ucount, ws_absmax, s_avg);
     });
     LAUNCH_CHECK();  // the table's last working workgroup finalizes its |W| hierarchy
-    if (a.fin_launch) return launch_finalize(set, st, true);
+    if (a.fin_launch) return launch_finalize(set, st, true, true);
     return DQRM_OK;
 }
 

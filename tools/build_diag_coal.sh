@@ -6,5 +6,5 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/tools/diag_build
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DDQRM_DIAG_CLOCK $* -I $R/include"
 /opt/rocm/bin/hipcc $F -c $R/deep_quantized_recommendation_model_dqrm_amd/csrc/dqrm_coalesce.hip -o $O/dqrm_coalesce.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/dqrm_kernels.o $O/dqrm_coalesce.o $O/dqrm_dense.o $O/dqrm_input.o $O/dqrm_sync.o -o $O/libdqrm_clock.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $O/*.o -o $O/libdqrm_clock.so
 echo built $O/libdqrm_clock.so
