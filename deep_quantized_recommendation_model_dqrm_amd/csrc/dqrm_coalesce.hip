@@ -77,6 +77,12 @@ constexpr int FIX_MAX = 64;       // largest bucket the MSD pass finishes by ran
 #define DQRM_COAL_CSPAN 4096
 #endif
 constexpr int CSPAN = DQRM_COAL_CSPAN;  // largest row span sorted by counting rows (0: never)
+#ifndef DQRM_COAL_UNIQ
+#define DQRM_COAL_UNIQ 1  // 0: an A/B build without the one-launch step's distinct-rows fast path
+#endif
+constexpr int UNIQ_MAXN = TPB;      // fast path: at most one lookup per thread
+constexpr int UNIQ_HLOG = 12;       // its LDS hash: 4096 slots
+constexpr int UNIQ_HASH = 1 << UNIQ_HLOG;
 constexpr int RPT = CSPAN > 0 ? (CSPAN + TPB - 1) / TPB : 1;  // rows per thread in the row scan
 constexpr int LDS_BYTES = 156 * 1024;
 // dynamic LDS: keys u64[MAXB] | while sorting: ping-pong u64[MAXB] + digit counters
@@ -775,6 +781,43 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     int U, NS, M;
     bool counted = false;
     int ta = 0, tm = 0;
+    // 3u. one-launch step: a wide row-split slot whose rows are all distinct (a big table's
+    //     slot, nearly always) needs no sort -- every lookup is its own segment, in compaction
+    //     (= lookup) order, and the update keeps no order. Distinctness from one LDS hash insert
+    //     per lookup. (The N > 1 coalesce keeps the sort: its payload rows must be ascending.)
+    bool uniq = false;
+    if (APPLY && DQRM_COAL_UNIQ && !dsplit && !ranked && !atomic_mode && n <= UNIQ_MAXN) {
+        uint32_t* hk = reinterpret_cast<uint32_t*>(stage);  // the stage is not used before the land phase
+        for (int q = tid; q < UNIQ_HASH; q += TPB) hk[q] = 0u;
+        if (tid == 0) s_crowd = 0;
+        __syncthreads();
+        if (tid < n) {
+            const uint32_t key = krow(keys[tid]) + 1u;
+            uint32_t h = (key * 2654435761u) >> (32 - UNIQ_HLOG);
+            for (;;) {  // linear probing, load <= 1/4
+                const uint32_t old = atomicCAS(&hk[h], 0u, key);
+                if (old == 0u) break;
+                if (old == key) {
+                    s_crowd = 1;  // a repeated row: the sorting path
+                    break;
+                }
+                h = (h + 1u) & (UNIQ_HASH - 1);
+            }
+        }
+        __syncthreads();
+        uniq = s_crowd == 0;
+        if (uniq) {
+            for (int p = tid; p < n; p += TPB) {
+                pos[kgat(keys[p])] = (uint16_t)p;
+                hpos[p] = (uint16_t)p;
+                sdest[p] = (int)((j ? cb_e - n : cb_s) + p);
+            }
+            if (tid == 0) hpos[n] = (uint16_t)n;
+            U = n;
+            M = 0;
+            NS = n;
+        }
+    }
     if (ranked) {
         // 3a'. wave w ranks keys [w*64*kpl, (w+1)*64*kpl) in order: same-row lanes by
         //      bit-slice ballots, earlier keys of the wave by its row counters
@@ -931,7 +974,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         for (int i = 0; i < MAXI; ++i)
             if (tid + TPB * i < B && !(r[i] >= 0 && r[i] < nrows)) pos[tid + TPB * i] = 0xFFFF;
     }
-    if (counted) __syncthreads();
+    if (counted || uniq) __syncthreads();
     else {
     // 3. sort by row
     {

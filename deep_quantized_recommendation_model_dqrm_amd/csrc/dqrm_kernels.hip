@@ -1940,8 +1940,27 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
     int* pos = s_pos[grp];
     const int32_t* rows_r = reinterpret_cast<const int32_t*>(pr + pl.rows_off) + cb;
+    // one rank (N == 1, finalize launch after): a block whose entries all fall in this
+    // workgroup's chunk is OWNED here (the table's rows are ascending, so another entry of the
+    // block would be a neighbour of the chunk): a shrunk holder of it is re-reduced below, as
+    // k_apply_local does, instead of flagging the table for the finalize launch
+    const bool own_mode = !FIN && N == 1;
+    __shared__ int s_oq_n;
+    __shared__ uint32_t s_oq_blk[OWN_QCAP];
+    __shared__ float s_oq_old[OWN_QCAP];
+    OwnQueue oq;  // (filled at run time: a constant aggregate of LDS addresses cannot be a static initializer)
+    oq.cnt = &s_oq_n;
+    oq.blk = s_oq_blk;
+    oq.old = s_oq_old;
+    if (own_mode) {
+        if (threadIdx.x == 0) s_oq_n = 0;
+        __syncthreads();
+    }
     for (int e = blockIdx.x * G + grp; e < cnt_r; e += gridDim.x * G) {
         const int32_t x = rows_r[e];
+        const int c0 = e - grp;  // the chunk's first entry
+        const int32_t xlo = (own_mode && c0 > 0) ? rows_r[c0 - 1] : -1;
+        const int32_t xhi = (own_mode && c0 + G < cnt_r) ? rows_r[c0 + G] : -1;
         if (x < 0 || x >= nrows) {  // cannot happen for payloads this library packed
             if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
             continue;
@@ -1969,7 +1988,35 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
                 if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
             }
         }
-        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub);
+        const bool owned = own_mode && (xlo < 0 || (xlo >> 8) != (x >> 8)) && (xhi < 0 || (xhi >> 8) != (x >> 8));
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub, owned, own_mode ? &oq : nullptr);
+    }
+    if (own_mode) {  // owned blocks whose max holder shrank: re-reduce their 256 row maxima
+        __syncthreads();
+        const int nq = s_oq_n < OWN_QCAP ? s_oq_n : OWN_QCAP;
+        if (nq > 0) {  // uniform
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's row maxima have landed
+            __syncthreads();
+            const int lane = threadIdx.x % WAVE;
+            for (int q = threadIdx.x / WAVE; q < nq; q += FLAT_TPB / WAVE) {
+                const int64_t blk = s_oq_blk[q];
+                float mv = 0.0f;
+#pragma unroll
+                for (int i = 0; i < BLK / WAVE; ++i) {
+                    const int64_t rr = blk * BLK + lane + i * WAVE;
+                    if (rr < nrows) mv = fmaxf(mv, ld_wt(a.rowmax + rb + rr));  // sc1: past any stale L1 line
+                }
+                mv = wave_max(mv);
+                if (lane == 0) {
+                    a.blkmax[bb + blk] = mv;
+                    const int64_t sb = sbb + (blk >> 8);
+                    if (mv < s_oq_old[q] && s_oq_old[q] == a.sblkmax[sb]) {  // held the superblock max
+                        flag_set(a.sdirty, sb);
+                        mark_table_flagged(a.sync, t);
+                    }
+                }
+            }
+        }
     }
     if constexpr (FIN) {
         if (arrive_last(a.sync + (int64_t)t * DQRM_SYNC_STRIDE, expected))
