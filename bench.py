@@ -136,7 +136,8 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
 
 def pmc_traffic(path, phase, D, workload=None):
     """HBM bytes per launch of the phase's kernel from a committed rocprofv3 PMC summary
-    (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None. The summary must
+    (reads by L2 request size + WRITE_SIZE when the summary has the request-size pass, else
+    2 x FETCH_SIZE + WRITE_SIZE; tools/prof_summary.py), or None. The summary must
     have been profiled on the same workload (tools/prof_summary.py records the profiled bench
     line's config, batch per GPU, mode and N=1 update form): a summary of another batch
     size or mode is refused, not rescaled."""
@@ -150,7 +151,8 @@ def pmc_traffic(path, phase, D, workload=None):
     kernels = summ["kernels"]
     for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
         if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
-            return {"bytes": round(v["hbm_bytes_per_launch"]), "profiled_avg_us": round(v["avg_us"], 2),
+            return {"bytes": round(v["hbm_bytes_per_launch"]), "correction": summ.get("correction"),
+                    "profiled_avg_us": round(v["avg_us"], 2),
                     "profiled_median_us": round(v["median_us"], 2) if v.get("median_us") else None,
                     "source": os.path.relpath(path, ROOT)}
     return None

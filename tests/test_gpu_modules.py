@@ -92,9 +92,9 @@ def test_quant_embedding_bag_two_forward_and_sparse_grad(dq, per_lookup_grads):
 def test_sparse_grad_sgd_step_matches_kaggle_pool1(dq, golden_dir):
     """The single-GPU driver unchanged (dlrm_s_pytorch_single_gpu.py:1943-1950): 26
     QuantEmbeddingBagTwo(grad_mode="sparse") + torch.optim.SGD(lr=0.1).step() on their
-    uncoalesced grads, against kaggle_pool1.npz (the reference's modules + SGD in torch-CPU).
-    The first forward is bit-exact. W: ATen-ROCm's sparse add (index_add_ of alpha * value)
-    and torch-CPU's per-lookup add round differently, so W (|W| <= 0.58 here) and the
+    default (presummed, deterministic) COO grads, against kaggle_pool1.npz (the reference's
+    modules + SGD in torch-CPU). The first forward is bit-exact. W: ATen-ROCm's sparse add
+    of the row sums and torch-CPU's per-lookup add round differently, so W (|W| <= 0.58 here) and the
     later forwards, whose table scale follows max|W|, are held to 1e-6 absolute (most
     elements agree to the bit). The |W| maxima follow ATen's writes (dqrm_rows_changed)."""
     import os

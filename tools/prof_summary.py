@@ -5,9 +5,14 @@
   <tag>_summary.json       per libdqrm kernel: calls, average and MEDIAN duration (us, the
                            median from the per-dispatch kernel trace, so a rare outlier
                            does not move roofline fractions), and the
-                           per-launch HBM traffic from the separate --pmc passes:
-                           FETCH_SIZE x 2 (gfx950 reports half the bytes of wide coalesced
-                           reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, in bytes.
+                           per-launch HBM traffic from the separate --pmc passes. Reads:
+                           from the L2's memory-side read requests by size when the
+                           request-size pass exists (128 x TCC_EA0_RDREQ_128B + 64 x _64B +
+                           32 x _32B: exact for every access shape, profiles/r5_tcc_*),
+                           else FETCH_SIZE x 2 (gfx950 tallies a 128-B request at 64 B,
+                           MI355X_MICROARCH.md "HBM"; that doubles 64-B requests too).
+                           Writes: WRITE_SIZE (64 B per 64-B request, 32 B per 32-B one:
+                           exact). In bytes.
 bench.py reads <tag>_summary.json (if present) to fill roofline.traffic.
 
 usage: python tools/prof_summary.py gpurun_out/prof_tb profiles/r1_tb
@@ -52,12 +57,25 @@ def main(src: str, tag: str) -> None:
             if r["Counter_Name"] == cname:
                 acc[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)  # KB -> B
         counters[cname] = {k: sum(v) / len(v) for k, v in acc.items()}
+    # read requests by size (optional pass): bytes = 128 * _128B + 64 * _64B + 32 * _32B
+    rd_exact = {}
+    try:
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(f"{src}_rdreq/tb_counter_collection.csv")):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in acc.items():
+            mean = {c: sum(x) / len(x) for c, x in d.items()}
+            rd_exact[k] = sum(mean.get(f"TCC_EA0_RDREQ_{n}B_sum", 0.0) * n for n in (32, 64, 128))
+    except OSError:
+        pass
     for k, v in out.items():
         fe = counters["FETCH_SIZE"].get(k)
         wr = counters["WRITE_SIZE"].get(k)
         v["fetch_size_bytes"] = fe
         v["write_size_bytes"] = wr
-        v["hbm_bytes_per_launch"] = (2.0 * fe + wr) if fe is not None and wr is not None else None
+        v["read_bytes_by_request_size"] = rd_exact.get(k)
+        rd = rd_exact.get(k, 2.0 * fe if fe is not None else None)
+        v["hbm_bytes_per_launch"] = (rd + wr) if rd is not None and wr is not None else None
     # the profiled bench line's workload: bench.pmc_traffic only uses a summary of the same one
     workload = None
     try:
@@ -67,7 +85,9 @@ def main(src: str, tag: str) -> None:
             workload = roof.get("workload_profiled")
     except (OSError, ValueError):
         pass
-    json.dump({"source": src, "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)",
+    corr = ("hbm = reads by request size (128*RDREQ_128B + 64*RDREQ_64B + 32*RDREQ_32B) + WRITE_SIZE"
+            if rd_exact else "hbm = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halving)")
+    json.dump({"source": src, "correction": corr,
                "workload": workload, "kernels": out}, open(f"{tag}_summary.json", "w"), indent=1)
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1]["calls"]):
         hb = v["hbm_bytes_per_launch"]
