@@ -109,6 +109,9 @@ def parse(argv=None):
                    help="run the N>1 exchange (two all-gathers, quantize-pack, payload apply; the MLP "
                         "exchange's collectives) through the process group at world size 1 too: the RCCL leg "
                         "on a one-GPU box")
+    p.add_argument("--separate-forward", action="store_true",
+                   help="N=1 one-launch step: the forward as its own launch (dqrm_emb_fwd) instead of inside "
+                        "the previous step's update launch (dqrm_emb_bwd_apply_fwd_local)")
     p.add_argument("--two-launch-local", action="store_true",
                    help="N=1: coalesce + dqrm_apply_local as two launches (not dqrm_emb_bwd_apply_local)")
     p.add_argument("--sample-every", type=int, default=0,
@@ -127,6 +130,8 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     # Criteo form (<APPLY, row-major stage>; round-3 summaries: <APPLY>) / general
     "bwd_coalesce": ("k_coalesce_p1<false,", "k_coalesce_p1<false>", "k_coalesce_p1", "k_bwd_fused<{lpr}, 1>"),
     "bwd_apply_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),  # N=1: coalesce + update in one launch
+    # N=1 at the step boundary: the same kernel, with the next batch's forward inside
+    "bwd_apply_fwd_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),
     "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
     "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_ranges<{lpr}>"),
@@ -184,6 +189,9 @@ def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
         "bwd_sgd": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
         # N=1 backward + update in one launch: as bwd_sgd (the coalesced rows never need HBM)
         "bwd_apply_local": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
+        # ... and the next batch's forward in the same launch: + emb_fwd's bytes
+        "bwd_apply_fwd_local": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk
+                               + L * (D * 4 + 8) + offs + L * D * 4 + T * 4,
         "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
         "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4 + pk,
         "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4 + pk,
@@ -203,12 +211,14 @@ def timed_events(n):
     return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
 
 
-def phase_names(mode, use_packed, fused, one_launch=False):
+def phase_names(mode, use_packed, fused, one_launch=False, next_fwd=False):
     fwd = "emb_fwd_packed" if use_packed else "emb_fwd"
     if mode == "fwd":
         return [fwd]
     if mode == "sgd":
         return [fwd, "bwd_sgd"]
+    if fused and one_launch and next_fwd:
+        return ["bwd_apply_fwd_local"]
     if fused and one_launch:
         return [fwd, "bwd_apply_local"]
     return [fwd, "bwd_coalesce"] + (["apply_local"] if fused else ["grad_quant_pack", "apply_sparse_update"])
@@ -279,7 +289,12 @@ def main():
     # whose grid the device can hold at once (the library decides; asked here for the line)
     one_launch = fused and not a.two_launch_local and ts.apply_local_is_one_launch(batches[0])
     repack = a.use_packed
-    names = phase_names(a.mode, a.use_packed, fused, one_launch)
+    # ... and at the step boundary the NEXT batch's forward inside that launch (the update of
+    # step i and apply_emb of step i+1 are adjacent in the training loop; dqrm_emb_bwd_apply_fwd_local):
+    # each timed step still runs one forward and one backward + update
+    next_fwd = (one_launch and a.mode == "dp" and not a.use_packed and not a.separate_forward
+                and len(batches) > 1 and ts.apply_fwd_local_is_one_launch(batches[0], batches[1]))
+    names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd)
 
     # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
     # (dqrm_exchange_grad: coalesce + both all-gathers + quantize-pack; dqrm_exchange_apply);
@@ -298,6 +313,14 @@ def main():
             if ev is not None and (only is None or only == j):
                 ev[j][k].record()
 
+        if next_fwd:  # this batch's forward ran in the previous step's launch; this one runs the next's
+            nxt = batches[(i + 1) % len(batches)]
+            mark(0, 0)
+            ts.backward_apply_forward_local(b, dy, ex.ws, a.grad_bits, ex.s_avg, a.lr, nxt, bits=4,
+                                            refresh_scale=a.scale_period <= 0 or (i + 1) % a.scale_period == 0,
+                                            out=y)
+            mark(0, 1)
+            return
         mark(0, 0)
         if a.use_packed:
             if refresh:  # periodic refresh: new scales, tables whose scale moved are repacked
@@ -347,6 +370,8 @@ def main():
                    L.DQRM_UPD_DP, repack)
         mark(3, 1)
 
+    if next_fwd:  # the first batch's forward (every later one runs inside the previous step's launch)
+        ts.forward(batches[0], bits=4, out=y)
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -471,6 +496,7 @@ def main():
         replicas_match = True
     n1_update = (None if a.mode != "dp" or world > 1 else
                  "coalesce + quant-pack + payload apply (RCCL at world size 1)" if coll else
+                 "one launch: update of step i + forward of step i+1 (dqrm_emb_bwd_apply_fwd_local)" if next_fwd else
                  "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
                  "coalesce + dqrm_apply_local" if fused else "coalesce + quant-pack + payload apply")
     workload = {"config": a.config, "mode": a.mode, "batch_per_gpu": B, "n1_update": n1_update,
@@ -539,7 +565,9 @@ def main():
                               "phases": names},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events; " + (
-                "bwd_apply_local is ONE launch (coalesce, quantize, update and the |W| hierarchy)" if one_launch
+                "bwd_apply_fwd_local is ONE launch per step: coalesce, quantize, update and the |W| hierarchy of "
+                "this step's batch, then the next batch's fake-quant forward, table by table" if next_fwd
+                else "bwd_apply_local is ONE launch (coalesce, quantize, update and the |W| hierarchy)" if one_launch
                 else "apply_local = the fused quantize + update kernel + a short k_table_finalize launch" if fused
                 else "sgd = one launch (|W| hierarchy inside)" if a.mode == "sgd"
                 else "apply_sparse_update = " + L.apply_update_form() if a.mode == "dp" else "forward only"),

@@ -52,7 +52,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 8  # include/dqrm.h
+DQRM_ABI_VERSION = 9  # include/dqrm.h
 DQRM_PRESUM_MAX_LOOKUPS = 2048
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
@@ -78,6 +78,8 @@ EXPORTED_SYMBOLS = (
     "dqrm_apply_local",
     "dqrm_emb_bwd_apply_local",
     "dqrm_bwd_apply_local_is_one_launch",
+    "dqrm_emb_bwd_apply_fwd_local",
+    "dqrm_bwd_apply_fwd_local_is_one_launch",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
     "dqrm_dense_grad_quant",
@@ -270,6 +272,12 @@ def load(path: str | None = None) -> C.CDLL:
              C.c_size_t, P],
         ),
         "dqrm_bwd_apply_local_is_one_launch": (C.c_int, [TS, BA, P]),
+        "dqrm_emb_bwd_apply_fwd_local": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P,
+             C.c_size_t, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P],
+        ),
+        "dqrm_bwd_apply_fwd_local_is_one_launch": (C.c_int, [TS, BA, BA, C.c_uint32, P]),
         "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
         "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),
         "dqrm_dense_grad_quant": (C.c_int, [DS, C.c_int, P, C.c_int, P, C.c_int, P, P]),

@@ -433,6 +433,16 @@ __device__ __forceinline__ float chain_sum_rm(const float* c, int p, int pe, int
 #ifndef DQRM_COAL_ROWMAJOR
 #define DQRM_COAL_ROWMAJOR 1
 #endif
+// A dimension-split table's workgroup stages its slice (SW = D/8 floats per position) for a
+// few rows with hundreds of lookups each: its cost is the ordered chains, which read 16 B at a
+// time from a dimension-major stage (4 positions per LDS read) but 4 B from a row-major one.
+// DQRM_COAL_DSDM 1: such workgroups take the dimension-major stage under RM too -- in the
+// N > 1 coalesce (APPLY false; TB forced-collectives step 60.4 -> 56.5 us, A/B r5j). In the
+// one-launch step the runtime layout choice cost every table ~1.5 us (38.4 -> 40.7 us/step),
+// so that kernel keeps the compile-time layout.
+#ifndef DQRM_COAL_DSDM
+#define DQRM_COAL_DSDM 1
+#endif
 
 #ifndef DQRM_COAL_WPF
 #define DQRM_COAL_WPF 4
@@ -476,6 +486,10 @@ static_assert(MAXB < (1 << 13), "distinct-row count field of a granule");
 
 
 constexpr int STALL_WORD = 3;  // a table's sync word: bit (s + 8 j) = workgroup (slot s, sub-slot j) stalled
+// fused next-batch forward: sync words 4-5 hold the table's final |W| max as a granule
+// {max bits, launch epoch}, stored by the table's last arriver after its finalize
+constexpr int FWD_WORD = 4;
+static_assert(FWD_WORD % 2 == 0 && FWD_WORD + 2 <= GRAN_WORD, "8-B word below the slot granules");
 
 // The table's last-arriving workgroup, when some of the table's workgroups gave up waiting at
 // the rendezvous (stall_mask): every workgroup published its granule before it arrived, so the
@@ -528,8 +542,8 @@ __device__ __forceinline__ void recover_stalled(const dqrm_internal::CoalesceArg
             acc.x = fake_quant(v.x, rr, qlo, qhi) + 0.0f; acc.y = fake_quant(v.y, rr, qlo, qhi) + 0.0f;
             acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
             wn.x = upd(w0.x, acc.x); wn.y = upd(w0.y, acc.y); wn.z = upd(w0.z, acc.z); wn.w = upd(w0.w, acc.w);
-            if (ok) {
-                reinterpret_cast<float4*>(la.W + grow * D)[sub] = wn;
+            if (ok) {  // write-through: a fused forward may read the row from another CU
+                st4_wt(reinterpret_cast<float4*>(la.W + grow * D) + sub, wn);
                 if (la.repack) pack4_row(wn, la.packed + grow * (D / 2), sub, r_pack);
             }
             float old_rm = abs_max4(w0), rm = abs_max4(wn);
@@ -600,6 +614,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_dirty;
     __shared__ int s_fin;
     __shared__ int s_stallmask;
+    __shared__ int s_lastarr;
+    __shared__ float s_ftm;
+    __shared__ int s_fok;
     __shared__ uint32_t s_oq_blk[OWN_Q];
     __shared__ float s_oq_old[OWN_Q];
     __shared__ float s_oq_sold[OWN_Q];
@@ -672,7 +689,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     const bool active = dsplit ? s < DS : r0 < r1;
     const int SP = (STAGE_FLOATS / SW) & ~3;  // stage entries (dimension-major: the column pitch, 16-B columns)
     const int CE = SP - 4;                    // stage entries per chunk
-    constexpr bool rmaj = RM;
+    const bool rmaj = RM && !(DQRM_COAL_DSDM && !APPLY && dsplit);
     // stage index of (entry p, dimension d)
     auto sx = [&](int p, int d) -> int { return rmaj ? p * SW + d : d * SP + p; };
     const float* dyt = a.dy + (int64_t)t * a.dst_t;
@@ -1401,6 +1418,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
         const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
         bool dirty = false;
+        const bool wt_rows = dsplit && la.fwd_idx != nullptr;
         // a workgroup that updates ONE row-range slot keeps its rows' new maxima in LDS (the
         // stage, free by now): a shrunk block is then re-reduced from the other rows' stored
         // maxima (untouched this launch) and these, with no wait for its own stores
@@ -1421,7 +1439,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
             float4 wn;
             wn.x = upd(w0.x, acc.x); wn.y = upd(w0.y, acc.y); wn.z = upd(w0.z, acc.z); wn.w = upd(w0.w, acc.w);
-            reinterpret_cast<float4*>(la.W + grow * a.D)[sub] = wn;
+            // (a dimension-split table's rows are read by its other workgroups in the fused
+            // forward: stored write-through then, as every hand-off)
+            st4_w(reinterpret_cast<float4*>(la.W + grow * a.D) + sub, wn, wt_rows);
             if (la.repack) pack4_row(wn, la.packed + grow * (a.D / 2), sub, r_pack);
             float old_rm = abs_max4(w0), rm = abs_max4(wn);
             for (int o = 1; o < LPR; o <<= 1) {
@@ -1620,9 +1640,18 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                                            __HIP_MEMORY_SCOPE_AGENT);
             }
             s_stallmask = (int)sm;
+            s_lastarr = last ? 1 : 0;
             s_fin = last && ((now >> 16) != 0u || sm != 0u);
         }
         __syncthreads();
+        // the next batch's indices (fused forward): in flight across the recovery / finalize
+        // and the wait for the table's final max
+        int64_t nx[MAXI];
+#pragma unroll
+        for (int i = 0; i < MAXI; ++i) {
+            const int b = tid + TPB * i;
+            nx[i] = (la.fwd_idx != nullptr && b < B) ? la.fwd_idx[(int64_t)t * B + b] : -1;
+        }
         if (s_stallmask) {  // uniform, rare: apply the stalled workgroups' rows (then finalize)
             recover_stalled(a, la, t, (uint32_t)s_stallmask, gran, NG, K, dsplit, NA, nblk, s_cb);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1632,6 +1661,122 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
                                  la.bdirty, la.tmax, a.D, true, false);
         CDIAG_W(13);
+        // 9. the NEXT batch's forward (dqrm_emb_bwd_apply_fwd_local): emb_fwd_table's
+        //    arithmetic for pooling 1, y[b] = fake-quant(W[row_b]) with the scale of the updated
+        //    table. The table's last arriver publishes its final max (FWD_WORD granule, after
+        //    the finalize); the others wait for it. Who reads which row: a row split reads only
+        //    the rows of its own range -- updated by itself (or untouched) -- so its own stores
+        //    are what it reads; a dimension-split table (one XCD, no sub-slots) splits the
+        //    lookups evenly and reads its rows with sc1 loads past the L1, from the XCD's L2
+        //    the writers stored into before they arrived. Out-of-range rows: workgroup (0, 0)
+        //    writes zeros and flags them. A stalled workgroup's share (its rows were applied by
+        //    the last arriver) is the last arriver's.
+        if (la.fwd_idx != nullptr) {  // uniform
+            const bool refresh = (la.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
+            const bool fullp = (la.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
+            uint64_t* fword = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
+            if (s_lastarr) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    const float tm = ld_wt(la.tmax + t);
+                    s_ftm = tm;
+                    s_fok = 1;
+                    __hip_atomic_store(fword, gr_make(tm, 0, epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (tid == 0) {
+                // a workgroup that stalled at the rendezvous leaves its share to the last arriver
+                // and does not wait (its CU may be what a late workgroup of the table needs);
+                // the others met every workgroup of the table there, so all of them arrive
+                uint64_t g = 0;
+                int ok = go ? 1 : 0;
+                for (uint32_t spin = 0; ok; ++spin) {
+                    g = __hip_atomic_load(fword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (gr_epoch(g) == epoch) break;
+                    if (spin > (1u << 20)) {  // (never, all resident) flagged, this share skipped
+                        flag_error(a.err, DQRM_ERRF_STALL);
+                        ok = 0;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                s_ftm = __uint_as_float((uint32_t)g);
+                s_fok = ok;
+            }
+            __syncthreads();
+            const float sf = fullp ? 1.0f : (refresh ? sym_scale(s_ftm, la.fwd_bits) : la.fwd_scale[t]);
+            if (refresh && !fullp && s_lastarr && tid == 0) la.fwd_scale[t] = sf;
+            const float rf = 1.0f / sf;
+            const float fqlo = -(float)(1 << (la.fwd_bits - 1)), fqhi = (float)((1 << (la.fwd_bits - 1)) - 1);
+            // this workgroup's lookups, per wave as an LDS list {row | 0xFFFFFFFF, b} in lookup
+            // order (the keys region is dead by now)
+            const int me = s + SPLIT * j;
+            const uint32_t smask = s_lastarr ? (uint32_t)s_stallmask : 0u;
+            const int per = (B + NA - 1) / NA;
+            const int lane = tid % WAVE;
+            uint64_t* lst = keys + w * (WAVE * MAXI);
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i) {
+                const int b = tid + TPB * i;
+                const int64_t x = nx[i];
+                const bool okr = x >= 0 && x < nrows;
+                int own = 0;
+                if (dsplit) {
+                    own = b / per;
+                } else if (okr) {
+                    const int sl = slot_of_row(x, nblk);
+                    int jj = 0;
+                    if (K == 2) {
+                        const int64_t b0 = nblk * sl / SPLIT, b1 = nblk * (sl + 1) / SPLIT;
+                        jj = (x >> 8) >= (b0 + b1) / 2 ? 1 : 0;
+                    }
+                    own = sl + SPLIT * jj;
+                }
+                const bool mine = s_fok && b < B && ((own == me && go) || ((smask >> own) & 1u));
+                const uint64_t m = __ballot(mine);
+                if (mine) {
+                    const int p = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    lst[p] = ((uint64_t)(okr ? (uint32_t)x : 0xFFFFFFFFu) << 32) | (uint32_t)b;
+                    if (!okr) flag_error(a.err, DQRM_ERRF_INDEX);
+                }
+                cnt += __popcll(m);
+            }
+            __syncthreads();
+            const int G = LPR < WAVE ? WAVE / LPR : 1;  // rows per wave pass
+            const int gl = lane / LPR, sub = lane % LPR;
+            float* outt = la.fwd_out + (int64_t)t * la.fwd_ost_t;
+            constexpr int FU = 4;  // rows per lane group in flight
+            for (int p0 = 0; p0 < cnt; p0 += G * FU) {  // uniform per wave
+                uint64_t e[FU];
+                float4 v[FU];
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const int ix = p0 + gl + G * u;
+                    e[u] = ix < cnt && lane < G * LPR ? lst[ix] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t x = (uint32_t)(e[u] >> 32);
+                    v[u] = nrows > 0 ? ld4_sc1(la.W + (rb + (x != 0xFFFFFFFFu ? x : 0u)) * a.D, (uint32_t)sub * 16u)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    if (e[u] == ~0ull) continue;
+                    float4 y = (uint32_t)(e[u] >> 32) != 0xFFFFFFFFu ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (!fullp) {
+                        y.x = fake_quant(y.x, rf, fqlo, fqhi) * sf;
+                        y.y = fake_quant(y.y, rf, fqlo, fqhi) * sf;
+                        y.z = fake_quant(y.z, rf, fqlo, fqhi) * sf;
+                        y.w = fake_quant(y.w, rf, fqlo, fqhi) * sf;
+                    }
+                    reinterpret_cast<float4*>(outt + (int64_t)(uint32_t)e[u] * la.fwd_ost_b)[sub] = y;
+                }
+            }
+            CDIAG_W(17);
+        }
     }
 }
 

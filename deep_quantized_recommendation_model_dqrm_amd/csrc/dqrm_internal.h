@@ -55,6 +55,15 @@ struct LocalApplyArgs {
     // rendezvous polls before a workgroup gives up (DQRM_ERRF_STALL; its rows are then applied
     // by the table's last-arriving workgroup); the host sets it (DQRM_STALL_SPIN, default 2^20)
     uint32_t spin_limit;
+    // the next batch's forward behind the update (dqrm_emb_bwd_apply_fwd_local; fwd_idx null:
+    // none): Criteo-form indices [T][B] (the same B), out[t*fwd_ost_t + b*fwd_ost_b + d],
+    // dqrm_emb_fwd's bits and flags (DQRM_FWD_REFRESH_SCALE / DQRM_FWD_FULL_PRECISION)
+    const int64_t* fwd_idx;
+    float* fwd_out;
+    int64_t fwd_ost_t, fwd_ost_b;
+    float* fwd_scale;           // [T] the forward scale: written (refresh) or read (held)
+    int fwd_bits;
+    uint32_t fwd_flags;
 };
 constexpr int kSubTables = 32;  // LocalApplyArgs::sub_table entries
 

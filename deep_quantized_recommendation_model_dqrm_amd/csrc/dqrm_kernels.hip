@@ -4440,6 +4440,17 @@ static bool apply_local_one_launch(const dqrm_table_set* set, const dqrm_batch* 
            dqrm_internal::coalesce_apply_resident(set->num_tables, (hipStream_t)stream);
 }
 
+// the next batch's forward runs inside the one-launch step when it is a Criteo-form batch of
+// the same size on the exact FP32 rows (the INT4 packed path stays a launch of its own)
+static bool fused_fwd_fits(const dqrm_batch* batch, const dqrm_batch* next, uint32_t flags) {
+    static const bool off = [] {
+        const char* e = getenv("DQRM_FUSED_FWD");
+        return e && !strcmp(e, "0");
+    }();
+    return !off && next && (next->flags & DQRM_BATCH_POOLING_ONE) && next->num_bags == batch->num_bags &&
+           next->max_lookups >= next->num_bags && !(flags & DQRM_FWD_USE_PACKED);
+}
+
 int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
@@ -4447,11 +4458,61 @@ int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_bat
     return apply_local_one_launch(set, batch, stream) ? 1 : 0;
 }
 
+// The next batch's forward fused behind the one-launch update (nullptr: none)
+struct FusedFwd {
+    const dqrm_batch* next;
+    int bits;
+    uint32_t flags;
+    float* out;
+    int64_t ost_t, ost_b;
+};
+
+static int bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy, int64_t dy_stride_t,
+                           int64_t dy_stride_b, int ste, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                           int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount, float* ws_absmax, int grad_bits,
+                           float* s_avg, float lr, int repack_bits, void* workspace, size_t workspace_bytes,
+                           const FusedFwd* ff, void* stream);
+
 int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
                              int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
                              int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
                              float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
                              void* workspace, size_t workspace_bytes, void* stream) {
+    return bwd_apply_local(set, batch, dy, dy_stride_t, dy_stride_b, ste, ws_cap_base, ws_cap_total, ws_rows, ws_vals,
+                           ws_ucount, ws_absmax, grad_bits, s_avg, lr, repack_bits, workspace, workspace_bytes, nullptr,
+                           stream);
+}
+
+int dqrm_emb_bwd_apply_fwd_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                                 int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
+                                 int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
+                                 float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                                 void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                                 uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                                 void* stream) {
+    FwdArgs fa;  // the forward's arguments, validated as dqrm_emb_fwd validates them
+    int rc = fwd_args(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, "dqrm_emb_bwd_apply_fwd_local", &fa);
+    if (rc) return rc;
+    const FusedFwd ff{next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b};
+    return bwd_apply_local(set, batch, dy, dy_stride_t, dy_stride_b, ste, ws_cap_base, ws_cap_total, ws_rows, ws_vals,
+                           ws_ucount, ws_absmax, grad_bits, s_avg, lr, repack_bits, workspace, workspace_bytes, &ff,
+                           stream);
+}
+
+int dqrm_bwd_apply_fwd_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch,
+                                           const dqrm_batch* next, uint32_t fwd_flags, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_bwd_apply_fwd_local_is_one_launch"))) return rc;
+    if ((rc = check_batch(next, "dqrm_bwd_apply_fwd_local_is_one_launch"))) return rc;
+    return apply_local_one_launch(set, batch, stream) && fused_fwd_fits(batch, next, fwd_flags) ? 1 : 0;
+}
+
+static int bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy, int64_t dy_stride_t,
+                           int64_t dy_stride_b, int ste, const int64_t* ws_cap_base, int64_t ws_cap_total,
+                           int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount, float* ws_absmax, int grad_bits,
+                           float* s_avg, float lr, int repack_bits, void* workspace, size_t workspace_bytes,
+                           const FusedFwd* ff, void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if ((rc = check_batch(batch, "dqrm_emb_bwd_apply_local"))) return rc;
@@ -4478,16 +4539,26 @@ int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch,
         la.pscale = set->pscale; la.sync = set->sync; la.s_avg = s_avg; la.bits = grad_bits; la.nlr = -lr;
         la.repack = repack_bits == 4;
         dqrm_internal::plan_sub_slots(set->num_rows_host, set->num_tables, &la);
+        const bool fused_fwd = ff && fused_fwd_fits(batch, ff->next, ff->flags);
+        if (fused_fwd) {
+            la.fwd_idx = ff->next->idx; la.fwd_out = ff->out; la.fwd_ost_t = ff->ost_t; la.fwd_ost_b = ff->ost_b;
+            la.fwd_scale = set->scale; la.fwd_bits = ff->bits; la.fwd_flags = ff->flags;
+        }
         const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, &la, (hipStream_t)stream);
         if (e != hipSuccess)
             return set_error(DQRM_E_HIP, "dqrm_emb_bwd_apply_local: launch failed: %s (%d)", hipGetErrorString(e), (int)e);
+        if (ff && !fused_fwd)
+            return dqrm_emb_fwd(set, ff->next, ff->bits, ff->flags, ff->out, ff->ost_t, ff->ost_b, stream);
         return DQRM_OK;
     }
     if ((rc = dqrm_emb_bwd_coalesce(set, batch, dy, dy_stride_t, dy_stride_b, ste, ws_cap_base, ws_rows, ws_vals,
                                     ws_ucount, ws_absmax, workspace, workspace_bytes, stream)))
         return rc;
-    return dqrm_apply_local(set, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, ws_absmax, grad_bits, s_avg,
-                            lr, repack_bits, stream);
+    if ((rc = dqrm_apply_local(set, ws_cap_base, ws_cap_total, ws_rows, ws_vals, ws_ucount, ws_absmax, grad_bits,
+                               s_avg, lr, repack_bits, stream)))
+        return rc;
+    if (ff) return dqrm_emb_fwd(set, ff->next, ff->bits, ff->flags, ff->out, ff->ost_t, ff->ost_b, stream);
+    return DQRM_OK;
 }
 
 int dqrm_read_errors(const dqrm_table_set* set, uint32_t* flags, int clear, void* stream) {

@@ -569,6 +569,52 @@ class EmbeddingTableSet:
             "dqrm_emb_bwd_apply_local",
         )
 
+    def _fwd_flags(self, refresh_scale: bool, use_packed: bool, full_precision: bool) -> int:
+        flags = L.DQRM_FWD_REFRESH_SCALE if refresh_scale else 0
+        if use_packed:
+            flags |= L.DQRM_FWD_USE_PACKED
+        if full_precision:
+            flags |= L.DQRM_FWD_FULL_PRECISION
+        return flags
+
+    def apply_fwd_local_is_one_launch(self, batch: LookupBatch, next_batch: LookupBatch,
+                                      use_packed: bool = False) -> bool:
+        """Whether backward_apply_forward_local runs the update AND the next batch's forward
+        as ONE launch (dqrm_bwd_apply_fwd_local_is_one_launch)."""
+        rc = self.lib.dqrm_bwd_apply_fwd_local_is_one_launch(
+            C.byref(self._c), C.byref(batch.c), C.byref(next_batch.c),
+            self._fwd_flags(True, use_packed, False), _stream_handle())
+        if rc < 0:
+            L.check(rc, "dqrm_bwd_apply_fwd_local_is_one_launch")
+        return rc == 1
+
+    def backward_apply_forward_local(self, batch: LookupBatch, dy: torch.Tensor, ws: "CoalescedGrad",
+                                     grad_bits: int, s_avg: torch.Tensor, lr: float, next_batch: LookupBatch,
+                                     bits: int = 4, refresh_scale: bool = True, full_precision: bool = False,
+                                     out: torch.Tensor | None = None, layout: str = "tbd", repack: bool = False,
+                                     ste: bool = True, dy_layout: str = "tbd") -> torch.Tensor:
+        """World size 1 at the step boundary: backward_apply_local(batch, dy, ...) followed by
+        forward(next_batch, ...) -- the embedding update of step i and apply_emb of step i+1,
+        adjacent in the training loop -- with the same results; for Criteo-form batches of one
+        size the forward runs inside the update's launch, table by table as each table's update
+        completes (dqrm_emb_bwd_apply_fwd_local). Returns the next batch's output."""
+        if next_batch.num_tables != self.T:
+            raise ValueError("batch has %d tables, set has %d" % (next_batch.num_tables, self.T))
+        B, T, D = next_batch.num_bags, self.T, self.D
+        if out is None:
+            out = torch.empty((T, B, D) if layout == "tbd" else (B, T, D), dtype=torch.float32, device=self.device)
+        ost, osb = (B * D, D) if layout == "tbd" else (D, T * D)
+        st, sb = self._dy_strides(dy, dy_layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_apply_fwd_local(
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), _ptr(ws.slot_cap_base),
+                ws.cap_total, _ptr(ws.rows), _ptr(ws.vals), _ptr(ws.ucount), _ptr(ws.absmax), int(grad_bits),
+                _ptr(s_avg), float(lr), 4 if repack else 0, *self._ws_args(batch), C.byref(next_batch.c), int(bits),
+                self._fwd_flags(refresh_scale, False, full_precision), _ptr(out), ost, osb, _stream_handle()),
+            "dqrm_emb_bwd_apply_fwd_local",
+        )
+        return out
+
 
 def slot_caps(num_rows: Sequence[int], max_lookups: int) -> list[int]:
     """Exclusive prefix of the coalesce-slot capacities (dqrm_coalesce_slot_caps): slot

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 8  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 9  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
@@ -54,7 +54,9 @@ extern "C" {
                                   dqrm_table_set.num_rows_host;
                                7: dqrm_emb_fwd_after_update;
                                8: dqrm_comm (RCCL communicator owned by libdqrm), dqrm_exchange
-                                  (the N > 1 exchange as two calls), dqrm_emb_bwd_lookup_grad_presum */
+                                  (the N > 1 exchange as two calls), dqrm_emb_bwd_lookup_grad_presum;
+                               9: dqrm_emb_bwd_apply_fwd_local (the next batch's forward behind the
+                                  one-launch update), dqrm_bwd_apply_fwd_local_is_one_launch */
 
 /* status codes */
 #define DQRM_OK            0
@@ -379,6 +381,30 @@ int dqrm_emb_bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch,
 /* 1 if dqrm_emb_bwd_apply_local would run this batch as ONE launch on `stream` (the current
  * device), 0 if as the two calls, <0 on bad arguments. */
 int dqrm_bwd_apply_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, void* stream);
+
+/* World size 1, the step boundary of a training loop: dqrm_emb_bwd_apply_local on `batch`,
+ * then dqrm_emb_fwd(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b) on the
+ * NEXT batch -- with the same results as those two calls (W and the |W| hierarchy, s_avg,
+ * scale[] and out bit for bit). In the training loop these two are adjacent: the embedding
+ * backward + update of step i (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1895-1904, at N=1)
+ * and apply_emb of step i+1 (dlrm_s_pytorch_single_gpu.py:609-674, q_m_n_q_g.py:317-398),
+ * whose indices the data loader has ready. When the update takes its one launch and `next`
+ * is a Criteo-form batch of the same size without DQRM_FWD_USE_PACKED, the forward runs in
+ * that launch: each table's workgroups, once the table's update and |W| maxima are final,
+ * gather and fake-quantize the next batch's rows of that table (no second launch, no wait
+ * for the other tables). Otherwise the two calls run. Error flags as the two calls'. */
+int dqrm_emb_bwd_apply_fwd_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                                 int64_t dy_stride_t, int64_t dy_stride_b, int ste, const int64_t* ws_cap_base,
+                                 int64_t ws_cap_total, int32_t* ws_rows, float* ws_vals, int32_t* ws_ucount,
+                                 float* ws_absmax, int grad_bits, float* s_avg, float lr, int repack_bits,
+                                 void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                                 uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                                 void* stream);
+
+/* 1 if dqrm_emb_bwd_apply_fwd_local would run batch + next as ONE launch on `stream`, 0 if
+ * not, <0 on bad arguments. */
+int dqrm_bwd_apply_fwd_local_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch,
+                                           const dqrm_batch* next, uint32_t fwd_flags, void* stream);
 
 /* Which kernel dqrm_apply_sparse_update launches (process-wide; returns the previous
  * choice, or DQRM_E_INVALID). FLAT: one lane group per payload entry over the whole chip,

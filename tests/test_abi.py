@@ -32,7 +32,7 @@ def test_header_declares_what_binding_expects():
 def test_library_exports_every_header_symbol(lib):
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 8
+    assert lib.dqrm_abi_version() == L.DQRM_ABI_VERSION == 9
 
 
 def test_payload_bytes_agree(lib):
@@ -73,6 +73,17 @@ def test_exchange_and_comm_reject_bad_arguments_without_device(lib):
     assert lib.dqrm_comm_allgather(None, None, None, 0, None) == L.DQRM_E_INVALID
     assert lib.dqrm_comm_destroy(None) == L.DQRM_OK
     assert lib.dqrm_emb_bwd_lookup_grad_presum(None, None, None, 0, 0, 1, None, None, None) == L.DQRM_E_INVALID
+
+
+def test_fused_next_forward_rejects_bad_arguments_without_device(lib):
+    """dqrm_emb_bwd_apply_fwd_local validates the next batch's forward as dqrm_emb_fwd does
+    (before any launch)."""
+    ts = L.TableSet()
+    ts.num_tables, ts.dim = 2, 12  # dim must be 4 * 2^k
+    args = [C.byref(ts), None, None, 0, 0, 1, None, 0, None, None, None, None, 8, None, 0.1, 0, None, 0]
+    assert lib.dqrm_emb_bwd_apply_fwd_local(*args, None, 4, 0, None, 0, 0, None) == L.DQRM_E_INVALID
+    assert b"dim" in lib.dqrm_last_error()
+    assert lib.dqrm_bwd_apply_fwd_local_is_one_launch(None, None, None, 0, None) == L.DQRM_E_INVALID
 
 
 def test_apply_kernel_selector(lib):

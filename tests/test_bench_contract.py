@@ -86,6 +86,13 @@ def test_phase_names(bench):
     assert bench.phase_names("dp", False, True) == ["emb_fwd", "bwd_coalesce", "apply_local"]
     assert bench.phase_names("dp", False, False) == ["emb_fwd", "bwd_coalesce", "grad_quant_pack",
                                                      "apply_sparse_update"]
+    assert bench.phase_names("dp", False, True, True) == ["emb_fwd", "bwd_apply_local"]
+    # the step boundary in one launch: the update of step i and the forward of step i+1
+    assert bench.phase_names("dp", False, True, True, True) == ["bwd_apply_fwd_local"]
+    T, B, D, U = 26, 2048, 64, 40000
+    assert bench.alg_bytes("bwd_apply_fwd_local", T, B, D, U) == (bench.alg_bytes("bwd_apply_local", T, B, D, U)
+                                                                  + bench.alg_bytes("emb_fwd", T, B, D, U))
+    assert "bwd_apply_fwd_local" in bench.KERNEL_SYMBOL
 
 
 @pytest.mark.parametrize("mode", ["dp", "sgd", "fwd"])

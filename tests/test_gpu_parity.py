@@ -944,3 +944,72 @@ def test_sgd_small_criteo_form_matches_oracle(dq, B, D, dist):
     ts.refresh_absmax()
     for x, y in zip(inc, (ts.rowmax, ts.blkmax, ts.sblkmax, ts.tmax)):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("D,B,dist,layout,refresh,full", [(64, 2048, "uniform", "tbd", True, False),
+                                                          (64, 2048, "zipf", "btd", True, False),
+                                                          (16, 2048, "uniform", "btd", True, False),
+                                                          (16, 4096, "zipf", "tbd", False, False),
+                                                          (32, 1000, "uniform", "tbd", True, True),
+                                                          (256, 700, "zipf", "btd", True, False)])
+def test_fused_next_forward_matches_separate_calls(dq, D, B, dist, layout, refresh, full):
+    """dqrm_emb_bwd_apply_fwd_local -- the one-launch update of step i with the forward of
+    batch i+1 inside the same launch (each table's workgroups gather its next rows once the
+    table's update and |W| maxima are final) -- against dqrm_emb_bwd_apply_local followed by
+    dqrm_emb_fwd on a copy of the tables, bit for bit over four steps: the forward outputs,
+    the forward scale, W, s_avg and the |W| hierarchy. Tables: dimension-split (3 ... 1793
+    rows), row-split with and without sub-slots (2208 ... 20 M rows); out-of-range indices in
+    a next batch give zeros and the same flag. Reference: apply_emb (dlrm_s_pytorch_single_gpu.py
+    :609-674) after weight_update_parallel_comm (s_q_g_p_c.py:601-628)."""
+    rows = COAL_ROWS
+    T = len(rows)
+    sets = [dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=131) for _ in range(2)]
+    s_avg = [torch.zeros(T, dtype=torch.float32, device="cuda") for _ in range(2)]
+    Ps = [G.pooling_one(rows, B, 141 + k, dist=dist) for k in range(5)]
+    Ps[2][0, 11] = 3       # out of range on the 3-row table (the forward of step 1's next batch)
+    Ps[2][5, 9] = -2       # negative on a row-split table
+    bs = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+    assert sets[0].apply_fwd_local_is_one_launch(bs[0], bs[1])
+    kw = dict(refresh_scale=refresh, full_precision=full, layout=layout)
+    ys = [ts.forward(bs[0], **kw) for ts in sets]
+    assert torch.equal(ys[0], ys[1])
+    for it in range(4):
+        dy = torch.from_numpy(G.upstream_grad(T, B, D, 151 + it) * 30).cuda()
+        ws = [dq.CoalescedGrad.allocate(rows, B, D, "cuda") for _ in range(2)]
+        y0 = sets[0].backward_apply_forward_local(bs[it], dy, ws[0], 8, s_avg[0], 0.5, bs[it + 1], **kw)
+        sets[1].backward_apply_local(bs[it], dy, ws[1], 8, s_avg[1], 0.5)
+        y1 = sets[1].forward(bs[it + 1], **kw)
+        errs = [ts.read_errors() for ts in sets]
+        assert errs[0] == errs[1] and (errs[0] != 0) == (it == 1), (it, errs)
+        assert torch.equal(y0, y1), it
+        assert torch.equal(s_avg[0], s_avg[1]), it
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
+    # and the last output is the oracle's forward of the updated tables (tables 0 and 7)
+    for t in (0, 7):
+        yt = (y0[t] if layout == "tbd" else y0[:, t]).cpu().numpy()
+        Wt = sets[0].table_weight(t).cpu().numpy()
+        st = np.float32(1.0) if full else np.float32(sets[0].scale[t].item())
+        want, _ = O.emb_fwd(Wt, Ps[4][t], np.arange(B, dtype=np.int64), st, 4, full_precision=full)
+        np.testing.assert_array_equal(yt, want)
+
+
+def test_fused_next_forward_packed_falls_back(dq):
+    """A next batch the fused forward does not take (a different batch size) runs as the two
+    calls, with the same results."""
+    rows, D = [3, 971, 40000, 2208], 32
+    T = len(rows)
+    sets = [dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=5) for _ in range(2)]
+    s_avg = [torch.zeros(T, dtype=torch.float32, device="cuda") for _ in range(2)]
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, 512, 1)).cuda())
+    nb = dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, 256, 2)).cuda())
+    assert not sets[0].apply_fwd_local_is_one_launch(b, nb)
+    dy = torch.from_numpy(G.upstream_grad(T, 512, D, 3) * 30).cuda()
+    ws = [dq.CoalescedGrad.allocate(rows, 512, D, "cuda") for _ in range(2)]
+    for ts in sets:
+        ts.forward(b)
+    y0 = sets[0].backward_apply_forward_local(b, dy, ws[0], 8, s_avg[0], 0.5, nb)
+    sets[1].backward_apply_local(b, dy, ws[1], 8, s_avg[1], 0.5)
+    y1 = sets[1].forward(nb)
+    assert torch.equal(y0, y1)
+    assert torch.equal(sets[0].W, sets[1].W)
