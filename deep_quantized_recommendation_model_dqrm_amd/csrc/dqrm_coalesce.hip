@@ -130,6 +130,15 @@ __device__ __forceinline__ uint32_t kgat(uint64_t x) { return (uint32_t)x >> LK_
 __device__ __forceinline__ uint32_t kbag(uint64_t x) { return (uint32_t)x & LK_MASK; }
 // 16-B load of bytes another workgroup of the launch stored write-through (sc1): an sc1
 // buffer load (L2-served, past this CU's L1), tracked by the compiler's vmcnt accounting
+// 16-B load past the L1 at a per-lane address (a buffer load needs a wave-uniform base: with
+// one row per lane the compiler would loop over the lanes' bases): global_load ... nt,
+// L2-served like sc1 (MI355X_MICROARCH.md, inter-workgroup visibility table)
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(x[0], x[1], x[2], x[3]);
+}
+
 __device__ __forceinline__ float4 ld4_sc1(const float* base, uint32_t byte_off) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -592,7 +601,9 @@ __device__ __forceinline__ void recover_stalled(const dqrm_internal::CoalesceArg
 // re-reduced here, superblock / table growth by atomicMax, shrunk superblocks flagged for the
 // table's last workgroup. The W rows are loaded before the segment phase, so the update's
 // random-row latency hides behind the coalesce.
-template <bool APPLY, bool RM>
+// FWD (APPLY only; dqrm_emb_bwd_apply_fwd_local): the next batch's forward behind the update,
+// its own instantiation so the update-only kernel keeps its registers.
+template <bool APPLY, bool RM, bool FWD>
 __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs a, dqrm_internal::LocalApplyArgs la) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ int s_cnt[MAXI * NW];
@@ -1418,7 +1429,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
         const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
         bool dirty = false;
-        const bool wt_rows = dsplit && la.fwd_idx != nullptr;
+        const bool wt_rows = FWD && dsplit;
         // a workgroup that updates ONE row-range slot keeps its rows' new maxima in LDS (the
         // stage, free by now): a shrunk block is then re-reduced from the other rows' stored
         // maxima (untouched this launch) and these, with no wait for its own stores
@@ -1644,14 +1655,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             s_fin = last && ((now >> 16) != 0u || sm != 0u);
         }
         __syncthreads();
-        // the next batch's indices (fused forward): in flight across the recovery / finalize
-        // and the wait for the table's final max
-        int64_t nx[MAXI];
-#pragma unroll
-        for (int i = 0; i < MAXI; ++i) {
-            const int b = tid + TPB * i;
-            nx[i] = (la.fwd_idx != nullptr && b < B) ? la.fwd_idx[(int64_t)t * B + b] : -1;
-        }
         if (s_stallmask) {  // uniform, rare: apply the stalled workgroups' rows (then finalize)
             recover_stalled(a, la, t, (uint32_t)s_stallmask, gran, NG, K, dsplit, NA, nblk, s_cb);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1671,7 +1674,14 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         //    the writers stored into before they arrived. Out-of-range rows: workgroup (0, 0)
         //    writes zeros and flags them. A stalled workgroup's share (its rows were applied by
         //    the last arriver) is the last arriver's.
-        if (la.fwd_idx != nullptr) {  // uniform
+        if constexpr (FWD) {
+            // the next batch's indices, in flight across the wait below
+            int64_t nx[MAXI];
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i) {
+                const int b = tid + TPB * i;
+                nx[i] = b < B ? la.fwd_idx[(int64_t)t * B + b] : -1;
+            }
             const bool refresh = (la.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
             const bool fullp = (la.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
             uint64_t* fword = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
@@ -1759,7 +1769,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 #pragma unroll
                 for (int u = 0; u < FU; ++u) {
                     const uint32_t x = (uint32_t)(e[u] >> 32);
-                    v[u] = nrows > 0 ? ld4_sc1(la.W + (rb + (x != 0xFFFFFFFFu ? x : 0u)) * a.D, (uint32_t)sub * 16u)
+                    v[u] = nrows > 0 ? ld4_nt(la.W + (rb + (x != 0xFFFFFFFFu ? x : 0u)) * a.D + sub * 4)
                                      : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
@@ -1775,7 +1785,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                     reinterpret_cast<float4*>(outt + (int64_t)(uint32_t)e[u] * la.fwd_ost_b)[sub] = y;
                 }
             }
-            CDIAG_W(17);
+            CDIAG_W(18);  // (diagnostic build: the next batch's forward done)
         }
     }
 }
@@ -1788,10 +1798,12 @@ hipError_t allow_coalesce_lds() {
     static std::once_flag once;
     static hipError_t attr = hipSuccess;
     std::call_once(once, [] {
-        const void* fns[] = {reinterpret_cast<const void*>(k_coalesce_p1<false, false>),
-                             reinterpret_cast<const void*>(k_coalesce_p1<false, true>),
-                             reinterpret_cast<const void*>(k_coalesce_p1<true, false>),
-                             reinterpret_cast<const void*>(k_coalesce_p1<true, true>)};
+        const void* fns[] = {reinterpret_cast<const void*>(k_coalesce_p1<false, false, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<false, true, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, false, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, true, false>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, false, true>),
+                             reinterpret_cast<const void*>(k_coalesce_p1<true, true, true>)};
         for (const void* f : fns)
             if (attr == hipSuccess) attr = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     });
@@ -1841,8 +1853,10 @@ bool coalesce_apply_resident(int T, hipStream_t stream) {
         int cus = 0, occ = 0;
         if (allow_coalesce_lds() != hipSuccess) return;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
-        for (const void* f : {reinterpret_cast<const void*>(k_coalesce_p1<true, false>),
-                              reinterpret_cast<const void*>(k_coalesce_p1<true, true>)}) {
+        for (const void* f : {reinterpret_cast<const void*>(k_coalesce_p1<true, false, false>),
+                              reinterpret_cast<const void*>(k_coalesce_p1<true, true, false>),
+                              reinterpret_cast<const void*>(k_coalesce_p1<true, false, true>),
+                              reinterpret_cast<const void*>(k_coalesce_p1<true, true, true>)}) {
             int o = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, TPB, LDS_BYTES) != hipSuccess) return;
             occ = occ == 0 || o < occ ? o : occ;
@@ -1881,11 +1895,14 @@ hipError_t launch_coalesce_pool1(const CoalesceArgs& a, const LocalApplyArgs* la
         }();
         LocalApplyArgs l2 = *la;
         l2.spin_limit = spin;
-        if (rm) hipLaunchKernelGGL((k_coalesce_p1<true, true>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
-        else hipLaunchKernelGGL((k_coalesce_p1<true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
+        const bool fwd = l2.fwd_idx != nullptr;
+        if (rm && fwd) hipLaunchKernelGGL((k_coalesce_p1<true, true, true>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
+        else if (fwd) hipLaunchKernelGGL((k_coalesce_p1<true, false, true>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
+        else if (rm) hipLaunchKernelGGL((k_coalesce_p1<true, true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
+        else hipLaunchKernelGGL((k_coalesce_p1<true, false, false>), grid, dim3(TPB), LDS_BYTES, stream, a, l2);
     } else {
-        if (rm) hipLaunchKernelGGL((k_coalesce_p1<false, true>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
-        else hipLaunchKernelGGL((k_coalesce_p1<false, false>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
+        if (rm) hipLaunchKernelGGL((k_coalesce_p1<false, true, false>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
+        else hipLaunchKernelGGL((k_coalesce_p1<false, false, false>), grid, dim3(TPB), LDS_BYTES, stream, a, LocalApplyArgs{});
     }
     return hipGetLastError();
 }

@@ -70,6 +70,7 @@ sys.path[:0] = [{here!r}, {golden!r}, {root!r}]
 import gen_inputs as G
 import deep_quantized_recommendation_model_dqrm_amd as dq
 from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
 rows, D, B, steps = {rows!r}, {D}, {B}, 3
 T = len(rows)
 sets = [dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=7) for _ in range(2)]
@@ -84,7 +85,8 @@ for it in range(steps):
     dy = torch.from_numpy(G.upstream_grad(T, B, D, 80 + it) * 30).cuda()
     ws = [dq.CoalescedGrad.allocate(rows, B, D, "cuda") for _ in range(2)]
     y0 = sets[0].backward_apply_forward_local(bs[it], dy, ws[0], 8, s_avg[0], 0.5, bs[it + 1])
-    sets[1].backward_apply_local(bs[it], dy, ws[1], 8, s_avg[1], 0.5)
+    sets[1].backward_coalesce(bs[it], dy, ws[1])  # the two-launch path (no rendezvous to stall)
+    HipExchangeKernels(sets[1]).apply_local(ws[1], 8, s_avg[1], 0.5, False)
     y1 = sets[1].forward(bs[it + 1])
     e0, e1 = sets[0].read_errors(), sets[1].read_errors()
     assert e1 == 0 and (e0 & ~L.DQRM_ERRF_STALL) == 0, (e0, e1)

@@ -4,8 +4,10 @@ compacted, 3 sorted, 4 heads, 5 stage landed, 6 segments done (stores issued), 7
 table's slowest workgroup over its slots and, in the one-launch step, sub-slots); with
 "apply" (the one-launch local step, dqrm_emb_bwd_apply_local): 11 the table's workgroups
 met, 16 every load landed (the W prefetch), 14 prefetched rows updated, 15 all rows
-updated, 12 owned blocks re-reduced, 13 end (after the table's last-workgroup finalize).
-usage: python tools/diag_coalesce.py [terabyte|terabyte_ref|kaggle] [B] [apply]"""
+updated, 12 owned blocks re-reduced, 13 end (after the table's last-workgroup finalize);
+with "applyfwd" (dqrm_emb_bwd_apply_fwd_local: the next batch's forward in the same launch)
+also 18, the workgroup's forward share done.
+usage: python tools/diag_coalesce.py [terabyte|terabyte_ref|kaggle] [B] [apply|applyfwd]"""
 import ctypes as C
 import os
 import sys
@@ -22,7 +24,8 @@ from deep_quantized_recommendation_model_dqrm_amd.workloads import CONFIGS  # no
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "terabyte"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
-APPLY = len(sys.argv) > 3 and sys.argv[3] == "apply"
+APPLY = len(sys.argv) > 3 and sys.argv[3] in ("apply", "applyfwd")
+FWD = len(sys.argv) > 3 and sys.argv[3] == "applyfwd"
 rows, D = CONFIGS[cfg]
 T = len(rows)
 lib = L.load()
@@ -37,11 +40,14 @@ bs = [dq.LookupBatch.pooling_one(torch.stack([torch.randint(0, n, (B,), generato
 dy = torch.randn(T, B, D, device="cuda", generator=g) * 0.05
 ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
 s_avg = torch.zeros(T, device="cuda")
+y = torch.empty(T, B, D, device="cuda")
 
 
 def run(i):
     b = bs[i % NB]
-    if APPLY:
+    if FWD:  # this batch's forward ran in the previous launch
+        ts.backward_apply_forward_local(b, dy, ws, 8, s_avg, 0.01, bs[(i + 1) % NB], ste=STE, out=y)
+    elif APPLY:
         ts.forward(b)
         ts.backward_apply_local(b, dy, ws, 8, s_avg, 0.01, ste=STE)
     else:
@@ -63,7 +69,7 @@ for i in range(NB):  # one launch per batch, read after each
     k0 = c[:, :, 0][c[:, :, 0] > 0].min()
     c = np.where(c >= k0, c - k0, -1)  # -1: not stamped in this launch
     cs.append(c)
-end = 13 if APPLY else 7
+end = 18 if FWD else 13 if APPLY else 7
 spans = [c[:, :, end].max() / 100 for c in cs]
 print(f"{cfg} B={B} D={D}: span median {np.median(spans):.1f} us over {NB} launches (min {min(spans):.1f}, "
       f"max {max(spans):.1f}), each on a batch not used in the previous {NB - 1}")
@@ -106,4 +112,10 @@ if APPLY:
         print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} {ph[1]:5.1f} {ph[2]:5.1f} || {ph[3]:5.1f}   "
               f"(updated = W landed {ph[4]:4.1f} | prefetched rows {ph[5]:4.1f} | rest+barrier {ph[6]:4.1f} | "
               f"re-reduce {ph[7]:4.1f})")
+if FWD:
+    print("next-batch forward per table, slowest workgroup, median (us): finalize end -> forward done || end")
+    for t in np.argsort(-np.median([c[:, :, 18].max(axis=1) for c in cs], axis=0)):
+        ps = [slow(c, t, 18) for c in cs]
+        ph = np.median([[p[18] - max(p[13], 0), p[18]] for p in ps], axis=0) / 100
+        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} || {ph[1]:5.1f}")
 print("errors", ts.read_errors())
