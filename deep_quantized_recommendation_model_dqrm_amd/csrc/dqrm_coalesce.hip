@@ -130,15 +130,6 @@ __device__ __forceinline__ uint32_t kgat(uint64_t x) { return (uint32_t)x >> LK_
 __device__ __forceinline__ uint32_t kbag(uint64_t x) { return (uint32_t)x & LK_MASK; }
 // 16-B load of bytes another workgroup of the launch stored write-through (sc1): an sc1
 // buffer load (L2-served, past this CU's L1), tracked by the compiler's vmcnt accounting
-// 16-B load past the L1 at a per-lane address (a buffer load needs a wave-uniform base: with
-// one row per lane the compiler would loop over the lanes' bases): global_load ... nt,
-// L2-served like sc1 (MI355X_MICROARCH.md, inter-workgroup visibility table)
-__device__ __forceinline__ float4 ld4_nt(const float* p) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f x = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-    return make_float4(x[0], x[1], x[2], x[3]);
-}
-
 __device__ __forceinline__ float4 ld4_sc1(const float* base, uint32_t byte_off) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -1429,7 +1420,6 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         const ApplyUpdate upd{DQRM_UPD_DP, 1.0f, sv, sv, la.nlr};
         const float r_pack = la.repack ? 1.0f / la.pscale[t] : 0.0f;
         bool dirty = false;
-        const bool wt_rows = FWD && dsplit;
         // a workgroup that updates ONE row-range slot keeps its rows' new maxima in LDS (the
         // stage, free by now): a shrunk block is then re-reduced from the other rows' stored
         // maxima (untouched this launch) and these, with no wait for its own stores
@@ -1450,9 +1440,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             acc.z = fake_quant(v.z, rr, qlo, qhi) + 0.0f; acc.w = fake_quant(v.w, rr, qlo, qhi) + 0.0f;
             float4 wn;
             wn.x = upd(w0.x, acc.x); wn.y = upd(w0.y, acc.y); wn.z = upd(w0.z, acc.z); wn.w = upd(w0.w, acc.w);
-            // (a dimension-split table's rows are read by its other workgroups in the fused
-            // forward: stored write-through then, as every hand-off)
-            st4_w(reinterpret_cast<float4*>(la.W + grow * a.D) + sub, wn, wt_rows);
+            reinterpret_cast<float4*>(la.W + grow * a.D)[sub] = wn;
             if (la.repack) pack4_row(wn, la.packed + grow * (a.D / 2), sub, r_pack);
             float old_rm = abs_max4(w0), rm = abs_max4(wn);
             for (int o = 1; o < LPR; o <<= 1) {
@@ -1667,24 +1655,86 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
         // 9. the NEXT batch's forward (dqrm_emb_bwd_apply_fwd_local): emb_fwd_table's
         //    arithmetic for pooling 1, y[b] = fake-quant(W[row_b]) with the scale of the updated
         //    table. The table's last arriver publishes its final max (FWD_WORD granule, after
-        //    the finalize); the others wait for it. Who reads which row: a row split reads only
-        //    the rows of its own range -- updated by itself (or untouched) -- so its own stores
-        //    are what it reads; a dimension-split table (one XCD, no sub-slots) splits the
-        //    lookups evenly and reads its rows with sc1 loads past the L1, from the XCD's L2
-        //    the writers stored into before they arrived. Out-of-range rows: workgroup (0, 0)
-        //    writes zeros and flags them. A stalled workgroup's share (its rows were applied by
-        //    the last arriver) is the last arriver's.
+        //    the finalize); the others wait for it. Which workgroup gathers which lookup: a row
+        //    split the rows of its own range -- updated by itself (or untouched) -- so its row
+        //    loads go out before the wait; a dimension-split table (one XCD, no sub-slots) deals
+        //    the lookups round-robin and reads after the wait, from the XCD's L2. Out-of-range
+        //    rows: workgroup (0, 0) writes zeros and flags them. A stalled workgroup's share (its
+        //    rows were applied by the last arriver) is the last arriver's.
         if constexpr (FWD) {
-            // the next batch's indices, in flight across the wait below
+            const bool refresh = (la.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
+            const bool fullp = (la.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
+            uint64_t* fword = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
+            // (i) this workgroup's lookups of the next batch -- they do not depend on the table's
+            //     final max -- as per-wave LDS lists {row | 0xFFFFFFFF, b} in lookup order (the
+            //     key region is dead by now). A dimension-split table deals its lookups round-robin
+            //     over its NA workgroups (every wave gets some); a row split takes the rows of its
+            //     own range; the last arriver also the stalled workgroups' shares.
             int64_t nx[MAXI];
 #pragma unroll
             for (int i = 0; i < MAXI; ++i) {
                 const int b = tid + TPB * i;
                 nx[i] = b < B ? la.fwd_idx[(int64_t)t * B + b] : -1;
             }
-            const bool refresh = (la.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
-            const bool fullp = (la.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
-            uint64_t* fword = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
+            const int me = s + SPLIT * j;
+            const uint32_t smask = s_lastarr ? (uint32_t)s_stallmask : 0u;
+            const int lane = tid % WAVE;
+            uint64_t* lst = keys + w * (WAVE * MAXI);
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i) {
+                const int b = tid + TPB * i;
+                const int64_t x = nx[i];
+                const bool okr = x >= 0 && x < nrows;
+                int own = 0;
+                if (dsplit) {
+                    own = b % NA;
+                } else if (okr) {
+                    const int sl = slot_of_row(x, nblk);
+                    int jj = 0;
+                    if (K == 2) {
+                        const int64_t b0 = nblk * sl / SPLIT, b1 = nblk * (sl + 1) / SPLIT;
+                        jj = (x >> 8) >= (b0 + b1) / 2 ? 1 : 0;
+                    }
+                    own = sl + SPLIT * jj;
+                }
+                const bool mine = b < B && ((own == me && go) || ((smask >> own) & 1u));
+                const uint64_t m = __ballot(mine);
+                if (mine) {
+                    const int p = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    lst[p] = ((uint64_t)(okr ? (uint32_t)x : 0xFFFFFFFFu) << 32) | (uint32_t)b;
+                    if (!okr) flag_error(a.err, DQRM_ERRF_INDEX);
+                }
+                cnt += __popcll(m);
+            }
+            CDIAG(20);
+            // (ii) a row split reads only rows it updated itself (or untouched ones): its first
+            //      rows go out now, in flight across the wait for the table's final max. Plain
+            //      loads: a workgroup's own stores are visible to it, and a dimension-split
+            //      table's rows (other workgroups' stores, one XCD) were never loaded by this CU
+            //      in this launch -- its slot ranges are block-aligned, no line is shared -- so
+            //      they come from the XCD's L2, once the wait below has ordered them.
+            const int G = LPR < WAVE ? WAVE / LPR : 1;  // rows per wave pass
+            const int gl = lane / LPR, sub = lane % LPR;
+            constexpr int FU = 4;  // rows per lane group in flight
+            uint64_t e[FU];
+            float4 v[FU];
+            auto issue = [&](int p0) {
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const int ix = p0 + gl + G * u;
+                    e[u] = ix < cnt && lane < G * LPR ? lst[ix] : ~0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < FU; ++u) {
+                    const uint32_t x = (uint32_t)(e[u] >> 32);
+                    v[u] = nrows > 0 ? reinterpret_cast<const float4*>(la.W + (rb + (x != 0xFFFFFFFFu ? x : 0u)) * a.D)[sub]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            };
+            if (!dsplit && cnt > 0) issue(0);
+            // (iii) the table's final max: the last arriver publishes it, the others wait
             if (s_lastarr) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
@@ -1714,64 +1764,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 s_fok = ok;
             }
             __syncthreads();
+            CDIAG(19);
+            if (!s_fok) cnt = 0;  // (uniform)
             const float sf = fullp ? 1.0f : (refresh ? sym_scale(s_ftm, la.fwd_bits) : la.fwd_scale[t]);
             if (refresh && !fullp && s_lastarr && tid == 0) la.fwd_scale[t] = sf;
             const float rf = 1.0f / sf;
             const float fqlo = -(float)(1 << (la.fwd_bits - 1)), fqhi = (float)((1 << (la.fwd_bits - 1)) - 1);
-            // this workgroup's lookups, per wave as an LDS list {row | 0xFFFFFFFF, b} in lookup
-            // order (the keys region is dead by now)
-            const int me = s + SPLIT * j;
-            const uint32_t smask = s_lastarr ? (uint32_t)s_stallmask : 0u;
-            const int per = (B + NA - 1) / NA;
-            const int lane = tid % WAVE;
-            uint64_t* lst = keys + w * (WAVE * MAXI);
-            int cnt = 0;
-#pragma unroll
-            for (int i = 0; i < MAXI; ++i) {
-                const int b = tid + TPB * i;
-                const int64_t x = nx[i];
-                const bool okr = x >= 0 && x < nrows;
-                int own = 0;
-                if (dsplit) {
-                    own = b / per;
-                } else if (okr) {
-                    const int sl = slot_of_row(x, nblk);
-                    int jj = 0;
-                    if (K == 2) {
-                        const int64_t b0 = nblk * sl / SPLIT, b1 = nblk * (sl + 1) / SPLIT;
-                        jj = (x >> 8) >= (b0 + b1) / 2 ? 1 : 0;
-                    }
-                    own = sl + SPLIT * jj;
-                }
-                const bool mine = s_fok && b < B && ((own == me && go) || ((smask >> own) & 1u));
-                const uint64_t m = __ballot(mine);
-                if (mine) {
-                    const int p = cnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    lst[p] = ((uint64_t)(okr ? (uint32_t)x : 0xFFFFFFFFu) << 32) | (uint32_t)b;
-                    if (!okr) flag_error(a.err, DQRM_ERRF_INDEX);
-                }
-                cnt += __popcll(m);
-            }
-            __syncthreads();
-            const int G = LPR < WAVE ? WAVE / LPR : 1;  // rows per wave pass
-            const int gl = lane / LPR, sub = lane % LPR;
             float* outt = la.fwd_out + (int64_t)t * la.fwd_ost_t;
-            constexpr int FU = 4;  // rows per lane group in flight
             for (int p0 = 0; p0 < cnt; p0 += G * FU) {  // uniform per wave
-                uint64_t e[FU];
-                float4 v[FU];
-#pragma unroll
-                for (int u = 0; u < FU; ++u) {
-                    const int ix = p0 + gl + G * u;
-                    e[u] = ix < cnt && lane < G * LPR ? lst[ix] : ~0ull;
-                }
-#pragma unroll
-                for (int u = 0; u < FU; ++u) {
-                    const uint32_t x = (uint32_t)(e[u] >> 32);
-                    v[u] = nrows > 0 ? ld4_nt(la.W + (rb + (x != 0xFFFFFFFFu ? x : 0u)) * a.D + sub * 4)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
+                if (p0 > 0 || dsplit) issue(p0);
+                if (p0 == 0) CDIAG_W(21);
 #pragma unroll
                 for (int u = 0; u < FU; ++u) {
                     if (e[u] == ~0ull) continue;

@@ -113,9 +113,14 @@ if APPLY:
               f"(updated = W landed {ph[4]:4.1f} | prefetched rows {ph[5]:4.1f} | rest+barrier {ph[6]:4.1f} | "
               f"re-reduce {ph[7]:4.1f})")
 if FWD:
-    print("next-batch forward per table, slowest workgroup, median (us): finalize end -> forward done || end")
+    print("next-batch forward per table, slowest workgroup, median (us): finalize end -> forward done "
+          "(= lists | final max seen | first rows landed (wave 0) | rest + stores) || end")
     for t in np.argsort(-np.median([c[:, :, 18].max(axis=1) for c in cs], axis=0)):
         ps = [slow(c, t, 18) for c in cs]
-        ph = np.median([[p[18] - max(p[13], 0), p[18]] for p in ps], axis=0) / 100
-        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} || {ph[1]:5.1f}")
+        ph = np.median([[p[18] - max(p[13], 0), p[20] - p[13], p[19] - p[20], p[21] - p[19], p[18] - p[21], p[18]]
+                        for p in ps], axis=0) / 100
+        print(f"t{t:2d} n={rows[t]:>10d}: {ph[0]:5.1f} (= {ph[1]:4.1f} | {ph[2]:4.1f} | {ph[3]:4.1f} | {ph[4]:4.1f}) "
+              f"|| {ph[5]:5.1f}")
+    w13 = [c[t, s, 13] for c in cs for t in range(T) for s in range(16) if c[t, s, 13] >= 0]
+    print("table last-arrival spread: see 'apply phases' ends above; workgroups stamped:", len(w13))
 print("errors", ts.read_errors())
