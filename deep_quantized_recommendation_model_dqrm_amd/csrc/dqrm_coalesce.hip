@@ -619,6 +619,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     __shared__ int s_lastarr;
     __shared__ float s_ftm;
     __shared__ int s_fok;
+    __shared__ int s_pub;
     __shared__ uint32_t s_oq_blk[OWN_Q];
     __shared__ float s_oq_old[OWN_Q];
     __shared__ float s_oq_sold[OWN_Q];
@@ -1641,6 +1642,18 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             s_stallmask = (int)sm;
             s_lastarr = last ? 1 : 0;
             s_fin = last && ((now >> 16) != 0u || sm != 0u);
+            s_pub = 0;
+            if (FWD && last && !s_fin) {
+                // fused forward: nothing to finalize or recover, so the table max is final now
+                // (every workgroup's growth atomics landed before its arrival): published at
+                // once, the table's other workgroups wait on it (step 9)
+                const float tm = ld_wt(la.tmax + t);
+                s_ftm = tm;
+                s_fok = 1;
+                s_pub = 1;
+                __hip_atomic_store(reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD),
+                                   gr_make(tm, 0, epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
         if (s_stallmask) {  // uniform, rare: apply the stalled workgroups' rows (then finalize)
@@ -1665,6 +1678,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const bool refresh = (la.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
             const bool fullp = (la.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
             uint64_t* fword = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
+            if (s_lastarr && !s_pub) {  // after the recovery / finalize: the final max, then published
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    const float tm = ld_wt(la.tmax + t);
+                    s_ftm = tm;
+                    s_fok = 1;
+                    __hip_atomic_store(fword, gr_make(tm, 0, epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             // (i) this workgroup's lookups of the next batch -- they do not depend on the table's
             //     final max -- as per-wave LDS lists {row | 0xFFFFFFFF, b} in lookup order (the
             //     key region is dead by now). A dimension-split table deals its lookups round-robin
@@ -1734,17 +1757,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
                 }
             };
             if (!dsplit && cnt > 0) issue(0);
-            // (iii) the table's final max: the last arriver publishes it, the others wait
-            if (s_lastarr) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    const float tm = ld_wt(la.tmax + t);
-                    s_ftm = tm;
-                    s_fok = 1;
-                    __hip_atomic_store(fword, gr_make(tm, 0, epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else if (tid == 0) {
+            // (iii) the table's final max: published by the last arriver (above, or at its
+            //       arrival), the others wait for it
+            if (!s_lastarr && tid == 0) {
                 // a workgroup that stalled at the rendezvous leaves its share to the last arriver
                 // and does not wait (its CU may be what a late workgroup of the table needs);
                 // the others met every workgroup of the table there, so all of them arrive
@@ -1772,7 +1787,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             const float fqlo = -(float)(1 << (la.fwd_bits - 1)), fqhi = (float)((1 << (la.fwd_bits - 1)) - 1);
             float* outt = la.fwd_out + (int64_t)t * la.fwd_ost_t;
             for (int p0 = 0; p0 < cnt; p0 += G * FU) {  // uniform per wave
-                if (p0 > 0 || dsplit) issue(p0);
+                if (p0 > 0 || dsplit) issue(p0);  // (the first rows of a row split went out before the wait)
                 if (p0 == 0) CDIAG_W(21);
 #pragma unroll
                 for (int u = 0; u < FU; ++u) {
