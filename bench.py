@@ -115,8 +115,9 @@ def parse(argv=None):
     p.add_argument("--two-launch-local", action="store_true",
                    help="N=1: coalesce + dqrm_apply_local as two launches (not dqrm_emb_bwd_apply_local)")
     p.add_argument("--sample-every", type=int, default=0,
-                   help="bracket the dominant kernel with HIP events on every k-th timed step "
-                        "(0 = auto: at least 16 bracketed launches, at most every 8th step)")
+                   help="also bracket the dominant kernel with HIP events on every k-th TIMED step "
+                        "(0 = never: the roofline is timed on the untimed breakdown pass's >= 16 "
+                        "bracketed launches, so no event work sits inside the timed region)")
     p.add_argument("--traffic-profile", default=None,
                    help="rocprofv3 PMC summary (tools/prof_summary.py) for roofline.traffic; "
                         "default profiles/r2_<config>_summary.json when present")
@@ -377,7 +378,7 @@ def main():
     torch.cuda.synchronize()
     # per-phase breakdown (untimed, eager): every phase bracketed by events; picks the dominant.
     # Periodic mode: steady-state steps only; the refresh (every P steps) is timed apart.
-    nb = max(10, min(50, a.steps))
+    nb = max(16, min(50, a.steps))  # >= 16 bracketed launches of every phase
     bev = [timed_events(len(names)) for _ in range(nb)]
     for i in range(nb):
         step(i, bev[i], refresh=a.scale_period <= 0, split=True)
@@ -441,18 +442,19 @@ def main():
         torch.cuda.synchronize()
         sync_ms = (time.perf_counter() - t0s) / 3 * 1e3
 
-    # timed region: plain steps; the dominant kernel is bracketed by HIP events (on the stream
-    # it runs on) on every sample_every-th step, so the events barely perturb the timing
+    # timed region: plain steps. The dominant kernel's roofline time comes from the breakdown
+    # pass above (>= 16 event-bracketed launches); --sample-every k also brackets every k-th
+    # timed step (events on the stream the kernel runs on; not with graphs or the library exchange)
     if coll:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [timed_events(len(names)) for _ in range(a.steps)]
-    every = a.sample_every if a.sample_every > 0 else max(1, min(8, a.steps // 16))
-    # (graph replay / the library-issued exchange: the dominant kernel is timed in the breakdown pass)
-    sampled = [] if graphs is not None or lib_exchange else [i for i in range(a.steps) if i % every == 0]
+    every = a.sample_every
+    sampled = ([] if graphs is not None or lib_exchange or every <= 0 else
+               [i for i in range(a.steps) if i % every == 0])
+    evs = {i: timed_events(len(names)) for i in sampled}
     t_start = time.perf_counter()
     for i in range(a.steps):
-        run(a.warmup + i, evs[i] if i in sampled else None)
+        run(a.warmup + i, evs.get(i))
     if coll:
         dist.barrier()
     torch.cuda.synchronize()
@@ -462,7 +464,7 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     dom_ms = (float(np.mean([evs[i][dj][0].elapsed_time(evs[i][dj][1]) for i in sampled])) if sampled
-              else kms[dom])  # graph replay / library exchange: the breakdown pass's average (nb launches)
+              else kms[dom])  # the breakdown pass's average over its nb >= 16 bracketed launches
 
     # algorithmic bytes per launch; distinct rows of the last step's batch
     if ex is not None:
