@@ -133,7 +133,8 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "bwd_apply_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),  # N=1: coalesce + update in one launch
     # N=1 at the step boundary: the same kernel, with the next batch's forward inside
     "bwd_apply_fwd_local": ("k_coalesce_p1<true,", "k_coalesce_p1<true>"),
-    "bwd_sgd": ("k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
+    "bwd_sgd": ("k_sgd_small<{lpr}, false>", "k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
+    "bwd_sgd_fwd": ("k_sgd_small<{lpr}, true>",),  # ... with the next batch's forward in the launch
     "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
     "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_ranges<{lpr}>"),
     "apply_local": "k_apply_local<{lpr},",
@@ -188,6 +189,7 @@ def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
         "bwd_coalesce": L * 8 + offs + L * D * 4 + U * (D * 4 + 4),
         # index + dy row per lookup; W row read+write and |W| row max per distinct row
         "bwd_sgd": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
+        "bwd_sgd_fwd": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk + L * (D * 4 + 8) + offs + L * D * 4 + T * 4,
         # N=1 backward + update in one launch: as bwd_sgd (the coalesced rows never need HBM)
         "bwd_apply_local": L * 8 + offs + L * D * 4 + U * D * 8 + U * 4 + pk,
         # ... and the next batch's forward in the same launch: + emb_fwd's bytes
@@ -217,7 +219,7 @@ def phase_names(mode, use_packed, fused, one_launch=False, next_fwd=False):
     if mode == "fwd":
         return [fwd]
     if mode == "sgd":
-        return [fwd, "bwd_sgd"]
+        return ["bwd_sgd_fwd"] if next_fwd else [fwd, "bwd_sgd"]
     if fused and one_launch and next_fwd:
         return ["bwd_apply_fwd_local"]
     if fused and one_launch:
@@ -295,6 +297,10 @@ def main():
     # each timed step still runs one forward and one backward + update
     next_fwd = (one_launch and a.mode == "dp" and not a.use_packed and not a.separate_forward
                 and len(batches) > 1 and ts.apply_fwd_local_is_one_launch(batches[0], batches[1]))
+    # the same for the single-GPU SGD step (dqrm_emb_bwd_sgd_fwd: one launch when the small-batch
+    # kernel takes the update, config 3)
+    if a.mode == "sgd" and not a.use_packed and not a.separate_forward and len(batches) > 1:
+        next_fwd = True
     names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd)
 
     # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
@@ -316,10 +322,13 @@ def main():
 
         if next_fwd:  # this batch's forward ran in the previous step's launch; this one runs the next's
             nxt = batches[(i + 1) % len(batches)]
+            rf = a.scale_period <= 0 or (i + 1) % a.scale_period == 0
             mark(0, 0)
-            ts.backward_apply_forward_local(b, dy, ex.ws, a.grad_bits, ex.s_avg, a.lr, nxt, bits=4,
-                                            refresh_scale=a.scale_period <= 0 or (i + 1) % a.scale_period == 0,
-                                            out=y)
+            if a.mode == "sgd":
+                ts.backward_sgd_forward(b, dy, a.lr, nxt, bits=4, refresh_scale=rf, out=y, repack=repack)
+            else:
+                ts.backward_apply_forward_local(b, dy, ex.ws, a.grad_bits, ex.s_avg, a.lr, nxt, bits=4,
+                                                refresh_scale=rf, out=y)
             mark(0, 1)
             return
         mark(0, 0)
@@ -496,7 +505,8 @@ def main():
         replicas_match = all(torch.equal(allcs[0], c) for c in allcs)
     else:
         replicas_match = True
-    n1_update = (None if a.mode != "dp" or world > 1 else
+    n1_update = ("SGD of step i + forward of step i+1 (dqrm_emb_bwd_sgd_fwd)" if a.mode == "sgd" and next_fwd else
+                 None if a.mode != "dp" or world > 1 else
                  "coalesce + quant-pack + payload apply (RCCL at world size 1)" if coll else
                  "one launch: update of step i + forward of step i+1 (dqrm_emb_bwd_apply_fwd_local)" if next_fwd else
                  "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
@@ -567,7 +577,9 @@ def main():
                               "phases": names},
             "kernels_ms": {k: round(v, 5) for k, v in kms.items()},
             "kernels_ms_note": "untimed eager breakdown pass, every phase bracketed by events; " + (
-                "bwd_apply_fwd_local is ONE launch per step: coalesce, quantize, update and the |W| hierarchy of "
+                "bwd_sgd_fwd = the SGD of this step's batch, then the next batch's forward, one workgroup per "
+                "table (one launch when the small-batch kernel runs)" if a.mode == "sgd" and next_fwd
+                else "bwd_apply_fwd_local is ONE launch per step: coalesce, quantize, update and the |W| hierarchy of "
                 "this step's batch, then the next batch's fake-quant forward, table by table" if next_fwd
                 else "bwd_apply_local is ONE launch (coalesce, quantize, update and the |W| hierarchy)" if one_launch
                 else "apply_local = the fused quantize + update kernel + a short k_table_finalize launch" if fused

@@ -80,6 +80,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_bwd_apply_local_is_one_launch",
     "dqrm_emb_bwd_apply_fwd_local",
     "dqrm_bwd_apply_fwd_local_is_one_launch",
+    "dqrm_emb_bwd_sgd_fwd",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
     "dqrm_dense_grad_quant",
@@ -278,6 +279,11 @@ def load(path: str | None = None) -> C.CDLL:
              C.c_size_t, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P],
         ),
         "dqrm_bwd_apply_fwd_local_is_one_launch": (C.c_int, [TS, BA, BA, C.c_uint32, P]),
+        "dqrm_emb_bwd_sgd_fwd": (
+            C.c_int,
+            [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P, C.c_size_t, BA, C.c_int, C.c_uint32,
+             P, C.c_int64, C.c_int64, P],
+        ),
         "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
         "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),
         "dqrm_dense_grad_quant": (C.c_int, [DS, C.c_int, P, C.c_int, P, C.c_int, P, P]),

@@ -2379,6 +2379,14 @@ struct FArgs {
     uint64_t* gtmp;
     uint32_t* gbag;
     int64_t Lc;
+    // k_sgd_small<LPR, true>: the next Criteo-form batch's forward after the table's update
+    // (dqrm_emb_bwd_sgd_fwd; the same B), emb_fwd_table's arithmetic
+    const int64_t* fwd_idx;
+    float* fwd_out;
+    int64_t fwd_ost_t, fwd_ost_b;
+    float* fwd_scale;
+    int fwd_bits;
+    uint32_t fwd_flags;
 };
 
 // workspace: the spill regions, only when a slot can exceed the in-LDS key capacity
@@ -3051,8 +3059,11 @@ __host__ __device__ constexpr int64_t sg_hash_bytes(int L) {
     return (int64_t)(1 << sg_hash_log(L)) * (4 + 8 * ((L + 63) / 64));
 }
 
-template <int LPR>
+template <int LPR, bool FWD>
 __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
+    // FWD: after the table's update and |W| maxima (one workgroup holds the whole table, so they
+    // are final at its end -- no other workgroup to wait for), the next batch's forward of the
+    // table: its rows are this workgroup's own stores or untouched
     constexpr int D = LPR * 4;
     constexpr int G = SG_TPB / LPR;                              // lane groups
     constexpr int MAXL = sg_maxl(LPR);
@@ -3097,6 +3108,55 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
         xr[k] = i < L ? a.idx[ib + i] : -1;
     }
     const int64_t o0 = (!p1 && (int)threadIdx.x < B) ? a.off[(int64_t)t * B + threadIdx.x] : 0;
+    int64_t nxr[FWD ? NPG : 1];  // the next batch's rows of this lane group's bags (FWD)
+    if constexpr (FWD) {
+#pragma unroll
+        for (int k = 0; k < NPG; ++k) {
+            const int i = grp + k * G;
+            nxr[k] = i < B ? a.fwd_idx[(int64_t)t * B + i] : -1;
+        }
+    }
+    // the next batch's forward of this table, after its update and maxima (all threads, at
+    // every exit below): the final table max, the scale, then the rows and their stores
+    __shared__ float s_ftm;
+    auto fwd_tail = [&]() {
+        if constexpr (FWD) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's stores and atomics landed
+            __syncthreads();
+            if (threadIdx.x == 0) s_ftm = ld_wt(a.tmax + t);
+            __syncthreads();
+            const bool refresh = (a.fwd_flags & DQRM_FWD_REFRESH_SCALE) != 0;
+            const bool fullp = (a.fwd_flags & DQRM_FWD_FULL_PRECISION) != 0;
+            const float sf = fullp ? 1.0f : (refresh ? sym_scale(s_ftm, a.fwd_bits) : a.fwd_scale[t]);
+            if (refresh && !fullp && threadIdx.x == 0) a.fwd_scale[t] = sf;
+            const float rf = 1.0f / sf;
+            const float qlo = -(float)(1 << (a.fwd_bits - 1)), qhi = (float)((1 << (a.fwd_bits - 1)) - 1);
+            float4 v[NPG];
+#pragma unroll
+            for (int k = 0; k < NPG; ++k) {  // every row load issued, clamped, then dropped if invalid
+                const int64_t x = nxr[k];
+                const bool ok = x >= 0 && x < nrows;
+                v[k] = nrows > 0 ? reinterpret_cast<const float4*>(a.W + (rb + (ok ? x : 0)) * D)[sub]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            float* outt = a.fwd_out + (int64_t)t * a.fwd_ost_t;
+#pragma unroll
+            for (int k = 0; k < NPG; ++k) {
+                const int i = grp + k * G;
+                if (i >= B) continue;
+                const bool ok = nxr[k] >= 0 && nxr[k] < nrows;
+                if (!ok && sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
+                float4 y = ok ? v[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (!fullp) {
+                    y.x = fake_quant(y.x, rf, qlo, qhi) * sf;
+                    y.y = fake_quant(y.y, rf, qlo, qhi) * sf;
+                    y.z = fake_quant(y.z, rf, qlo, qhi) * sf;
+                    y.w = fake_quant(y.w, rf, qlo, qhi) * sf;
+                }
+                reinterpret_cast<float4*>(outt + (int64_t)i * a.fwd_ost_b)[sub] = y;
+            }
+        }
+    };
     const float* dyt = a.dy + (int64_t)t * a.dst_t;
     float4 gv[DYF];
 #pragma unroll
@@ -3308,12 +3368,14 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             a.sblkmax[sbb] = r;
             a.tmax[t] = r;
         }
+        fwd_tail();
         DIAG_W(5);
         return;
     }
     const int64_t nblk = ceil_div(nrows, BLK);
     const int nq = s_n[0];
     if (nq == 0) {  // uniform: no block max holder shrank (the common case)
+        fwd_tail();
         DIAG_W(5);
         return;
     }
@@ -3370,6 +3432,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             a.tmax[t] = r;
         }
     }
+    fwd_tail();
     DIAG_W(5);
 }
 
@@ -3815,9 +3878,24 @@ struct BwdCall {
     void* ws;
     size_t ws_bytes;
     float div = 1.0f;
+    // MODE 0: the next batch's forward (dqrm_emb_bwd_sgd_fwd); taken inside k_sgd_small when it
+    // runs, else a dqrm_emb_fwd launch after the update
+    const dqrm_batch* next = nullptr;
+    int fwd_bits = 4;
+    uint32_t fwd_flags = 0;
+    float* fwd_out = nullptr;
+    int64_t fwd_ost_t = 0, fwd_ost_b = 0;
 };
 
 int64_t bwd_lookup_cap(const dqrm_batch* batch) { return batch->max_lookups > 0 ? batch->max_lookups : 1; }
+
+bool fused_sgd_fwd_on() {  // DQRM_FUSED_FWD=0: the next batch's forward as its own launch (A/B)
+    static const bool off = [] {
+        const char* e = getenv("DQRM_FUSED_FWD");
+        return e && !strcmp(e, "0");
+    }();
+    return !off;
+}
 
 template <int MODE>
 int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
@@ -3853,14 +3931,33 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
         const bool p1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
         const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float) +
                            (p1 ? (size_t)sg_hash_bytes((int)c.batch->num_bags) : 0);
+        // the next batch's forward inside the launch: a Criteo-form batch of the same size on
+        // the exact FP32 rows (the packed INT4 path stays a launch of its own)
+        const bool fwd = c.next && (c.next->flags & DQRM_BATCH_POOLING_ONE) && c.next->num_bags == c.batch->num_bags &&
+                         c.next->max_lookups >= c.next->num_bags && !(c.fwd_flags & DQRM_FWD_USE_PACKED) &&
+                         fused_sgd_fwd_on();
         bool fits = false;
-        DISPATCH_LPR(D, { fits = dyn + static_lds_bytes(k_sgd_small<LPR>) <= (size_t)LDS_PER_CU; });
+        DISPATCH_LPR(D, {
+            fits = dyn + (fwd ? static_lds_bytes(k_sgd_small<LPR, true>) : static_lds_bytes(k_sgd_small<LPR, false>)) <=
+                   (size_t)LDS_PER_CU;
+        });
         if (fits) {
+            if (fwd) {
+                fa.fwd_idx = c.next->idx; fa.fwd_out = c.fwd_out; fa.fwd_ost_t = c.fwd_ost_t; fa.fwd_ost_b = c.fwd_ost_b;
+                fa.fwd_scale = set->scale; fa.fwd_bits = c.fwd_bits; fa.fwd_flags = c.fwd_flags;
+            }
             DISPATCH_LPR(D, {
-                if ((rc = allow_lds(k_sgd_small<LPR>, dyn))) return rc;
-                hipLaunchKernelGGL(k_sgd_small<LPR>, dim3(T), dim3(SG_TPB), dyn, st, fa);
+                if (fwd) {
+                    if ((rc = allow_lds(k_sgd_small<LPR, true>, dyn))) return rc;
+                    hipLaunchKernelGGL((k_sgd_small<LPR, true>), dim3(T), dim3(SG_TPB), dyn, st, fa);
+                } else {
+                    if ((rc = allow_lds(k_sgd_small<LPR, false>, dyn))) return rc;
+                    hipLaunchKernelGGL((k_sgd_small<LPR, false>), dim3(T), dim3(SG_TPB), dyn, st, fa);
+                }
             });
             LAUNCH_CHECK();
+            if (c.next && !fwd)
+                return dqrm_emb_fwd(set, c.next, c.fwd_bits, c.fwd_flags, c.fwd_out, c.fwd_ost_t, c.fwd_ost_b, st);
             return DQRM_OK;
         }
     }
@@ -3869,7 +3966,9 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
         hipLaunchKernelGGL((k_bwd_fused<LPR, MODE>), dim3(T * SPLIT), dim3(FB_TPB), FB_LDS, st, fa);
     });
     LAUNCH_CHECK();  // MODE 0 / 2: the |W| hierarchy is finalized inside the launch
-    if (MODE != 1 && fa.fin_launch) return launch_finalize(set, st, true);
+    if (MODE != 1 && fa.fin_launch && (rc = launch_finalize(set, st, true))) return rc;
+    if (MODE == 0 && c.next)  // the next batch's forward as its own launch
+        return dqrm_emb_fwd(set, c.next, c.fwd_bits, c.fwd_flags, c.fwd_out, c.fwd_ost_t, c.fwd_ost_b, st);
     return DQRM_OK;
 }
 
@@ -4082,6 +4181,31 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch, const f
     c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
     c.lr = lr; c.repack = repack_bits == 4; c.ws = workspace; c.ws_bytes = workspace_bytes;
     return launch_bwd<0>(c, (hipStream_t)stream, "dqrm_emb_bwd_sgd");
+}
+
+int dqrm_emb_bwd_sgd_fwd(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                         int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, int repack_bits,
+                         void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                         uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b, void* stream) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_emb_bwd_sgd_fwd"))) return rc;
+    FwdArgs fa;  // the forward's arguments, validated as dqrm_emb_fwd validates them
+    if ((rc = fwd_args(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, "dqrm_emb_bwd_sgd_fwd", &fa)))
+        return rc;
+    if (!dy || (((uintptr_t)dy) & 15) || (dy_stride_t & 3) || (dy_stride_b & 3))
+        return set_error(DQRM_E_INVALID, "%s: dy must be 16-B aligned with strides %% 4 == 0", "dqrm_emb_bwd_sgd_fwd");
+    if (repack_bits && (repack_bits != 4 || !set->packed))
+        return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)", "dqrm_emb_bwd_sgd_fwd",
+                         repack_bits);
+    if (batch->num_bags <= 0)
+        return dqrm_emb_fwd(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, stream);
+    BwdCall c{};
+    c.set = set; c.batch = batch; c.dy = dy; c.dst_t = dy_stride_t; c.dst_b = dy_stride_b; c.ste = ste;
+    c.lr = lr; c.repack = repack_bits == 4; c.ws = workspace; c.ws_bytes = workspace_bytes;
+    c.next = next; c.fwd_bits = fwd_bits; c.fwd_flags = fwd_flags; c.fwd_out = out;
+    c.fwd_ost_t = out_stride_t; c.fwd_ost_b = out_stride_b;
+    return launch_bwd<0>(c, (hipStream_t)stream, "dqrm_emb_bwd_sgd_fwd");
 }
 
 int dqrm_rows_changed(const dqrm_table_set* set, const int64_t* rows, int64_t n, int repack_bits, void* stream) {

@@ -468,6 +468,29 @@ class EmbeddingTableSet:
             "dqrm_emb_bwd_sgd",
         )
 
+    def backward_sgd_forward(self, batch: LookupBatch, dy: torch.Tensor, lr: float, next_batch: LookupBatch,
+                             bits: int = 4, refresh_scale: bool = True, full_precision: bool = False,
+                             out: torch.Tensor | None = None, layout: str = "tbd", ste: bool = True,
+                             repack: bool = False, dy_layout: str = "tbd") -> torch.Tensor:
+        """backward_sgd(batch, dy, lr) followed by forward(next_batch): the single-GPU
+        driver's SGD step and its next apply_emb, adjacent in the loop, with the same results;
+        one launch for small batches (dqrm_emb_bwd_sgd_fwd). Returns the next batch's output."""
+        if next_batch.num_tables != self.T:
+            raise ValueError("batch has %d tables, set has %d" % (next_batch.num_tables, self.T))
+        B, T, D = next_batch.num_bags, self.T, self.D
+        if out is None:
+            out = torch.empty((T, B, D) if layout == "tbd" else (B, T, D), dtype=torch.float32, device=self.device)
+        ost, osb = (B * D, D) if layout == "tbd" else (D, T * D)
+        st, sb = self._dy_strides(dy, dy_layout, self.T, batch.num_bags, self.D)
+        L.check(
+            self.lib.dqrm_emb_bwd_sgd_fwd(
+                C.byref(self._c), C.byref(batch.c), _ptr(dy), st, sb, int(ste), float(lr), 4 if repack else 0,
+                *self._ws_args(batch), C.byref(next_batch.c), int(bits),
+                self._fwd_flags(refresh_scale, False, full_precision), _ptr(out), ost, osb, _stream_handle()),
+            "dqrm_emb_bwd_sgd_fwd",
+        )
+        return out
+
     def local_update(self, batch: LookupBatch, dy: torch.Tensor, lr: float, table_mask: torch.Tensor | None = None,
                      ste: bool = True, repack: bool = False, layout: str = "tbd") -> None:
         """W.add_(-lr * grad) with the rank's own uncoalesced gradient, product rounded, in

@@ -56,7 +56,8 @@ extern "C" {
                                8: dqrm_comm (RCCL communicator owned by libdqrm), dqrm_exchange
                                   (the N > 1 exchange as two calls), dqrm_emb_bwd_lookup_grad_presum;
                                9: dqrm_emb_bwd_apply_fwd_local (the next batch's forward behind the
-                                  one-launch update), dqrm_bwd_apply_fwd_local_is_one_launch */
+                                  one-launch update), dqrm_bwd_apply_fwd_local_is_one_launch,
+                                  dqrm_emb_bwd_sgd_fwd */
 
 /* status codes */
 #define DQRM_OK            0
@@ -197,6 +198,21 @@ int dqrm_emb_bwd_sgd(const dqrm_table_set* set, const dqrm_batch* batch,
                      const float* dy, int64_t dy_stride_t, int64_t dy_stride_b,
                      int ste, float lr, int repack_bits, void* workspace, size_t workspace_bytes,
                      void* stream);
+
+/* dqrm_emb_bwd_sgd on `batch`, then dqrm_emb_fwd(set, next, fwd_bits, fwd_flags, out, ...) on
+ * the NEXT batch, with the same results as the two calls: the single-GPU driver's SGD step
+ * (dlrm_s_pytorch_single_gpu.py:1943-1950) and the next apply_emb (:609-674), adjacent in its
+ * loop. When the update takes the small-batch kernel (one workgroup per table, B <= 512
+ * lookups) and `next` is a Criteo-form batch of the same size without DQRM_FWD_USE_PACKED,
+ * each table's workgroup runs the next forward of that table itself right after its update:
+ * one launch per step. Otherwise the two calls run. (A table whose batch overflows the
+ * declared max_lookups is skipped and flagged, DQRM_ERRF_OVERFLOW, by the update and, in the
+ * one-launch form, by its forward too.) */
+int dqrm_emb_bwd_sgd_fwd(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy,
+                         int64_t dy_stride_t, int64_t dy_stride_b, int ste, float lr, int repack_bits,
+                         void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                         uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                         void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Data-parallel gradient path (sgd_quantized_gradients_parallel_comm.py)

@@ -84,6 +84,8 @@ def test_fused_next_forward_rejects_bad_arguments_without_device(lib):
     assert lib.dqrm_emb_bwd_apply_fwd_local(*args, None, 4, 0, None, 0, 0, None) == L.DQRM_E_INVALID
     assert b"dim" in lib.dqrm_last_error()
     assert lib.dqrm_bwd_apply_fwd_local_is_one_launch(None, None, None, 0, None) == L.DQRM_E_INVALID
+    assert lib.dqrm_emb_bwd_sgd_fwd(C.byref(ts), None, None, 0, 0, 1, 0.1, 0, None, 0, None, 4, 0, None, 0, 0,
+                                    None) == L.DQRM_E_INVALID
 
 
 def test_apply_kernel_selector(lib):

@@ -93,6 +93,9 @@ def test_phase_names(bench):
     assert bench.alg_bytes("bwd_apply_fwd_local", T, B, D, U) == (bench.alg_bytes("bwd_apply_local", T, B, D, U)
                                                                   + bench.alg_bytes("emb_fwd", T, B, D, U))
     assert "bwd_apply_fwd_local" in bench.KERNEL_SYMBOL
+    assert bench.phase_names("sgd", False, True, False, True) == ["bwd_sgd_fwd"]
+    assert bench.alg_bytes("bwd_sgd_fwd", T, B, D, U) == (bench.alg_bytes("bwd_sgd", T, B, D, U)
+                                                          + bench.alg_bytes("emb_fwd", T, B, D, U))
 
 
 @pytest.mark.parametrize("mode", ["dp", "sgd", "fwd"])

@@ -1013,3 +1013,38 @@ def test_fused_next_forward_packed_falls_back(dq):
     y1 = sets[1].forward(nb)
     assert torch.equal(y0, y1)
     assert torch.equal(sets[0].W, sets[1].W)
+
+
+@pytest.mark.parametrize("D,B,dist,form,refresh", [(16, 128, "uniform", "criteo", True), (16, 128, "zipf", "criteo", False),
+                                                  (32, 512, "zipf", "criteo", True), (16, 200, "uniform", "bags", True),
+                                                  (16, 2048, "uniform", "criteo", True)])
+def test_fused_sgd_next_forward_matches_separate_calls(dq, D, B, dist, form, refresh):
+    """dqrm_emb_bwd_sgd_fwd -- the single-GPU SGD step with the next batch's forward in the
+    same launch (k_sgd_small's workgroup holds its whole table, so the table max is final at
+    its end) -- against dqrm_emb_bwd_sgd + dqrm_emb_fwd on a copy, bit for bit over four steps:
+    outputs, scale, W and the |W| hierarchy; Kaggle-shaped tables (3 ... 20 000 rows), the
+    Criteo form and bags (the update) with Criteo-form next batches, an out-of-range index in a
+    next batch; B = 2048 takes the general kernel and the two calls."""
+    rows = [min(n, 20000) for n in G.KAGGLE_ROWS]
+    T = len(rows)
+    sets = [dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=171) for _ in range(2)]
+    Ps = [G.pooling_one(rows, B, 181 + k, dist=dist) for k in range(5)]
+    Ps[2][3, 5] = rows[3]  # out of range in the forward of step 1's next batch
+    nbs = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+    if form == "bags":
+        bags = [G.random_bags(rows, B, 190 + k, num_indices_per_lookup=3) for k in range(4)]
+        ubs = [to_batch(dq, idx, off) for idx, off in bags]
+    else:
+        ubs = nbs[:4]
+    kw = dict(refresh_scale=refresh)
+    ys = [ts.forward(nbs[0]) for ts in sets]  # (sets the scales a held-scale forward uses)
+    for it in range(4):
+        dy = torch.from_numpy(G.upstream_grad(T, B, D, 201 + it) * 30).cuda()
+        y0 = sets[0].backward_sgd_forward(ubs[it], dy, 0.5, nbs[it + 1], **kw)
+        sets[1].backward_sgd(ubs[it], dy, 0.5)
+        y1 = sets[1].forward(nbs[it + 1], **kw)
+        errs = [ts.read_errors() for ts in sets]
+        assert errs[0] == errs[1], (it, errs)
+        assert torch.equal(y0, y1), it
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
