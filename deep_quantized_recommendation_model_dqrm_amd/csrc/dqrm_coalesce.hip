@@ -1850,7 +1850,14 @@ void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la) {
         nb[t] = (num_rows_host[t] + BLK - 1) / BLK;
         if (nb[t] >= 2 * SPLIT) order[ne++] = t;
     }
-    std::stable_sort(order, order + ne, [&](int x, int y) { return nb[x] > nb[y]; });
+    // DQRM_SUBSLOT_ORDER=small (A/B): the smallest eligible tables first (their slots hold
+    // duplicate-heavy lookups: sort, ordered sums, block re-reductions), not the largest
+    static const bool small_first = [] {
+        const char* e = getenv("DQRM_SUBSLOT_ORDER");
+        return e && !strcmp(e, "small");
+    }();
+    if (small_first) std::stable_sort(order, order + ne, [&](int x, int y) { return nb[x] < nb[y]; });
+    else std::stable_sort(order, order + ne, [&](int x, int y) { return nb[x] > nb[y]; });
     for (int e = 0; e < nextra && e < ne && e < kSubTables; ++e) {
         la->sub_table[e] = (int8_t)order[e];
         la->sub_mask |= 1u << order[e];
