@@ -447,6 +447,9 @@ __device__ __forceinline__ float chain_sum_rm(const float* c, int p, int pe, int
 #ifndef DQRM_COAL_WPF
 #define DQRM_COAL_WPF 4
 #endif
+#ifndef DQRM_FWD_EARLY_IDX
+#define DQRM_FWD_EARLY_IDX 0
+#endif
 #ifndef DQRM_COAL_WLATE
 #define DQRM_COAL_WLATE 0  // 1: an A/B build issuing the W prefetch after the land phase
 #endif
@@ -1410,6 +1413,16 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     if constexpr (APPLY) {
         __syncthreads();
         CDIAG(11);
+        // (A/B DQRM_FWD_EARLY_IDX=1: the fused forward's next-batch indices issued here, in
+        // flight across the update, instead of after the arrival)
+        int64_t nxe[(FWD && DQRM_FWD_EARLY_IDX) ? MAXI : 1];
+        if constexpr (FWD && DQRM_FWD_EARLY_IDX) {
+#pragma unroll
+            for (int i = 0; i < MAXI; ++i) {
+                const int b = tid + TPB * i;
+                nxe[i] = b < B ? la.fwd_idx[(int64_t)t * B + b] : -1;
+            }
+        }
         CDIAG_W(16);  // (diagnostic build: every load of the workgroup landed, the W prefetch included)
         // the update of dqrm_apply_local: s = clamp(max|g|, 1e-8) / (2^(bits-1)-1) (* 1/N,
         // N = 1), q = clamp(round(g/s)), W += -lr * ((q * 1) * s)
@@ -1697,7 +1710,8 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
 #pragma unroll
             for (int i = 0; i < MAXI; ++i) {
                 const int b = tid + TPB * i;
-                nx[i] = b < B ? la.fwd_idx[(int64_t)t * B + b] : -1;
+                if constexpr (DQRM_FWD_EARLY_IDX) nx[i] = nxe[i];
+                else nx[i] = b < B ? la.fwd_idx[(int64_t)t * B + b] : -1;
             }
             const int me = s + SPLIT * j;
             const uint32_t smask = s_lastarr ? (uint32_t)s_stallmask : 0u;
