@@ -24,3 +24,5 @@ done
 done
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${T}_driver.log 2>&1 || { tail -n 20 gpurun_out/${T}_driver.log; exit 1; }
 tail -n 1 gpurun_out/${T}_driver.log | cut -c1-400
+timeout -k 10 300 python -u tools/diag_coalesce.py terabyte 2048 applyfwd > gpurun_out/${T}_phase_tb_applyfwd.txt 2>&1 || { tail -n 20 gpurun_out/${T}_phase_tb_applyfwd.txt; exit 1; }
+head -n 3 gpurun_out/${T}_phase_tb_applyfwd.txt; tail -n 30 gpurun_out/${T}_phase_tb_applyfwd.txt
