@@ -1015,10 +1015,12 @@ def test_fused_next_forward_packed_falls_back(dq):
     assert torch.equal(sets[0].W, sets[1].W)
 
 
-@pytest.mark.parametrize("D,B,dist,form,refresh", [(16, 128, "uniform", "criteo", True), (16, 128, "zipf", "criteo", False),
-                                                  (32, 512, "zipf", "criteo", True), (16, 200, "uniform", "bags", True),
-                                                  (16, 2048, "uniform", "criteo", True)])
-def test_fused_sgd_next_forward_matches_separate_calls(dq, D, B, dist, form, refresh):
+@pytest.mark.parametrize("D,B,dist,form,refresh,full,layout",
+                         [(16, 128, "uniform", "criteo", True, False, "tbd"), (16, 128, "zipf", "criteo", False, False, "tbd"),
+                          (32, 512, "zipf", "criteo", True, False, "btd"), (16, 200, "uniform", "bags", True, False, "tbd"),
+                          (64, 64, "uniform", "criteo", True, True, "btd"), (4, 256, "zipf", "criteo", True, False, "tbd"),
+                          (16, 2048, "uniform", "criteo", True, False, "tbd")])
+def test_fused_sgd_next_forward_matches_separate_calls(dq, D, B, dist, form, refresh, full, layout):
     """dqrm_emb_bwd_sgd_fwd -- the single-GPU SGD step with the next batch's forward in the
     same launch (k_sgd_small's workgroup holds its whole table, so the table max is final at
     its end) -- against dqrm_emb_bwd_sgd + dqrm_emb_fwd on a copy, bit for bit over four steps:
@@ -1036,12 +1038,12 @@ def test_fused_sgd_next_forward_matches_separate_calls(dq, D, B, dist, form, ref
         ubs = [to_batch(dq, idx, off) for idx, off in bags]
     else:
         ubs = nbs[:4]
-    kw = dict(refresh_scale=refresh)
+    kw = dict(refresh_scale=refresh, full_precision=full, layout=layout)
     ys = [ts.forward(nbs[0]) for ts in sets]  # (sets the scales a held-scale forward uses)
     for it in range(4):
         dy = torch.from_numpy(G.upstream_grad(T, B, D, 201 + it) * 30).cuda()
-        y0 = sets[0].backward_sgd_forward(ubs[it], dy, 0.5, nbs[it + 1], **kw)
-        sets[1].backward_sgd(ubs[it], dy, 0.5)
+        y0 = sets[0].backward_sgd_forward(ubs[it], dy, 0.5, nbs[it + 1], ste=not full, **kw)
+        sets[1].backward_sgd(ubs[it], dy, 0.5, ste=not full)
         y1 = sets[1].forward(nbs[it + 1], **kw)
         errs = [ts.read_errors() for ts in sets]
         assert errs[0] == errs[1], (it, errs)
