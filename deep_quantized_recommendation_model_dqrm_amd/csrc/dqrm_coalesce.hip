@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
     // are blocks (t/8)*64 + s*8 + t%8. A dimension-split table's slots read 32-B slices of
     // the same dy lines; on one XCD a line is fetched from HBM once, not once per slot.
     const int grp = (int)(blockIdx.x >> 6) * 8 + (int)(blockIdx.x & 7), s = (int)(blockIdx.x >> 3) & 7;
-    int t = grp, j = 0;
+    int t = (APPLY && la.group_perm && grp < a.T) ? (int)la.table_of_group[grp] : grp, j = 0;
     if (grp >= a.T) {  // a spare group: sub-slot 1 of a big table's slots, or idle
         const int e = grp - a.T;
         if (!APPLY || e >= dqrm_internal::kSubTables || la.sub_table[e] < 0) return;
@@ -1846,6 +1846,8 @@ namespace dqrm_internal {
 
 int coalesce_apply_grid(int T) { return (T + 7) / 8 * 64; }
 
+void plan_table_groups(const int64_t* num_rows_host, int T, LocalApplyArgs* la);
+
 void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la) {
     static const bool off = [] {
         const char* e = getenv("DQRM_SUBSLOTS");
@@ -1876,6 +1878,33 @@ void plan_sub_slots(const int64_t* num_rows_host, int T, LocalApplyArgs* la) {
         la->sub_table[e] = (int8_t)order[e];
         la->sub_mask |= 1u << order[e];
     }
+    plan_table_groups(num_rows_host, T, la);
+}
+
+// DQRM_TABLE_GROUPS=critical (A/B): the groups a table's 8 slots run in, XCD by XCD (group g's
+// workgroups share XCD g % 8), filled with the tables expected to end last first -- uneven
+// row-split slots (8 < blocks < 16, not a multiple of 8), then a few-row tables' long ordered
+// chains, then medium tables, the big distinct-row tables last
+void plan_table_groups(const int64_t* num_rows_host, int T, LocalApplyArgs* la) {
+    static const bool crit = [] {
+        const char* e = getenv("DQRM_TABLE_GROUPS");
+        return e && !strcmp(e, "critical");
+    }();
+    la->group_perm = 0;
+    for (int g = 0; g < kSubTables; ++g) la->table_of_group[g] = (int8_t)g;
+    if (!crit || !num_rows_host || T <= 0 || T > kCoalesceApplyMaxT) return;
+    int score[kCoalesceApplyMaxT], tabs[kCoalesceApplyMaxT], groups[kCoalesceApplyMaxT];
+    for (int t = 0; t < T; ++t) {
+        const int64_t n = num_rows_host[t], nb = (n + BLK - 1) / BLK;
+        score[t] = n >= (1 << 20) ? 0 : (nb > SPLIT && nb < 2 * SPLIT && nb % SPLIT) ? 3 : (nb < SPLIT && n <= 64) ? 2 : 1;
+        tabs[t] = t;
+    }
+    std::stable_sort(tabs, tabs + T, [&](int x, int y) { return score[x] > score[y]; });
+    int ng = 0;
+    for (int x = 0; x < SPLIT; ++x)
+        for (int g = x; g < T; g += SPLIT) groups[ng++] = g;
+    for (int i = 0; i < T; ++i) la->table_of_group[groups[i]] = (int8_t)tabs[i];
+    la->group_perm = 1;
 }
 
 bool coalesce_apply_resident(int T, hipStream_t stream) {

@@ -52,6 +52,10 @@ struct LocalApplyArgs {
     // (-1: idle); bit t of sub_mask = table t's slots are halved between two workgroups
     uint32_t sub_mask;
     int8_t sub_table[32];
+    // group g < T serves table table_of_group[g] when group_perm (host-planned, A/B
+    // DQRM_TABLE_GROUPS=critical: the tables expected to end last on the XCDs dealt first)
+    int8_t table_of_group[32];
+    int group_perm;
     // rendezvous polls before a workgroup gives up (DQRM_ERRF_STALL; its rows are then applied
     // by the table's last-arriving workgroup); the host sets it (DQRM_STALL_SPIN, default 2^20)
     uint32_t spin_limit;
