@@ -4651,7 +4651,9 @@ static int bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, c
         return set_error(DQRM_E_INVALID, "%s: repack needs packed rows and bits == 4 (got %d)",
                          "dqrm_emb_bwd_apply_local", repack_bits);
     if (apply_local_one_launch(set, batch, stream)) {
-        if (batch->num_bags <= 0) return DQRM_OK;
+        if (batch->num_bags <= 0)  // nothing to update; the next batch's forward still runs
+            return ff ? dqrm_emb_fwd(set, ff->next, ff->bits, ff->flags, ff->out, ff->ost_t, ff->ost_b, stream)
+                      : DQRM_OK;
         dqrm_internal::CoalesceArgs ca{};
         ca.meta = set->meta; ca.T = set->num_tables; ca.D = set->dim; ca.B = batch->num_bags; ca.idx = batch->idx;
         ca.dy = dy; ca.dst_t = dy_stride_t; ca.dst_b = dy_stride_b; ca.scale = set->scale; ca.ste = ste;

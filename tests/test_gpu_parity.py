@@ -1015,6 +1015,42 @@ def test_fused_next_forward_packed_falls_back(dq):
     assert torch.equal(sets[0].W, sets[1].W)
 
 
+def test_fused_next_forward_empty_update_still_forwards(dq):
+    """An empty batch to update (no bags) leaves the tables alone, and the next batch's
+    forward still runs and equals dqrm_emb_fwd (called through the C ABI: the Python wrapper
+    has no empty dy to pass)."""
+    import ctypes as C
+    from deep_quantized_recommendation_model_dqrm_amd import tables as TB
+
+    rows, D, B = COAL_ROWS, 64, 2048
+    T = len(rows)
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=9)
+    nb = dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, B, 4)).cuda())
+    # zero bags over valid pointers (a Python batch of zero bags has none to give)
+    empty = TB.L.Batch(TB._ptr(nb.idx), TB._ptr(nb.off), TB._ptr(nb.idx_base), 0, 0, TB.L.DQRM_BATCH_POOLING_ONE, 0)
+    W0 = ts.W.clone()
+    ws = dq.CoalescedGrad.allocate(rows, B, D, "cuda")
+    s_avg = torch.zeros(T, dtype=torch.float32, device="cuda")
+    dy = torch.zeros(64, dtype=torch.float32, device="cuda")  # any valid pointer: no bags read it
+    out = torch.full((T, B, D), 7.0, dtype=torch.float32, device="cuda")
+    rc = ts.lib.dqrm_emb_bwd_apply_fwd_local(
+        C.byref(ts._c), C.byref(empty), TB._ptr(dy), 0, D, 1, TB._ptr(ws.slot_cap_base), ws.cap_total,
+        TB._ptr(ws.rows), TB._ptr(ws.vals), TB._ptr(ws.ucount), TB._ptr(ws.absmax), 8, TB._ptr(s_avg), 0.5, 0,
+        *ts._ws_args(nb), C.byref(nb.c), 4, ts._fwd_flags(True, False, False), TB._ptr(out), B * D, D,
+        TB._stream_handle())
+    assert rc == 0
+    assert ts.read_errors() == 0
+    assert torch.equal(ts.W, W0)
+    assert torch.equal(out, ts.forward(nb))
+    out.fill_(7.0)  # and the SGD form (dqrm_emb_bwd_sgd_fwd)
+    rc = ts.lib.dqrm_emb_bwd_sgd_fwd(
+        C.byref(ts._c), C.byref(empty), TB._ptr(dy), 0, D, 1, 0.5, 0, *ts._ws_args(nb), C.byref(nb.c), 4,
+        ts._fwd_flags(True, False, False), TB._ptr(out), B * D, D, TB._stream_handle())
+    assert rc == 0
+    assert torch.equal(ts.W, W0)
+    assert torch.equal(out, ts.forward(nb))
+
+
 @pytest.mark.parametrize("D,B,dist,form,refresh,full,layout",
                          [(16, 128, "uniform", "criteo", True, False, "tbd"), (16, 128, "zipf", "criteo", False, False, "tbd"),
                           (32, 512, "zipf", "criteo", True, False, "btd"), (16, 200, "uniform", "bags", True, False, "tbd"),
