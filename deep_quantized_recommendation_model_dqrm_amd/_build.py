@@ -54,10 +54,10 @@ def needs_build() -> bool:
     return _stale(LIB_PATH, [*SOURCES, HEADER, INTERNAL_HEADER, DEVICE_HEADER, __file__])
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
+def build(force: bool = False, verbose: bool = True, relink: bool = False) -> str:
     """Compile csrc/*.hip (one object per translation unit, rebuilt when stale) and link
-    libdqrm.so next to this file."""
-    if not force and not needs_build():
+    libdqrm.so next to this file. relink: link even when nothing is stale."""
+    if not force and not relink and not needs_build():
         return LIB_PATH
     objs, jobs = [], []
     for src in SOURCES:  # translation units compile in parallel (one hipcc each)
