@@ -109,6 +109,11 @@ def parse(argv=None):
                    help="run the N>1 exchange (two all-gathers, quantize-pack, payload apply; the MLP "
                         "exchange's collectives) through the process group at world size 1 too: the RCCL leg "
                         "on a one-GPU box")
+    p.add_argument("--comm", default="rccl", choices=["rccl", "torch", "python"],
+                   help="N > 1 (or forced) exchange transport: rccl = libdqrm issues both all-gathers on its own "
+                        "RCCL communicator between the kernels (falls back to torch if RCCL cannot be set up); "
+                        "torch = the same C step with torch.distributed serving the all-gathers; python = the "
+                        "kernels and collectives issued one by one from Python (A/B)")
     p.add_argument("--separate-forward", action="store_true",
                    help="N=1 one-launch step: the forward as its own launch (dqrm_emb_fwd) instead of inside "
                         "the previous step's update launch (dqrm_emb_bwd_apply_fwd_local)")
@@ -278,7 +283,9 @@ def main():
     batches = make_batches(rows, B_global, rank, world, a.num_batches, a.seed, a.index_dist, dev)
     dy = torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + rank)) * 0.05
     y = torch.empty(T, B, D, device=dev)
-    ex = (dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits, force_collectives=a.force_collectives)
+    comm = a.comm if a.dist_backend == "nccl" or a.comm != "rccl" else "torch"
+    ex = (dq.SparseGradExchange(ts, B, grad_bits=a.grad_bits, force_collectives=a.force_collectives,
+                                transport=comm if coll else None)
           if a.mode == "dp" else None)
     if a.use_packed:
         ts.refresh_scale_and_pack(4)
@@ -300,7 +307,7 @@ def main():
     # the same for the single-GPU SGD step (dqrm_emb_bwd_sgd_fwd: one launch when the small-batch
     # kernel takes the update, config 3)
     if a.mode == "sgd" and not a.use_packed and not a.separate_forward and len(batches) > 1:
-        next_fwd = True
+        next_fwd = ts.sgd_fwd_is_one_launch(batches[0], batches[1])  # else the forward as its own phase
     names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd)
 
     # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
@@ -528,8 +535,9 @@ def main():
         colls = None
         if a.mode == "dp":
             colls = {"world_size": world, "backend": a.dist_backend if coll else None,
-                     "issued_by": ("libdqrm (dqrm_comm: RCCL ncclAllGather between the step's kernels)"
-                                   if lib_exchange else "torch.distributed" if coll else None),
+                     "issued_by": ({"rccl": "libdqrm (dqrm_comm: RCCL ncclAllGather between the step's kernels)",
+                                    "torch": "libdqrm's exchange, all-gathers served by torch.distributed",
+                                    "python": "torch.distributed"}.get(ex.transport) if coll else None),
                     "per_step": 2 if coll else 0,
                     "scale_allgather_bytes_per_rank": ex.ws.absmax.numel() * 4,
                     "payload_allgather_bytes_per_rank": int(ex.payload_bytes)}

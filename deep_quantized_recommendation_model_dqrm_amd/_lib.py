@@ -52,7 +52,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 9  # include/dqrm.h
+DQRM_ABI_VERSION = 10  # include/dqrm.h
 DQRM_PRESUM_MAX_LOOKUPS = 2048
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
@@ -81,6 +81,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_bwd_apply_fwd_local",
     "dqrm_bwd_apply_fwd_local_is_one_launch",
     "dqrm_emb_bwd_sgd_fwd",
+    "dqrm_bwd_sgd_fwd_is_one_launch",
     "dqrm_dense_wire_type",
     "dqrm_dense_grad_scale",
     "dqrm_dense_grad_quant",
@@ -95,7 +96,9 @@ EXPORTED_SYMBOLS = (
     "dqrm_replica_mean",
     "dqrm_comm_unique_id",
     "dqrm_comm_init",
+    "dqrm_comm_init_external",
     "dqrm_comm_destroy",
+    "dqrm_comm_size",
     "dqrm_comm_allgather",
     "dqrm_exchange_grad",
     "dqrm_exchange_apply",
@@ -108,6 +111,9 @@ EXPORTED_SYMBOLS = (
 )
 
 c_i64p = C.c_void_p  # device pointers are passed as integers
+
+# dqrm_allgather_fn: int (*)(const void* send, void* recv, size_t bytes, void* stream, void* user)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p)
 
 
 class TableSet(C.Structure):
@@ -284,6 +290,7 @@ def load(path: str | None = None) -> C.CDLL:
             [TS, BA, P, C.c_int64, C.c_int64, C.c_int, C.c_float, C.c_int, P, C.c_size_t, BA, C.c_int, C.c_uint32,
              P, C.c_int64, C.c_int64, P],
         ),
+        "dqrm_bwd_sgd_fwd_is_one_launch": (C.c_int, [TS, BA, BA, C.c_uint32]),
         "dqrm_dense_wire_type": (C.c_int, [C.c_int, C.c_int]),
         "dqrm_dense_grad_scale": (C.c_int, [DS, C.c_int, P, P]),
         "dqrm_dense_grad_quant": (C.c_int, [DS, C.c_int, P, C.c_int, P, C.c_int, P, P]),
@@ -301,7 +308,9 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_replica_mean": (C.c_int, [P, C.c_int64, C.c_int, C.c_float, P]),
         "dqrm_comm_unique_id": (C.c_int, [P]),
         "dqrm_comm_init": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, P]),
+        "dqrm_comm_init_external": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, ALLGATHER_FN, P]),
         "dqrm_comm_destroy": (C.c_int, [P]),
+        "dqrm_comm_size": (C.c_int, [P]),
         "dqrm_comm_allgather": (C.c_int, [P, P, P, C.c_size_t, P]),
         "dqrm_exchange_grad": (C.c_int, [C.POINTER(Exchange), BA, P, C.c_int64, C.c_int64, C.c_int, P]),
         "dqrm_exchange_apply": (C.c_int, [C.POINTER(Exchange), C.c_float, C.c_int, C.c_int, P]),

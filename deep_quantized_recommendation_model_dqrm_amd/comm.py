@@ -157,15 +157,18 @@ class DqrmComm:
     group: rank 0 draws RCCL's unique id, the group broadcasts it, every rank joins
     (ncclCommInitRank, collective). The exchange then issues its two all-gathers from C, on
     the compute stream between its kernels (dqrm_exchange_grad): no Python or c10d work per
-    collective. One per (group, device), shared by every exchange on that group; released at
-    exit or by close()."""
+    collective. One per (group, world size, rank, device), shared by every exchange on that
+    group; released by close() / close_all() (registered at exit), and dropped from the cache
+    when its group is no longer the live one of that key (destroy_process_group + re-init)."""
 
     _cache: dict = {}
+    _atexit = False
 
     def __init__(self, group=None, device=None):
         self.lib = L.load()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.group = group
         dev = torch.device(device if device is not None else "cuda")
         idbuf = torch.zeros(128, dtype=torch.uint8)
         if self.rank == 0:
@@ -182,12 +185,28 @@ class DqrmComm:
             L.check(self.lib.dqrm_comm_init(C.byref(h), self.world, self.rank, idbuf.data_ptr()), "dqrm_comm_init")
         self.handle = h
 
+    @staticmethod
+    def _key(group, device):
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        return (id(pg), dist.get_world_size(group), dist.get_rank(group), str(device))
+
     @classmethod
     def get(cls, group=None, device=None) -> "DqrmComm":
-        key = (id(group), str(device))
+        if not cls._atexit:
+            import atexit
+
+            atexit.register(cls.close_all)
+            cls._atexit = True
+        key = cls._key(group, device)
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
         c = cls._cache.get(key)
-        if c is None or c.handle is None:
-            c = cls._cache[key] = cls(group, device)
+        if c is not None and (c.handle is None or c._pg is not pg):  # a stale entry (group re-created)
+            c.close()
+            c = None
+        if c is None:
+            c = cls(group, device)
+            c._pg = pg
+            cls._cache[key] = c
         return c
 
     def close(self) -> None:
@@ -202,13 +221,91 @@ class DqrmComm:
         cls._cache.clear()
 
 
+class TorchServedComm:
+    """A dqrm_comm whose all-gathers torch.distributed serves (dqrm_comm_init_external): the
+    exchange's C orchestration (dqrm_exchange_grad / _apply: coalesce, all-gather of the
+    maxima, quantize-pack, all-gather of the payloads, apply) is the one the RCCL communicator
+    runs, and each of its two all-gathers calls back here with the device buffers and the
+    stream; they are gathered with all_gather_into over the process group (nccl: c10d's own
+    RCCL communicator; gloo: staged through host memory -- the reference's Gloo transport).
+    One per exchange: the callback maps the exchange's (send, recv) pointers to its tensors."""
+
+    def __init__(self, group, world: int, buffers):
+        self.lib = L.load()
+        self.group, self.world = group, world
+        self.rank = dist.get_rank(group)
+        self._bufs = {(inp.data_ptr(), out.data_ptr()): (inp, out) for inp, out in buffers}
+        self.exc = None
+        self.calls = 0
+
+        def _gather(send, recv, nbytes, stream, user):  # called by libdqrm on this thread
+            try:
+                inp, out = self._bufs[(send or 0, recv or 0)]
+                if inp.numel() * inp.element_size() != nbytes or out.numel() != self.world * inp.numel():
+                    raise ValueError(f"all-gather of {nbytes} bytes does not match the registered buffers")
+                all_gather_into(out, inp, self.group, self.world, force=True)
+                self.calls += 1
+                return 0
+            except BaseException as e:  # noqa: BLE001 -- re-raised by check() after the C call
+                self.exc = e
+                return 1
+
+        self._fn = L.ALLGATHER_FN(_gather)  # kept alive as long as the communicator
+        h = C.c_void_p()
+        L.check(self.lib.dqrm_comm_init_external(C.byref(h), world, self.rank, self._fn, None),
+                "dqrm_comm_init_external")
+        self.handle = h
+
+    def check(self, rc: int, what: str) -> None:
+        if rc != L.DQRM_OK and self.exc is not None:
+            e, self.exc = self.exc, None
+            raise L.DQRMError(f"{what}: the torch.distributed all-gather failed: {e!r}") from e
+        L.check(rc, what)
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None:
+            self.lib.dqrm_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+TRANSPORTS = ("rccl", "torch", "python")
+
+
+def exchange_transport(group=None, world: int | None = None) -> str:
+    """How an exchange over `group` runs its N > 1 step (also forced at world size 1):
+      rccl    libdqrm's C orchestration on its own RCCL communicator (DqrmComm): both
+              all-gathers issued from C between the kernels (nccl backend only);
+      torch   the same C orchestration, the all-gathers served by torch.distributed through
+              a callback (TorchServedComm: c10d's communicator, or Gloo staged via host);
+      python  the kernels and all-gathers issued one by one from Python (round-4 form, A/B).
+    DQRM_C_COMM=rccl|torch|python (0 = python) overrides. Default: rccl at world size 1 on nccl
+    (the forced N > 1 path on a one-GPU box, the library's measured form), torch otherwise --
+    with several ranks the drop-in hooks keep c10d's one RCCL communicator, which also carries
+    the MLP's all-reduces (bench.py selects rccl explicitly: --comm)."""
+    env = os.environ.get("DQRM_C_COMM", "").strip().lower()
+    if env in ("0", "python"):
+        return "python"
+    if not (dist.is_available() and dist.is_initialized()):
+        return "python"
+    nccl = dist.get_backend(group) == "nccl"
+    if env in ("rccl", "1"):
+        return "rccl" if nccl else "torch"
+    if env == "torch":
+        return "torch"
+    w = world if world is not None else dist.get_world_size(group)
+    return "rccl" if nccl and w == 1 else "torch"
+
+
 def use_library_collectives(group=None) -> bool:
-    """Whether an exchange over `group` issues its collectives from libdqrm (RCCL, nccl
-    backend) rather than through torch.distributed (gloo: host-staged rehearsal). DQRM_C_COMM=0
-    forces the torch.distributed path (A/B)."""
-    if os.environ.get("DQRM_C_COMM", "1") == "0":
-        return False
-    return dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"
+    """Whether an exchange over `group` issues its collectives from libdqrm's own RCCL
+    communicator (exchange_transport(group) == "rccl")."""
+    return exchange_transport(group) == "rccl"
 
 
 class SparseGradExchange:
@@ -223,11 +320,15 @@ class SparseGradExchange:
 
     def __init__(self, tables: EmbeddingTableSet, max_lookups: int, grad_bits: int = 8, group=None,
                  kernels: ExchangeKernels | None = None, device=None, absmax_buf: torch.Tensor | None = None,
-                 payload_buf: torch.Tensor | None = None, force_collectives: bool = False):
+                 payload_buf: torch.Tensor | None = None, force_collectives: bool = False,
+                 transport: str | None = None):
         """absmax_buf / payload_buf: caller-owned slices of buffers several sets gather
         together (MultiSetExchange); the per-set gather buffers are then not allocated.
         force_collectives: run the N > 1 step (both all-gathers, quantize-pack, payload
-        decode) at world size 1 too, through the process group's backend."""
+        decode) at world size 1 too, through the process group's backend.
+        transport: "rccl" | "torch" | "python" (exchange_transport; None = its default). An
+        "rccl" communicator that cannot be created falls back to "torch" (self.transport says
+        which runs)."""
         if not (grad_bits == 32 or 2 <= grad_bits <= 16):
             raise ValueError("grad_bits must be 2..16 or 32")
         self.tables = tables
@@ -262,13 +363,32 @@ class SparseGradExchange:
                                                           device=dev)
         self.gathered = None if shared else torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8,
                                                         device=dev)
-        # the library-issued step (dqrm_exchange_grad / _apply): RCCL collectives from C on a
-        # dqrm_comm, two host calls per step; only with the HIP kernels and unshared buffers
+        # the library-issued step (dqrm_exchange_grad / _apply): two host calls per step, the
+        # collectives from C on a dqrm_comm (libdqrm's RCCL communicator, or torch.distributed
+        # through a callback); only with the HIP kernels and unshared buffers
         self._x = None
-        if (self.coll and not shared and isinstance(self.kernels, HipExchangeKernels)
-                and use_library_collectives(group)):
-            self.dcomm = DqrmComm.get(group, dev)
-            self._x = self._make_exchange(self.dcomm.handle)
+        self.dcomm = None
+        self.transport = "local" if not self.coll else "python"
+        if self.coll and not shared and isinstance(self.kernels, HipExchangeKernels):
+            tr = transport if transport is not None else exchange_transport(group, self.world)
+            if tr not in TRANSPORTS:
+                raise ValueError(f"transport must be one of {TRANSPORTS}")
+            if tr == "rccl" and dist.get_backend(group) != "nccl":
+                raise ValueError("the rccl transport needs the nccl backend")
+            if tr == "rccl":
+                try:
+                    self.dcomm = DqrmComm.get(group, dev)
+                except L.DQRMError as e:  # e.g. RCCL missing: the same C step over torch.distributed
+                    import warnings
+
+                    warnings.warn(f"libdqrm's RCCL communicator is unavailable ({e}); using torch.distributed")
+                    tr = "torch"
+            if tr == "torch":
+                self.dcomm = TorchServedComm(group, self.world, [(self.ws.absmax, self.absmax_all),
+                                                                 (self.payload, self.gathered)])
+            self.transport = tr
+            if self.dcomm is not None:
+                self._x = self._make_exchange(self.dcomm.handle)
 
     def _make_exchange(self, comm_handle) -> "L.Exchange":
         x = L.Exchange()
@@ -287,6 +407,12 @@ class SparseGradExchange:
         x.workspace, x.workspace_bytes = w.data_ptr(), w.numel()
         return x
 
+    def _check(self, rc: int, what: str) -> None:
+        if isinstance(self.dcomm, TorchServedComm):
+            self.dcomm.check(rc, what)
+        else:
+            L.check(rc, what)
+
     # -------------------------------------------------------------- collectives
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         all_gather_into(out, inp, self.group, self.world, force=self.coll)
@@ -304,8 +430,8 @@ class SparseGradExchange:
             x = self._x
             if x.workspace != w.data_ptr():  # a larger batch grew the scratch
                 x.workspace, x.workspace_bytes = w.data_ptr(), w.numel()
-            L.check(t.lib.dqrm_exchange_grad(C.byref(x), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
-                                             _stream_handle()), "dqrm_exchange_grad")
+            self._check(t.lib.dqrm_exchange_grad(C.byref(x), C.byref(batch.c), _ptr(dy), st, sb, int(ste),
+                                                 _stream_handle()), "dqrm_exchange_grad")
             return self.s_avg
         k = self.kernels
         k.coalesce(batch, dy, self.ws, ste, layout)
@@ -325,8 +451,9 @@ class SparseGradExchange:
         if mode is None:
             mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
         if self._x is not None:
-            L.check(self.tables.lib.dqrm_exchange_apply(C.byref(self._x), float(lr), int(mode), 4 if repack else 0,
-                                                        _stream_handle()), "dqrm_exchange_apply")
+            self._check(self.tables.lib.dqrm_exchange_apply(C.byref(self._x), float(lr), int(mode),
+                                                            4 if repack else 0, _stream_handle()),
+                        "dqrm_exchange_apply")
             return
         gathered = self.gathered if self.coll else self.payload.view(1, -1)
         self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, gb, self.s_avg,
@@ -548,5 +675,5 @@ def get_my_slice(n: int, my_size: int, my_rank: int) -> slice:
     return slice(my_rank * k + min(my_rank, m), (my_rank + 1) * k + min(my_rank + 1, m), 1)
 
 
-__all__ = ["DqrmComm", "use_library_collectives", "SparseGradExchange", "MultiSetExchange", "ConsolidatedExchange", "HipExchangeKernels", "payload_bytes",
+__all__ = ["DqrmComm", "TorchServedComm", "exchange_transport", "TRANSPORTS", "use_library_collectives", "SparseGradExchange", "MultiSetExchange", "ConsolidatedExchange", "HipExchangeKernels", "payload_bytes",
            "get_my_slice", "all_gather_into"]

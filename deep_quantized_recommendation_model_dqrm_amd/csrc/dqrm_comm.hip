@@ -75,9 +75,11 @@ int rccl_fail(const char* what, RcclResult e) {
 }  // namespace
 
 struct dqrm_comm {
-    RcclComm comm;
+    RcclComm comm;              // RCCL (dqrm_comm_init), or null for a caller-served transport
     int nranks;
     int rank;
+    dqrm_allgather_fn fn;       // caller-served all-gather (dqrm_comm_init_external), else null
+    void* user;
 };
 
 extern "C" {
@@ -103,29 +105,48 @@ int dqrm_comm_init(dqrm_comm** comm, int nranks, int rank, const void* id128) {
     RcclComm c = nullptr;
     const RcclResult e = r.comm_init_rank(&c, nranks, id, rank);
     if (e) return rccl_fail("ncclCommInitRank", e);
-    *comm = new dqrm_comm{c, nranks, rank};
+    *comm = new dqrm_comm{c, nranks, rank, nullptr, nullptr};
+    return DQRM_OK;
+}
+
+int dqrm_comm_init_external(dqrm_comm** comm, int nranks, int rank, dqrm_allgather_fn fn, void* user) {
+    if (!comm || !fn || nranks <= 0 || rank < 0 || rank >= nranks)
+        return fail(DQRM_E_INVALID, "dqrm_comm_init_external", "bad arguments");
+    *comm = new dqrm_comm{nullptr, nranks, rank, fn, user};
     return DQRM_OK;
 }
 
 int dqrm_comm_destroy(dqrm_comm* comm) {
     if (!comm) return DQRM_OK;
-    const RcclResult e = rccl().comm_destroy(comm->comm);
+    const RcclResult e = comm->comm ? rccl().comm_destroy(comm->comm) : 0;
     delete comm;
     return e ? rccl_fail("ncclCommDestroy", e) : DQRM_OK;
 }
 
 int dqrm_comm_allgather(dqrm_comm* comm, const void* send, void* recv, size_t bytes, void* stream) {
     if (!comm || !send || !recv) return fail(DQRM_E_INVALID, "dqrm_comm_allgather", "null argument");
+    if (comm->fn) {  // the caller's transport, called on this thread in stream order
+        const int rc = comm->fn(send, recv, bytes, stream, comm->user);
+        return rc ? fail(DQRM_E_HIP, "dqrm_comm_allgather", "the caller's all-gather failed") : DQRM_OK;
+    }
     const RcclResult e = rccl().all_gather(send, recv, bytes, kRcclUint8, comm->comm, (hipStream_t)stream);
     return e ? rccl_fail("ncclAllGather", e) : DQRM_OK;
 }
+
+int dqrm_comm_size(const dqrm_comm* comm) { return comm ? comm->nranks : DQRM_E_INVALID; }
 
 static int check_exchange(const dqrm_exchange* x, const char* who) {
     if (!x || !x->set) return fail(DQRM_E_INVALID, who, "null exchange / table set");
     if (x->comm ? x->num_ranks != x->comm->nranks : x->num_ranks != 1)
         return fail(DQRM_E_INVALID, who, "num_ranks does not match the communicator (1 without one)");
-    if (x->num_ranks > 1 && (!x->absmax_all || !x->gathered))
-        return fail(DQRM_E_INVALID, who, "gather buffers required for num_ranks > 1");
+    if (x->comm && (!x->absmax_all || !x->gathered))
+        return fail(DQRM_E_INVALID, who, "gather buffers (absmax_all, gathered) required with a communicator");
+    if (!x->payload || !x->s_avg || !x->cap_base || x->cap_total < 0 || x->payload_bytes == 0)
+        return fail(DQRM_E_INVALID, who, "null payload / s_avg / cap_base");
+    if (x->grad_bits != 32 && (x->grad_bits < 2 || x->grad_bits > 16))
+        return fail(DQRM_E_INVALID, who, "grad_bits must be 2..16 or 32");
+    if (x->payload_bytes != dqrm_payload_bytes(x->set->num_tables, x->cap_total, x->set->dim, x->grad_bits))
+        return fail(DQRM_E_INVALID, who, "payload_bytes does not match dqrm_payload_bytes(T, cap_total, D, grad_bits)");
     return DQRM_OK;
 }
 
@@ -133,6 +154,8 @@ int dqrm_exchange_grad(const dqrm_exchange* x, const dqrm_batch* batch, const fl
                        int64_t dy_stride_b, int ste, void* stream) {
     int rc = check_exchange(x, "dqrm_exchange_grad");
     if (rc) return rc;
+    if (!x->ws_cap_base || !x->ws_rows || !x->ws_vals || !x->ws_ucount || !x->ws_absmax)
+        return fail(DQRM_E_INVALID, "dqrm_exchange_grad", "null coalesce workspace");
     const int T = x->set->num_tables, S = DQRM_TABLE_SPLIT;
     if ((rc = dqrm_emb_bwd_coalesce(x->set, batch, dy, dy_stride_t, dy_stride_b, ste, x->ws_cap_base, x->ws_rows,
                                     x->ws_vals, x->ws_ucount, x->ws_absmax, x->workspace, x->workspace_bytes,

@@ -3091,10 +3091,8 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
     const bool p1 = a.pool1 != 0;
     const int64_t ib = p1 ? (int64_t)t * B : a.idx_base[t];
     const int L = p1 ? B : (int)(a.idx_base[t + 1] - ib);
-    if (L > a.Lc || L > MAXL) {  // more lookups than the caller planned for: skipped, flagged
-        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
-        return;
-    }
+    const bool overflow = L > a.Lc || L > MAXL;  // more lookups than the caller planned for
+    const int Lv = overflow ? 0 : L;              // (checked below, after the forward's setup)
     const float s = a.scale[t];
     const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
     const int gbase = (threadIdx.x % WAVE) - sub;
@@ -3105,7 +3103,7 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
         const int i = grp + k * G;
-        xr[k] = i < L ? a.idx[ib + i] : -1;
+        xr[k] = i < Lv ? a.idx[ib + i] : -1;
     }
     const int64_t o0 = (!p1 && (int)threadIdx.x < B) ? a.off[(int64_t)t * B + threadIdx.x] : 0;
     int64_t nxr[FWD ? NPG : 1];  // the next batch's rows of this lane group's bags (FWD)
@@ -3157,6 +3155,11 @@ __global__ void __launch_bounds__(SG_TPB) k_sgd_small(FArgs a) {
             }
         }
     };
+    if (overflow) {  // the update is skipped and flagged; the next batch's forward still runs
+        if (threadIdx.x == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);
+        fwd_tail();
+        return;
+    }
     const float* dyt = a.dy + (int64_t)t * a.dst_t;
     float4 gv[DYF];
 #pragma unroll
@@ -3897,6 +3900,34 @@ bool fused_sgd_fwd_on() {  // DQRM_FUSED_FWD=0: the next batch's forward as its 
     return !off;
 }
 
+// Whether k_sgd_small takes an SGD call (MODE 0) of this batch, and whether the next batch's
+// forward then runs inside it: returns 0 (k_bwd_fused), 1 (k_sgd_small, forward apart or none),
+// 2 (k_sgd_small with the forward in the launch)
+int sgd_small_plan(const dqrm_table_set* set, const dqrm_batch* batch, const dqrm_batch* next, uint32_t fwd_flags,
+                   size_t* dyn_out) {
+    const int D = set->dim;
+    const int64_t Lc = bwd_lookup_cap(batch);
+    if (!(g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && Lc <= sg_maxl(D / 4) &&
+          batch->num_bags * D <= SG_DY_FLOATS && set->total_rows <= 0x7fffffffll))
+        return 0;
+    // dy staging, then (Criteo form) the row hash; the kernel reads L = B lookups per table.
+    // It takes the batch only if that dynamic LDS plus its static LDS fit one CU (else
+    // k_bwd_fused, which has no per-batch LDS).
+    const bool p1 = (batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
+    const size_t dyn = (size_t)batch->num_bags * D * sizeof(float) + (p1 ? (size_t)sg_hash_bytes((int)batch->num_bags) : 0);
+    // the next batch's forward inside the launch: a Criteo-form batch of the same size on
+    // the exact FP32 rows (the packed INT4 path stays a launch of its own)
+    const bool fwd = next && (next->flags & DQRM_BATCH_POOLING_ONE) && next->num_bags == batch->num_bags &&
+                     next->max_lookups >= next->num_bags && !(fwd_flags & DQRM_FWD_USE_PACKED) && fused_sgd_fwd_on();
+    bool fits = false;
+    DISPATCH_LPR(D, {
+        fits = dyn + (fwd ? static_lds_bytes(k_sgd_small<LPR, true>) : static_lds_bytes(k_sgd_small<LPR, false>)) <=
+               (size_t)LDS_PER_CU;
+    });
+    if (dyn_out) *dyn_out = dyn;
+    return fits ? (fwd ? 2 : 1) : 0;
+}
+
 template <int MODE>
 int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     const dqrm_table_set* set = c.set;
@@ -3923,25 +3954,11 @@ int launch_bwd(const BwdCall& c, hipStream_t st, const char* who) {
     fa.ws_vals = c.ws_vals; fa.ws_ucount = c.ws_ucount; fa.ws_absmax = c.ws_absmax; fa.Lc = Lc;
     int rc = 0;
     // SGD of a small batch: one workgroup per table, no sort, no hand-off (k_sgd_small)
-    if (MODE == 0 && g_coalesce_kernel.load() == DQRM_COALESCE_AUTO && Lc <= sg_maxl(D / 4) &&
-        c.batch->num_bags * D <= SG_DY_FLOATS && set->total_rows <= 0x7fffffffll) {
-        // dy staging, then (Criteo form) the row hash; the kernel reads L = B lookups per table.
-        // It takes the batch only if that dynamic LDS plus its static LDS fit one CU (else
-        // k_bwd_fused below, which has no per-batch LDS).
-        const bool p1 = (c.batch->flags & DQRM_BATCH_POOLING_ONE) != 0;
-        const size_t dyn = (size_t)c.batch->num_bags * D * sizeof(float) +
-                           (p1 ? (size_t)sg_hash_bytes((int)c.batch->num_bags) : 0);
-        // the next batch's forward inside the launch: a Criteo-form batch of the same size on
-        // the exact FP32 rows (the packed INT4 path stays a launch of its own)
-        const bool fwd = c.next && (c.next->flags & DQRM_BATCH_POOLING_ONE) && c.next->num_bags == c.batch->num_bags &&
-                         c.next->max_lookups >= c.next->num_bags && !(c.fwd_flags & DQRM_FWD_USE_PACKED) &&
-                         fused_sgd_fwd_on();
-        bool fits = false;
-        DISPATCH_LPR(D, {
-            fits = dyn + (fwd ? static_lds_bytes(k_sgd_small<LPR, true>) : static_lds_bytes(k_sgd_small<LPR, false>)) <=
-                   (size_t)LDS_PER_CU;
-        });
-        if (fits) {
+    if (MODE == 0) {
+        size_t dyn = 0;
+        const int plan = sgd_small_plan(set, c.batch, c.next, c.fwd_flags, &dyn);
+        const bool fwd = plan == 2;
+        if (plan > 0) {
             if (fwd) {
                 fa.fwd_idx = c.next->idx; fa.fwd_out = c.fwd_out; fa.fwd_ost_t = c.fwd_ost_t; fa.fwd_ost_b = c.fwd_ost_b;
                 fa.fwd_scale = set->scale; fa.fwd_bits = c.fwd_bits; fa.fwd_flags = c.fwd_flags;
@@ -4630,6 +4647,15 @@ int dqrm_bwd_apply_fwd_local_is_one_launch(const dqrm_table_set* set, const dqrm
     if ((rc = check_batch(batch, "dqrm_bwd_apply_fwd_local_is_one_launch"))) return rc;
     if ((rc = check_batch(next, "dqrm_bwd_apply_fwd_local_is_one_launch"))) return rc;
     return apply_local_one_launch(set, batch, stream) && fused_fwd_fits(batch, next, fwd_flags) ? 1 : 0;
+}
+
+int dqrm_bwd_sgd_fwd_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, const dqrm_batch* next,
+                                   uint32_t fwd_flags) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(batch, "dqrm_bwd_sgd_fwd_is_one_launch"))) return rc;
+    if ((rc = check_batch(next, "dqrm_bwd_sgd_fwd_is_one_launch"))) return rc;
+    return sgd_small_plan(set, batch, next, fwd_flags, nullptr) == 2 ? 1 : 0;
 }
 
 static int bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, const float* dy, int64_t dy_stride_t,

@@ -58,6 +58,13 @@ __global__ void __launch_bounds__(PS_TPB) k_lookup_grad_presum(dqrm_internal::Pr
     const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
     const int L = (int)(a.pool1 ? a.B : a.idx_base[t + 1] - ibase);
     const int64_t B = a.B;
+    if (L < 0 || L > PS_MAXL) {  // the caller understated max_lookups: the LDS lists cannot hold the
+        if (tid == 0) flag_error(a.err, DQRM_ERRF_OVERFLOW);  // table; flagged, its entries zero rows
+        for (int64_t j = tid; j < L; j += PS_TPB) a.rows[ibase + j] = rowbase;
+        for (int64_t q = tid; q < (int64_t)L * (D / 4); q += PS_TPB)
+            reinterpret_cast<float4*>(a.vals + ibase * D)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     const bool p1 = a.pool1 && L == B;
     // 1. indices of this thread's lookups (all in flight); the hash cleared meanwhile
     int64_t r[PS_PER];

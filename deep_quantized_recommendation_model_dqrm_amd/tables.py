@@ -491,6 +491,15 @@ class EmbeddingTableSet:
         )
         return out
 
+    def sgd_fwd_is_one_launch(self, batch: LookupBatch, next_batch: LookupBatch, use_packed: bool = False) -> bool:
+        """Whether backward_sgd_forward runs the SGD and the next batch's forward as ONE launch
+        (dqrm_bwd_sgd_fwd_is_one_launch)."""
+        rc = self.lib.dqrm_bwd_sgd_fwd_is_one_launch(C.byref(self._c), C.byref(batch.c), C.byref(next_batch.c),
+                                                     self._fwd_flags(True, use_packed, False))
+        if rc < 0:
+            L.check(rc, "dqrm_bwd_sgd_fwd_is_one_launch")
+        return rc == 1
+
     def local_update(self, batch: LookupBatch, dy: torch.Tensor, lr: float, table_mask: torch.Tensor | None = None,
                      ste: bool = True, repack: bool = False, layout: str = "tbd") -> None:
         """W.add_(-lr * grad) with the rank's own uncoalesced gradient, product rounded, in

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 9  /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 10 /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
@@ -57,7 +57,10 @@ extern "C" {
                                   (the N > 1 exchange as two calls), dqrm_emb_bwd_lookup_grad_presum;
                                9: dqrm_emb_bwd_apply_fwd_local (the next batch's forward behind the
                                   one-launch update), dqrm_bwd_apply_fwd_local_is_one_launch,
-                                  dqrm_emb_bwd_sgd_fwd */
+                                  dqrm_emb_bwd_sgd_fwd;
+                              10: dqrm_comm_init_external (a caller-served all-gather under the
+                                  same exchange orchestration), dqrm_comm_size,
+                                  dqrm_bwd_sgd_fwd_is_one_launch */
 
 /* status codes */
 #define DQRM_OK            0
@@ -213,6 +216,12 @@ int dqrm_emb_bwd_sgd_fwd(const dqrm_table_set* set, const dqrm_batch* batch, con
                          void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
                          uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
                          void* stream);
+
+/* 1 if dqrm_emb_bwd_sgd_fwd would run the SGD of `batch` and the forward of `next` as ONE
+ * launch (the small-batch kernel takes the update and `next` is a Criteo-form batch of the
+ * same size without DQRM_FWD_USE_PACKED), 0 if as two launches, <0 on bad arguments. */
+int dqrm_bwd_sgd_fwd_is_one_launch(const dqrm_table_set* set, const dqrm_batch* batch, const dqrm_batch* next,
+                                   uint32_t fwd_flags);
 
 /* ---------------------------------------------------------------------------------
  * Data-parallel gradient path (sgd_quantized_gradients_parallel_comm.py)
@@ -593,7 +602,20 @@ int dqrm_comm_unique_id(void* id128);
 /* Collective over the `nranks` processes (one per GPU, each with the same id): creates this
  * rank's communicator on the current HIP device. nranks == 1 is allowed (local copies). */
 int dqrm_comm_init(dqrm_comm** comm, int nranks, int rank, const void* id128);
+
+/* A communicator whose all-gather the caller serves: every dqrm_comm_allgather on it (and so
+ * both collectives of dqrm_exchange_grad) calls fn(send, recv, bytes, stream, user) on the
+ * issuing host thread, with the device pointers and the stream the call was given, in the
+ * step's order. fn must leave recv[r * bytes, (r+1) * bytes) = rank r's send in stream order
+ * before the stream's next work (e.g. a torch.distributed all_gather_into_tensor on that
+ * stream, or a Gloo gather staged through host memory after a stream synchronise) and return
+ * 0, else non-zero (the exchange call then fails with DQRM_E_HIP). The exchange's kernels and
+ * buffer handling are those of the RCCL communicator: this is how the N > 1 orchestration runs
+ * over the reference's own transport (Gloo, s_q_g_p_c.py:865,878) or torch.distributed's. */
+typedef int (*dqrm_allgather_fn)(const void* send, void* recv, size_t bytes, void* stream, void* user);
+int dqrm_comm_init_external(dqrm_comm** comm, int nranks, int rank, dqrm_allgather_fn fn, void* user);
 int dqrm_comm_destroy(dqrm_comm* comm);
+int dqrm_comm_size(const dqrm_comm* comm);
 
 /* recv[r * bytes, (r+1) * bytes) <- rank r's send[0, bytes), in rank order, on `stream`
  * (ncclAllGather of bytes uint8). */

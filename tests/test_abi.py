@@ -75,6 +75,68 @@ def test_exchange_and_comm_reject_bad_arguments_without_device(lib):
     assert lib.dqrm_emb_bwd_lookup_grad_presum(None, None, None, 0, 0, 1, None, None, None) == L.DQRM_E_INVALID
 
 
+def test_check_exchange_errors_without_device(lib):
+    """dqrm_exchange_grad / _apply reject an inconsistent exchange before any kernel or
+    collective: num_ranks against the communicator's size, missing gather buffers, a payload
+    size that is not dqrm_payload_bytes, bad grad_bits, a missing coalesce workspace. The
+    communicator here is a caller-served one (dqrm_comm_init_external), which needs no device."""
+    calls = []
+    fn = L.ALLGATHER_FN(lambda send, recv, n, stream, user: calls.append((send, recv, n)) or 0)
+    h = C.c_void_p()
+    assert lib.dqrm_comm_init_external(C.byref(h), 2, 1, fn, None) == L.DQRM_OK
+    try:
+        assert lib.dqrm_comm_size(h) == 2
+        ts = L.TableSet()
+        ts.num_tables, ts.dim = 3, 16
+        T, cap, D = 3, 100, 16
+        x = L.Exchange()
+        x.set = C.pointer(ts)
+        x.comm = h
+        x.grad_bits = 8
+        x.cap_total, x.cap_base = cap, 0x1000
+        x.payload, x.s_avg = 0x2000, 0x3000
+        x.absmax_all, x.gathered = 0x4000, 0x5000
+        x.ws_cap_base, x.ws_rows, x.ws_vals, x.ws_ucount, x.ws_absmax = 0x10, 0x20, 0x30, 0x40, 0x50
+        x.payload_bytes = lib.dqrm_payload_bytes(T, cap, D, 8)
+
+        def expect(field, value, msg, grad=False):
+            old = getattr(x, field)
+            setattr(x, field, value)
+            try:
+                fn_ = (lambda: lib.dqrm_exchange_grad(C.byref(x), None, None, 0, 0, 1, None)) if grad else \
+                    (lambda: lib.dqrm_exchange_apply(C.byref(x), 0.1, L.DQRM_UPD_DP, 0, None))
+                assert fn_() == L.DQRM_E_INVALID, field
+                assert msg in lib.dqrm_last_error(), (field, lib.dqrm_last_error())
+            finally:
+                setattr(x, field, old)
+
+        x.num_ranks = 2
+        expect("num_ranks", 1, b"num_ranks")        # the communicator has 2 ranks
+        expect("num_ranks", 3, b"num_ranks")
+        expect("comm", None, b"num_ranks")          # no communicator: world size 1 only
+        expect("absmax_all", None, b"gather buffers")
+        expect("gathered", None, b"gather buffers")
+        expect("payload", None, b"null payload")
+        expect("payload_bytes", x.payload_bytes + 16, b"payload_bytes")
+        expect("grad_bits", 1, b"grad_bits")
+        expect("grad_bits", 17, b"grad_bits")
+        expect("ws_rows", None, b"coalesce workspace", grad=True)
+        assert not calls  # nothing reached the transport
+        # the caller-served all-gather is called with the device pointers, in order
+        assert lib.dqrm_comm_allgather(h, 0x111, 0x222, 48, None) == L.DQRM_OK
+        assert calls == [(0x111, 0x222, 48)]
+        bad = L.ALLGATHER_FN(lambda *a: 1)
+        h2 = C.c_void_p()
+        assert lib.dqrm_comm_init_external(C.byref(h2), 2, 0, bad, None) == L.DQRM_OK
+        assert lib.dqrm_comm_allgather(h2, 0x111, 0x222, 48, None) == L.DQRM_E_HIP
+        assert b"all-gather failed" in lib.dqrm_last_error()
+        assert lib.dqrm_comm_destroy(h2) == L.DQRM_OK
+        assert lib.dqrm_comm_init_external(C.byref(h2), 2, 2, fn, None) == L.DQRM_E_INVALID  # rank >= nranks
+        assert lib.dqrm_comm_init_external(C.byref(h2), 2, 0, L.ALLGATHER_FN(), None) == L.DQRM_E_INVALID
+    finally:
+        assert lib.dqrm_comm_destroy(h) == L.DQRM_OK
+
+
 def test_fused_next_forward_rejects_bad_arguments_without_device(lib):
     """dqrm_emb_bwd_apply_fwd_local validates the next batch's forward as dqrm_emb_fwd does
     (before any launch)."""
@@ -86,6 +148,7 @@ def test_fused_next_forward_rejects_bad_arguments_without_device(lib):
     assert lib.dqrm_bwd_apply_fwd_local_is_one_launch(None, None, None, 0, None) == L.DQRM_E_INVALID
     assert lib.dqrm_emb_bwd_sgd_fwd(C.byref(ts), None, None, 0, 0, 1, 0.1, 0, None, 0, None, 4, 0, None, 0, 0,
                                     None) == L.DQRM_E_INVALID
+    assert lib.dqrm_bwd_sgd_fwd_is_one_launch(None, None, None, 0) == L.DQRM_E_INVALID
 
 
 def test_apply_kernel_selector(lib):

@@ -26,7 +26,7 @@ def _free_port() -> int:
     return port
 
 
-def _rank(rank, world, port, grad_bits, out_dir):
+def _rank(rank, world, port, grad_bits, out_dir, transport="torch"):
     sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,7 +38,11 @@ def _rank(rank, world, port, grad_bits, out_dir):
         Ws = G.table_weights(ROWS, D, 41)
         ts = dq.EmbeddingTableSet(ROWS, D, device="cuda", init=None, weights=[torch.from_numpy(w) for w in Ws])
         sl = dq.get_my_slice(B_GLOBAL, world, rank)
-        ex = dq.SparseGradExchange(ts, sl.stop - sl.start, grad_bits=grad_bits)
+        ex = dq.SparseGradExchange(ts, sl.stop - sl.start, grad_bits=grad_bits, transport=transport)
+        # torch: libdqrm's N > 1 orchestration (dqrm_exchange_grad / _apply with num_ranks = 2,
+        # the C path RCCL runs) with its two all-gathers served by Gloo through the callback
+        assert ex.transport == transport and (ex._x is not None) == (transport == "torch")
+        assert ex._x is None or ex._x.num_ranks == world
         from deep_quantized_recommendation_model_dqrm_amd.dense import DenseGradExchange
 
         layers = []
@@ -64,6 +68,8 @@ def _rank(rank, world, port, grad_bits, out_dir):
             ex.step(b, torch.from_numpy(np.ascontiguousarray(dy[:, sl])).cuda(), lr=0.1)
         torch.cuda.synchronize()
         assert ts.read_errors() == 0
+        if transport == "torch":  # both all-gathers of every step went through the C orchestration
+            assert ex.dcomm.calls == STEPS * (2 if grad_bits != 32 else 1)
         mlp = {f"W{j}": l.weight.detach().cpu().numpy() for j, l in enumerate(layers)}
         mlp.update({f"b{j}": l.bias.detach().cpu().numpy() for j, l in enumerate(layers)})
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), *[ts.table_weight(t).cpu().numpy() for t in range(len(ROWS))],
@@ -73,7 +79,14 @@ def _rank(rank, world, port, grad_bits, out_dir):
 
 
 @pytest.mark.parametrize("grad_bits", [8, 32])
-def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits):
+@pytest.mark.parametrize("transport", ["torch", "python"])
+def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits, transport):
+    """Two processes, the global batch sliced: every rank's tables and MLP layers equal
+    oracle.dp_step / dense_dp_step over the whole batch, bit for bit. transport "torch":
+    the step runs through libdqrm's exchange calls with num_ranks = 2 (the orchestration,
+    buffer checks, gathered-maxima pitch and gathered-payload apply RCCL uses), the
+    all-gathers served by Gloo; "python": kernels and collectives issued one by one.
+    Reference: s_q_g_p_c.py:863-885 (scale all_reduce, sparse all_reduce), :601-628."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import gen_inputs as G
@@ -81,7 +94,7 @@ def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits):
     from deep_quantized_recommendation_model_dqrm_amd import get_my_slice
 
     world = 2
-    mp.spawn(_rank, args=(world, _free_port(), grad_bits, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank, args=(world, _free_port(), grad_bits, str(tmp_path), transport), nprocs=world, join=True)
     Ws = G.table_weights(ROWS, D, 41)
     sls = [get_my_slice(B_GLOBAL, world, r) for r in range(world)]
     for k in range(STEPS):

@@ -357,6 +357,59 @@ def test_max_lookups_understated_is_flagged(dq):
     assert torch.equal(ts.W, W0)
 
 
+def test_sgd_next_forward_understated_max_lookups_still_forwards(dq):
+    """k_sgd_small with the next batch's forward (dqrm_emb_bwd_sgd_fwd, one launch) on a batch
+    whose tables hold more lookups than dqrm_batch.max_lookups promised: the update is skipped
+    and flagged (DQRM_ERRF_OVERFLOW), and the next batch's forward is still written -- equal to
+    dqrm_emb_fwd on the unchanged tables, never left as garbage."""
+    rows, D, B = [3, 500, 70000], 16, 128
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=4)
+    W0 = ts.W.clone()
+    b = dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, B, 7)).cuda())
+    nb = dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, B, 8)).cuda())
+    b.c.max_lookups = B - 28
+    assert ts.sgd_fwd_is_one_launch(b, nb)
+    out = torch.full((len(rows), B, D), 7.0, device="cuda")
+    ts.backward_sgd_forward(b, torch.ones(len(rows), B, D, device="cuda"), 0.1, nb, out=out)
+    assert ts.read_errors() & dq._lib.DQRM_ERRF_OVERFLOW
+    assert torch.equal(ts.W, W0)
+    assert torch.equal(out, ts.forward(nb))
+    assert ts.read_errors() == 0
+
+
+def test_presum_understated_max_lookups_is_flagged(dq):
+    """dqrm_emb_bwd_lookup_grad_presum trusts no host-side bound: a table with more lookups
+    than its LDS lists hold (DQRM_PRESUM_MAX_LOOKUPS), under a batch whose max_lookups
+    understates it, is flagged DQRM_ERRF_OVERFLOW with its entries written as zero rows (no
+    out-of-bounds LDS writes); the other table's entries are the normal presummed ones."""
+    import ctypes as C
+    from deep_quantized_recommendation_model_dqrm_amd import tables as TB
+
+    rows, D = [50, 400], 16
+    lens = [3000, 40]
+    rng = np.random.default_rng(3)
+    idxs = [rng.integers(0, n, size=l).astype(np.int64) for n, l in zip(rows, lens)]
+    offs = [np.arange(l, dtype=np.int64)[:: max(1, l // 8)][:8] for l in lens]  # 8 bags per table
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=5)
+    b = to_batch(dq, idxs, offs)
+    b.c.max_lookups = 100  # understated: table 0 has 3000 lookups
+    dy = torch.from_numpy(G.upstream_grad(2, 8, D, 9)).cuda()
+    Lk = sum(lens)
+    r = torch.full((Lk,), -5, dtype=torch.int64, device="cuda")
+    v = torch.full((Lk, D), 9.0, dtype=torch.float32, device="cuda")
+    rc = ts.lib.dqrm_emb_bwd_lookup_grad_presum(C.byref(ts._c), C.byref(b.c), TB._ptr(dy), 8 * D, D, 1, TB._ptr(r),
+                                                TB._ptr(v), TB._stream_handle())
+    assert rc == 0
+    assert ts.read_errors() & dq._lib.DQRM_ERRF_OVERFLOW
+    assert torch.equal(r[:3000], torch.zeros(3000, dtype=torch.int64, device="cuda") + ts.row_base[0])
+    assert torch.equal(v[:3000], torch.zeros(3000, D, device="cuda"))
+    b2 = to_batch(dq, idxs[1:], offs[1:])  # table 1 alone, through the normal path
+    ts1 = ts.view(1)
+    r1, v1 = ts1.lookup_grad(b2, dy[1:].contiguous(), presum=True)
+    assert torch.equal(r[3000:] - ts.row_base[1], r1 - ts1.row_base[0])
+    assert torch.equal(v[3000:], v1)
+
+
 def test_kaggle_full_size_forward_and_step(dq):
     """Full Criteo-Kaggle tables (33.8M rows, D=16): forward of every table equals the
     oracle; after 3 SGD steps the scales still equal a full-table oracle scan."""
@@ -753,6 +806,74 @@ def test_terabyte_full_size_773m_rows(dq):
         torch.cuda.empty_cache()
 
 
+def test_terabyte_full_size_step_boundary_773m_rows(dq):
+    """The exact form bench.py times at N=1 (bench.py step(): backward_apply_forward_local,
+    k_coalesce_p1<APPLY> with the next batch's forward inside the launch) on the full
+    773,280,534-row TB slab, pinned to the oracle on EVERY table over two steps: the first
+    forward, then per step the averaged gradient scale s_avg, every row any of the batches
+    touches (updated rows = oracle.dp_step, the others unchanged), the next batch's forward
+    scale (= a full-table max taken independently with torch.aminmax) and the next batch's
+    fake-quantized output (= oracle.emb_fwd on the updated rows); at the end the incremental
+    |W| hierarchy equals a rebuild. Reference: quant_modules_not_quantize_grad.py:317-398,
+    sgd_quantized_gradients_parallel_comm.py:601-628,850-890 (world size 1)."""
+    from deep_quantized_recommendation_model_dqrm_amd.workloads import TERABYTE_X16_ROWS
+
+    rows, D, B = TERABYTE_X16_ROWS, 64, 2048
+    T = len(rows)
+    torch.cuda.empty_cache()
+    ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=78)
+    ex = dq.SparseGradExchange(ts, B, grad_bits=8)
+    try:
+        Ps = [G.pooling_one(rows, B, 180 + k, dist="zipf" if k == 1 else "uniform") for k in range(3)]
+        bs = [dq.LookupBatch.pooling_one(torch.from_numpy(P).cuda()) for P in Ps]
+        assert ts.apply_fwd_local_is_one_launch(bs[0], bs[1])
+        # compact host copies of every row the three batches touch, per table
+        uniq, inv, Wc = [], [], []
+        for t in range(T):
+            u, iv = np.unique(np.concatenate([P[t] for P in Ps]), return_inverse=True)
+            uniq.append(torch.from_numpy(u).cuda())
+            inv.append([iv[k * B:(k + 1) * B].astype(np.int64) for k in range(3)])
+            Wc.append(ts.table_weight(t)[uniq[t]].cpu().numpy())
+
+        def full_scales():
+            out = []
+            for t in range(T):
+                mn, mx = torch.aminmax(ts.table_weight(t))  # no table-sized temporary (largest 41 GB)
+                out.append(O.sym_scale(max(-float(mn), float(mx)), 4))
+            return np.array(out, dtype=np.float32)
+
+        ar = np.arange(B, dtype=np.int64)
+        y = ts.forward(bs[0]).cpu().numpy()
+        s = full_scales()
+        np.testing.assert_array_equal(ts.scale.cpu().numpy(), s)
+        for t in range(T):
+            np.testing.assert_array_equal(y[t], O.emb_fwd(Wc[t], inv[t][0], ar, s[t])[0])
+        for k in range(2):
+            dy = G.upstream_grad(T, B, D, 190 + k)
+            yn = ts.backward_apply_forward_local(bs[k], torch.from_numpy(dy).cuda(), ex.ws, 8, ex.s_avg, 0.1,
+                                                 bs[k + 1]).cpu().numpy()
+            res = O.dp_step(Wc, [[(inv[t][k], ar) for t in range(T)]], [[dy[t] for t in range(T)]], list(s), 0.1)
+            np.testing.assert_array_equal(ex.s_avg.cpu().numpy(), np.array([r[0] for r in res], np.float32))
+            for t in range(T):
+                np.testing.assert_array_equal(ts.table_weight(t)[uniq[t]].cpu().numpy(), Wc[t], err_msg=f"W {k} {t}")
+            s = full_scales()
+            np.testing.assert_array_equal(ts.scale.cpu().numpy(), s)
+            for t in range(T):
+                np.testing.assert_array_equal(yn[t], O.emb_fwd(Wc[t], inv[t][k + 1], ar, s[t])[0],
+                                              err_msg=f"forward {k} {t}")
+        assert ts.read_errors() == 0
+        inc = [x.clone() for x in (ts.blkmax, ts.sblkmax, ts.tmax)]
+        rm = ts.rowmax.clone()
+        ts.refresh_absmax()
+        assert torch.equal(rm, ts.rowmax)
+        del rm
+        for x, z in zip(inc, (ts.blkmax, ts.sblkmax, ts.tmax)):
+            assert torch.equal(x, z)
+    finally:
+        del ts, ex
+        torch.cuda.empty_cache()
+
+
 COAL_ROWS = [3, 62, 971, 1435, 1792, 1793, 2208, 7112, 32768, 300000, 20_000_000]
 
 
@@ -985,8 +1106,8 @@ def test_fused_next_forward_matches_separate_calls(dq, D, B, dist, layout, refre
         assert torch.equal(s_avg[0], s_avg[1]), it
         for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
             assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
-    # and the last output is the oracle's forward of the updated tables (tables 0 and 7)
-    for t in (0, 7):
+    # and the last output is the oracle's forward of the updated tables (every table)
+    for t in range(T):
         yt = (y0[t] if layout == "tbd" else y0[:, t]).cpu().numpy()
         Wt = sets[0].table_weight(t).cpu().numpy()
         st = np.float32(1.0) if full else np.float32(sets[0].scale[t].item())

@@ -32,9 +32,9 @@ def _free_port() -> int:
     return port
 
 
-def _rank(rank, port, grad_bits, out_dir, c_comm=True):
+def _rank(rank, port, grad_bits, out_dir, transport="rccl"):
     sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(ROOT, "oracle"), ROOT]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DQRM_C_COMM="1" if c_comm else "0")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DQRM_C_COMM=transport)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
@@ -47,9 +47,10 @@ def _rank(rank, port, grad_bits, out_dir, c_comm=True):
         ts = dq.EmbeddingTableSet(ROWS, D, device="cuda", init=None, weights=[torch.from_numpy(w) for w in Ws])
         ex = dq.SparseGradExchange(ts, B, grad_bits=grad_bits, force_collectives=True)
         assert ex.coll and ex.world == 1
-        # c_comm: the two all-gathers are issued by libdqrm on its own RCCL communicator
-        # (dqrm_exchange_grad / _apply); else through torch.distributed
-        assert (ex._x is not None) == c_comm
+        # rccl: the two all-gathers are issued by libdqrm on its own RCCL communicator
+        # (dqrm_exchange_grad / _apply); torch: the same calls, c10d's RCCL all-gathers served
+        # through the callback; python: kernels and all-gathers issued from Python
+        assert ex.transport == transport and (ex._x is not None) == (transport != "python")
         s_avgs = []
         for k in range(STEPS):
             P = G.pooling_one(ROWS, B, 50 + k, dist="zipf" if k % 2 else "uniform")
@@ -84,19 +85,19 @@ def _rank(rank, port, grad_bits, out_dir, c_comm=True):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("grad_bits,c_comm", [(8, True), (32, True), (8, False)])
-def test_rccl_world1_exchange_matches_oracle(tmp_path, grad_bits, c_comm):
+@pytest.mark.parametrize("grad_bits,transport", [(8, "rccl"), (32, "rccl"), (8, "torch"), (8, "python")])
+def test_rccl_world1_exchange_matches_oracle(tmp_path, grad_bits, transport):
     """SparseGradExchange(force_collectives=True) and DenseGradExchange(force_collectives=True)
     over a real RCCL communicator: W of every table after 3 steps, the per-step averaged
     scales and the MLP parameters equal oracle.dp_step / dense_dp_step at N = 1. c_comm: the
-    embedding exchange's all-gathers issued by libdqrm (dqrm_comm, the default on nccl) or
-    through torch.distributed (DQRM_C_COMM=0)."""
+    embedding exchange's all-gathers issued by libdqrm (dqrm_comm, the default at world size 1
+    on nccl), served by torch.distributed through the callback, or issued from Python."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import gen_inputs as G
     import oracle as O
 
-    mp.spawn(_rank, args=(_free_port(), grad_bits, str(tmp_path), c_comm), nprocs=1, join=True)
+    mp.spawn(_rank, args=(_free_port(), grad_bits, str(tmp_path), transport), nprocs=1, join=True)
     got = np.load(os.path.join(tmp_path, "r0.npz"))
     Ws = G.table_weights(ROWS, D, 41)
     for k in range(STEPS):
