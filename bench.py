@@ -114,6 +114,12 @@ def parse(argv=None):
                         "RCCL communicator between the kernels (falls back to torch if RCCL cannot be set up); "
                         "torch = the same C step with torch.distributed serving the all-gathers; python = the "
                         "kernels and collectives issued one by one from Python (A/B)")
+    p.add_argument("--emulate-ranks", type=int, default=1,
+                   help="N > 1 on ONE GPU: time rank 0's step of an N-rank run (its slice: --batch-per-gpu "
+                        "per rank, or --global-batch / --scaling strong split N ways) with the other ranks' "
+                        "maxima and payloads precomputed from their own slices; the two all-gathers are replaced "
+                        "by those resident buffers (rank 0's parts written in place), so the line is the per-rank "
+                        "kernel time at N without xGMI time (a projection input, not a measurement of N GPUs)")
     p.add_argument("--separate-forward", action="store_true",
                    help="N=1 one-launch step: the forward as its own launch (dqrm_emb_fwd) instead of inside "
                         "the previous step's update launch (dqrm_emb_bwd_apply_fwd_local)")
@@ -265,6 +271,12 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:  # gloo: functional rehearsal of the N>1 path (e.g. several ranks on one GPU)
             dist.init_process_group("gloo")
+    if a.emulate_ranks > 1:
+        if world > 1 or a.mode != "dp":
+            print("--emulate-ranks runs the dp step at world size 1", file=sys.stderr)
+            sys.exit(2)
+        emulate_main(a, dev)
+        return
     if a.mode.startswith("dropin"):
         dropin_main(a, world, rank, dev)
         return
@@ -616,6 +628,116 @@ def main():
         dist.destroy_process_group()
     if err:  # a step that dropped or mis-indexed lookups is not a measurement
         print(f"device error flags 0x{err:x}", file=sys.stderr)
+        sys.exit(3)
+
+
+def emulate_main(a, dev):
+    """rank 0 of an N-rank data-parallel step on one GPU (--emulate-ranks N): the kernels rank 0
+    runs at N GPUs -- forward, coalesce of its slice, quantize-pack against all N ranks' maxima
+    (the rank-averaged scale), the apply over all N payloads (+ the finalize launch) -- with
+    the two all-gathers replaced by resident buffers: every other rank's per-slot maxima and
+    INT8 payload of each resident batch are computed beforehand from that rank's own slice
+    (untimed), and rank 0's coalesce / quantize-pack write their maxima / payload straight into
+    row 0 of the gathered buffers (what the all-gather leaves there). What the line adds to a
+    real N-GPU step is the xGMI time of the two all-gathers, estimated in DESIGN.md 6."""
+    N = a.emulate_ranks
+    cfg = CONFIGS[a.config]
+    rows, D = cfg["rows"], cfg["dim"]
+    T = len(rows)
+    strong = a.scaling == "strong" or a.global_batch > 0
+    B_global = (a.global_batch or a.batch_per_gpu) if strong else a.batch_per_gpu * N
+    if B_global % N:
+        print(f"global batch {B_global} is not divisible by {N} ranks", file=sys.stderr)
+        sys.exit(2)
+    B = B_global // N
+    nb = a.num_batches
+    gb = a.grad_bits
+    S = L.DQRM_TABLE_SPLIT
+    t0 = time.time()
+    ts = dq.EmbeddingTableSet(rows, D, device=dev, init="uniform", seed=a.seed)
+    ex = dq.SparseGradExchange(ts, B, grad_bits=gb)
+    kern = ex.kernels
+    per_rank = [make_batches(rows, B_global, r, N, nb, a.seed, a.index_dist, dev) for r in range(N)]
+    dys = [torch.randn(T, B, D, device=dev, generator=torch.Generator(device=dev).manual_seed(a.seed + r)) * 0.05
+           for r in range(N)]
+    am_all = [torch.zeros(N, T * S, dtype=torch.float32, device=dev) for _ in range(nb)]
+    gathered = [torch.zeros(N, ex.payload_bytes, dtype=torch.uint8, device=dev) for _ in range(nb)]
+    wss = [dq.CoalescedGrad.allocate(rows, B, D, dev, absmax=am_all[k][0]) for k in range(nb)]
+    tmp = dq.CoalescedGrad.allocate(rows, B, D, dev)
+    s_tmp = torch.zeros(T, dtype=torch.float32, device=dev)
+    for k in range(nb):  # the other ranks' maxima, then their payloads (against every rank's maxima)
+        ts.forward(per_rank[0][k], bits=4)
+        for r in range(1, N):
+            kern.coalesce(per_rank[r][k], dys[r], tmp, True, "tbd")
+            am_all[k][r].copy_(tmp.absmax)
+        kern.coalesce(per_rank[0][k], dys[0], wss[k], True, "tbd")
+        for r in range(1, N):
+            kern.coalesce(per_rank[r][k], dys[r], tmp, True, "tbd")
+            kern.quant_pack(tmp, am_all[k], N, gb, ex.cap_base, ex.cap_total, s_tmp, gathered[k][r])
+    del tmp
+    y = torch.empty(T, B, D, device=dev)
+    torch.cuda.synchronize()
+    setup_s = time.time() - t0
+    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
+
+    def step(i, ev=None):
+        k = i % nb
+        b = per_rank[0][k]
+
+        def mark(j, e):
+            if ev is not None:
+                ev[j][e].record()
+
+        mark(0, 0)
+        ts.forward(b, bits=4, out=y)
+        mark(0, 1)
+        mark(1, 0)
+        kern.coalesce(b, dys[0], wss[k], True, "tbd")  # maxima -> row 0 of the "gathered" maxima
+        mark(1, 1)
+        mark(2, 0)
+        kern.quant_pack(wss[k], am_all[k], N, gb, ex.cap_base, ex.cap_total, ex.s_avg, gathered[k][0])
+        mark(2, 1)
+        mark(3, 0)
+        kern.apply(ex.cap_base, ex.cap_total, gathered[k], ex.payload_bytes, N, gb, ex.s_avg, a.lr, L.DQRM_UPD_DP,
+                   False)
+        mark(3, 1)
+
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    nbk = max(16, min(50, a.steps))
+    bev = [timed_events(len(names)) for _ in range(nbk)]
+    for i in range(nbk):
+        step(a.warmup + i, bev[i])
+    torch.cuda.synchronize()
+    kms = {n: float(np.median([bev[i][j][0].elapsed_time(bev[i][j][1]) for i in range(nbk)]))
+           for j, n in enumerate(names)}
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + nbk + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    err = ts.read_errors()
+    us = elapsed / a.steps * 1e6
+    U = int(wss[(a.warmup + nbk + a.steps - 1) % nb].ucount.sum().item())
+    line = {
+        "metric": "emulated per-rank DP QAT step (rank 0 of N; all-gathers replaced by resident buffers)",
+        "value": None, "unit": "samples/s", "n_gpus": 1, "emulated_ranks": N, "steps": a.steps, "warmup": a.warmup,
+        "us_per_step": round(us, 2), "higher_is_better": True, "scaling": "strong" if strong else "weak",
+        "projected_samples_per_s_without_collectives": round(B_global / (us * 1e-6), 1),
+        "config": {"workload": f"criteo-{a.config} embedding QAT step", "tables": T, "total_rows": sum(rows),
+                   "emb_dim": D, "batch_per_rank": B, "global_batch": B_global, "grad_bits": gb,
+                   "index_dist": a.index_dist},
+        "kernels_ms_median": {k: round(v, 5) for k, v in kms.items()},
+        "alg_bytes": {n: alg_bytes(n, T, B, D, U, N, pool1=True) for n in names},
+        "distinct_rows_rank0": U,
+        "payload_bytes_per_rank": int(ex.payload_bytes), "maxima_bytes_per_rank": T * S * 4,
+        "apply_update_form": L.apply_update_form(),
+        "device_errors": err, "setup_s": round(setup_s, 1),
+    }
+    print(json.dumps(line), flush=True)
+    if err:
         sys.exit(3)
 
 

@@ -28,6 +28,7 @@ all tables instead of 26.
 from __future__ import annotations
 
 import os
+import weakref
 from typing import Sequence
 
 import numpy as np
@@ -123,6 +124,74 @@ def set_default_grad_mode(mode: str) -> None:
     _DEFAULT_GRAD_MODE = mode
 
 
+# grad_mode "sparse" under torch.optim.SGD: when a plain SGD step (no momentum, weight decay,
+# nesterov or maximize) is about to add a module's COO -- the one its last backward produced,
+# untouched since (no accumulation, no in-place edit) -- the module applies that update itself
+# with the reference's rounding: torch's sparse SGD adds -lr * g of every lookup to its row in
+# lookup order (dlrm_s_pytorch_single_gpu.py:1943-1950), which dqrm_emb_bwd_sgd reproduces bit for
+# bit (deterministic; ATen's GPU scatter-add orders duplicate rows by atomics), and then clears
+# .grad so the optimizer skips it. Any other optimizer, or a modified grad, gets the COO as is.
+# DQRM_SGD_HOOK=0 turns this off (the optimizer then adds the COO).
+_SGD_HOOK = os.environ.get("DQRM_SGD_HOOK", "1") != "0"
+_SGD_OWNERS: dict = {}  # id(embedding_bag.weight) -> (weakref(weight), weakref(module)); tensors
+                        # compare elementwise, so a WeakKeyDictionary cannot key them
+_SGD_HOOK_HANDLE = None
+
+
+def set_fused_optimizer_step(enabled: bool) -> None:
+    """Whether plain torch.optim.SGD steps on grad_mode="sparse" modules run as the module's own
+    per-lookup SGD kernel (default; bit-exact with torch's sparse SGD in lookup order) or as
+    the optimizer's add of the COO."""
+    global _SGD_HOOK
+    _SGD_HOOK = bool(enabled)
+
+
+def _plain_sgd_group(opt, g) -> bool:
+    return (isinstance(opt, torch.optim.SGD) and not g.get("momentum", 0) and not g.get("weight_decay", 0)
+            and not g.get("nesterov", False) and not g.get("maximize", False))
+
+
+def _sgd_step_pre_hook(opt, args, kwargs):
+    """torch.optim global step pre-hook: the fused per-lookup SGD of every pending module whose
+    weight this optimizer steps with plain SGD (see _SGD_HOOK)."""
+    if not _SGD_HOOK or not _SGD_OWNERS:
+        return None
+    for g in opt.param_groups:
+        if not _plain_sgd_group(opt, g):
+            continue
+        for p in g["params"]:
+            ent = _SGD_OWNERS.get(id(p))
+            if ent is None or ent[0]() is not p:
+                continue
+            m = ent[1]()
+            if m is not None:
+                m._apply_pending_sgd(p, float(g["lr"]))
+    return None
+
+
+def _register_sgd_owner(module, weight: nn.Parameter) -> None:
+    global _SGD_HOOK_HANDLE
+    if _SGD_HOOK_HANDLE is None:
+        from torch.optim.optimizer import register_optimizer_step_pre_hook
+
+        _SGD_HOOK_HANDLE = register_optimizer_step_pre_hook(_sgd_step_pre_hook)
+    key = id(weight)
+    _SGD_OWNERS[key] = (weakref.ref(weight, lambda _r, k=key: _SGD_OWNERS.pop(k, None)), weakref.ref(module))
+    mref = weakref.ref(module)
+
+    def _post_accumulate(p):
+        m = mref()
+        pend = m.__dict__.get("_sgd_pend") if m is not None else None
+        if pend is None:
+            return
+        if pend["gid"] is None:  # the COO of the last backward, now p.grad
+            pend["gid"], pend["gver"] = id(p.grad), p.grad._version
+        else:  # accumulated into again: the optimizer adds the sum itself
+            m._sgd_pend = None
+
+    weight.register_post_accumulate_grad_hook(_post_accumulate)
+
+
 # grad_mode "sparse": the rows an optimizer changed are synced by the next forward's own launch
 # (dqrm_emb_fwd_after_update); DQRM_FUSE_SYNC=0 issues dqrm_rows_changed as a call of its own (A/B)
 _FUSE_SYNC = os.environ.get("DQRM_FUSE_SYNC", "1") != "0"
@@ -202,7 +271,8 @@ class _WeightHolder(nn.Module):
 # per-call bookkeeping attributes of the modules: plain instance attributes, written without
 # nn.Module.__setattr__'s parameter / buffer / submodule checks (the drivers call 26 modules a
 # step, and the hooks reset these for every module)
-_PLAIN_ATTRS = frozenset({"_pending", "_ready", "_rr", "_ext_rows", "_counters", "_exchange", "_dqrm_err_calls"})
+_PLAIN_ATTRS = frozenset({"_pending", "_ready", "_rr", "_ext_rows", "_counters", "_exchange", "_dqrm_err_calls",
+                          "_sgd_pend"})
 
 
 class _QuantEmbeddingBase(nn.Module):
@@ -232,6 +302,8 @@ class _QuantEmbeddingBase(nn.Module):
         self._rr = None           # ranking range: (bits host int32 [T], bits dev, scale dev) of this step
         self._ext_rows = []       # rows of the sparse grads handed to an optimizer since the last sync
                                   # (grad_mode "sparse"; several with gradient accumulation)
+        self._sgd_pend = None     # grad_mode "sparse": the last backward's (batch, dy, ...) for the
+                                  # fused optimizer step (_sgd_step_pre_hook)
 
     def _sync_external_update(self) -> None:
         """grad_mode "sparse": the optimizer stepped W on the rows of the last COO outside
@@ -302,7 +374,28 @@ class _QuantEmbeddingBase(nn.Module):
         rows, vals = self._tset.lookup_grad(batch, dy, ste=ste, layout=layout,
                                             presum=_SPARSE_GRAD_FORM == "presummed")
         self._ext_rows.append(rows)
+        # the fused optimizer step applies this update if the COO reaches a plain SGD step as
+        # the weight's whole gradient (nothing accumulated before it: .grad is None now)
+        self._sgd_pend = (dict(batch=batch, dy=dy, ste=ste, layout=layout, rows=rows, gid=None, gver=None)
+                          if _SGD_HOOK and self.embedding_bag.weight.grad is None else None)
         return torch.sparse_coo_tensor(rows.view(1, -1), vals, (self._tset.R, self._tset.D), is_coalesced=False)
+
+    def _apply_pending_sgd(self, p: nn.Parameter, lr: float) -> bool:
+        """Called before a plain torch.optim.SGD step over `p` (this module's weight): if p.grad
+        is still exactly the COO of the last backward, apply W -= lr * grad with torch's sparse
+        SGD rounding per lookup in lookup order (dqrm_emb_bwd_sgd: the |W| hierarchy and INT4
+        rows kept too), and clear p.grad so the optimizer skips it. Returns whether it did."""
+        pend, self._sgd_pend = self._sgd_pend, None
+        g = p.grad
+        if (pend is None or g is None or pend["gid"] != id(g) or g._version != pend["gver"]
+                or self.grad_mode != "sparse"):
+            return False
+        self._ext_rows = [r for r in self._ext_rows if r is not pend["rows"]]
+        self._sync_external_update()  # rows an earlier optimizer step changed, first
+        self._tset.backward_sgd(pend["batch"], pend["dy"], lr, ste=pend["ste"], repack=self._use_packed(False),
+                                layout=pend["layout"])
+        p.grad = None
+        return True
 
 
 class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
@@ -343,6 +436,7 @@ class QuantEmbeddingBagTwo(_QuantEmbeddingBase):
         self.register_buffer("emb_scaling_factor", torch.zeros(1, device=dev), persistent=True)
         self.register_buffer("gradient_bit_width", torch.zeros(1, device=dev), persistent=True)
         self.embedding_bag = _WeightHolder(nn.Parameter(self._tset.W, requires_grad=True))
+        _register_sgd_owner(self, self.embedding_bag.weight)
 
     def __repr__(self):
         s = super().__repr__()
@@ -499,6 +593,7 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
         self.register_buffer("emb_scaling_factor", torch.zeros(T, device=dev), persistent=True)
         self.register_buffer("gradient_bit_width", torch.zeros(T, device=dev), persistent=True)
         self.embedding_bag = _WeightHolder(nn.Parameter(self._tset.W, requires_grad=True))
+        _register_sgd_owner(self, self.embedding_bag.weight)
 
     def table_weight(self, t: int) -> torch.Tensor:
         return self._tset.table_weight(t)
@@ -532,4 +627,5 @@ class QuantEmbeddingBagCollection(_QuantEmbeddingBase):
 
 
 __all__ = ["QuantEmbeddingBagTwo", "QuantEmbeddingBagCollection", "set_default_grad_mode", "set_sparse_grad_form",
+           "set_fused_optimizer_step",
            "set_error_check_interval", "set_pooling_one_inputs", "consolidate_tables", "can_consolidate"]

@@ -89,42 +89,52 @@ def test_quant_embedding_bag_two_forward_and_sparse_grad(dq, per_lookup_grads):
     assert m.embedding_bag.weight.shape == (n, D)
 
 
-def test_sparse_grad_sgd_step_matches_kaggle_pool1(dq, golden_dir):
+@pytest.mark.parametrize("fused_step", [True, False])
+def test_sparse_grad_sgd_step_matches_kaggle_pool1(dq, golden_dir, fused_step):
     """The single-GPU driver unchanged (dlrm_s_pytorch_single_gpu.py:1943-1950): 26
-    QuantEmbeddingBagTwo(grad_mode="sparse") + torch.optim.SGD(lr=0.1).step() on their
-    default (presummed, deterministic) COO grads, against kaggle_pool1.npz (the reference's
-    modules + SGD in torch-CPU). The first forward is bit-exact. W: ATen-ROCm's sparse add
-    of the row sums and torch-CPU's per-lookup add round differently, so W (|W| <= 0.58 here) and the
-    later forwards, whose table scale follows max|W|, are held to 1e-6 absolute (most
-    elements agree to the bit). The |W| maxima follow ATen's writes (dqrm_rows_changed)."""
+    QuantEmbeddingBagTwo(grad_mode="sparse") + torch.optim.SGD(lr=0.1).step(), against
+    kaggle_pool1.npz (the reference's modules + SGD in torch-CPU). fused_step (default): the
+    SGD step runs as the modules' own per-lookup update (the optimizer pre-step hook), so every
+    forward, scale and W is bit-exact with the fixture. Without it, ATen-ROCm adds the
+    presummed COO: W and the later forwards (whose scale follows max|W|) are held to 1e-6
+    absolute (row sums round differently from torch-CPU's per-lookup adds)."""
     import os
     from test_oracle_golden import regen_single
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
 
     fx = dict(np.load(os.path.join(golden_dir, "kaggle_pool1.npz")))
     Ws, batches, dys = regen_single(fx)
-    mods = nn.ModuleList([_qebt(w.shape[0], w.shape[1], w, grad_mode="sparse") for w in Ws])
-    opt = torch.optim.SGD([m.embedding_bag.weight for m in mods], lr=float(fx["lr"]))
-    for k, ((idxs, offs), dy) in enumerate(zip(batches, dys)):
-        opt.zero_grad()
-        ys = [m(torch.from_numpy(i).cuda(), torch.from_numpy(o).cuda()) for m, i, o in zip(mods, idxs, offs)]
-        for t, (m, y) in enumerate(zip(mods, ys)):
-            if k == 0:  # from the fixture's own tables: bit-exact
-                np.testing.assert_array_equal(y.detach().cpu().numpy(), fx[f"y{k}"][t])
-                assert m.eb_scaling_factor.item() == fx[f"s{k}"][t]
-            else:  # after ATen's update (see above): the table max, hence the scale, within 1e-6
-                np.testing.assert_allclose(y.detach().cpu().numpy(), fx[f"y{k}"][t], rtol=0, atol=1e-6)
-                np.testing.assert_allclose(m.eb_scaling_factor.item(), fx[f"s{k}"][t], rtol=1e-6)
-        torch.autograd.backward(ys, [torch.from_numpy(dy[t]).cuda() for t in range(len(ys))])
-        opt.step()
-    exact = total = 0
-    for t, m in enumerate(mods):
-        rows = fx[f"rows_t{t}"]
-        got = m.embedding_bag.weight.detach().cpu().numpy()[rows]
-        np.testing.assert_allclose(got, fx[f"w_t{t}"], rtol=0, atol=1e-6)
-        exact += int((got == fx[f"w_t{t}"]).sum())
-        total += got.size
-    assert exact > total // 2  # most elements still agree to the bit
-    assert all(m._tset.read_errors() == 0 for m in mods)
+    Q.set_fused_optimizer_step(fused_step)
+    try:
+        mods = nn.ModuleList([_qebt(w.shape[0], w.shape[1], w, grad_mode="sparse") for w in Ws])
+        opt = torch.optim.SGD([m.embedding_bag.weight for m in mods], lr=float(fx["lr"]))
+        for k, ((idxs, offs), dy) in enumerate(zip(batches, dys)):
+            opt.zero_grad()
+            ys = [m(torch.from_numpy(i).cuda(), torch.from_numpy(o).cuda()) for m, i, o in zip(mods, idxs, offs)]
+            for t, (m, y) in enumerate(zip(mods, ys)):
+                if k == 0 or fused_step:  # bit-exact
+                    np.testing.assert_array_equal(y.detach().cpu().numpy(), fx[f"y{k}"][t])
+                    assert m.eb_scaling_factor.item() == fx[f"s{k}"][t]
+                else:  # after ATen's update (see above): the table max, hence the scale, within 1e-6
+                    np.testing.assert_allclose(y.detach().cpu().numpy(), fx[f"y{k}"][t], rtol=0, atol=1e-6)
+                    np.testing.assert_allclose(m.eb_scaling_factor.item(), fx[f"s{k}"][t], rtol=1e-6)
+            torch.autograd.backward(ys, [torch.from_numpy(dy[t]).cuda() for t in range(len(ys))])
+            opt.step()
+            if fused_step:  # the modules applied their own updates; the optimizer added nothing
+                assert all(m.embedding_bag.weight.grad is None for m in mods)
+        exact = total = 0
+        for t, m in enumerate(mods):
+            rows = fx[f"rows_t{t}"]
+            got = m.embedding_bag.weight.detach().cpu().numpy()[rows]
+            if fused_step:
+                np.testing.assert_array_equal(got, fx[f"w_t{t}"])
+            np.testing.assert_allclose(got, fx[f"w_t{t}"], rtol=0, atol=1e-6)
+            exact += int((got == fx[f"w_t{t}"]).sum())
+            total += got.size
+        assert exact > total // 2  # most elements still agree to the bit
+        assert all(m._tset.read_errors() == 0 for m in mods)
+    finally:
+        Q.set_fused_optimizer_step(True)
 
 
 @pytest.mark.parametrize("form", ["bags", "criteo"])
@@ -170,10 +180,13 @@ def test_presummed_sparse_grad_is_the_coalesced_gradient(dq, form):
 
 def test_sparse_sgd_default_is_deterministic(dq):
     """The unchanged single-GPU driver (26-style per-table modules + torch.optim.SGD on their
-    COO grads, dlrm_s_pytorch_single_gpu.py:1943-1950) with the default presummed COO: two
-    identical runs give bit-identical W over 4 steps on tables of 3..100k rows with heavy
-    duplicates (ATen's scatter-add of the per-lookup form varies there), and W stays within
-    1e-5 (relative) of the per-lookup (reference) form's result."""
+    COO grads, dlrm_s_pytorch_single_gpu.py:1943-1950), 4 steps on tables of 3..100k rows
+    with heavy duplicates (~700 lookups per row of the 3-row table, dy x 10). Default (the
+    fused optimizer step): W equals the oracle's torch sparse SGD -- -lr * g of every lookup
+    added in lookup order (oracle.emb_bwd_sgd) -- bit for bit, hence is deterministic. With the
+    fused step off, ATen adds the presummed COO: two runs are bit-identical and W is within
+    1e-5 relative of the oracle (row sums round differently); the per-lookup COO is the reference's
+    own (ATen's atomic scatter-add orders its duplicates run to run)."""
     from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
 
     rows, D, B = [3, 10, 27, 5000, 100000], 16, 2048
@@ -181,8 +194,9 @@ def test_sparse_sgd_default_is_deterministic(dq):
     P = [G.pooling_one(rows, B, 50 + k, dist="zipf") for k in range(4)]
     dys = [G.upstream_grad(len(rows), B, D, 60 + k) * 10 for k in range(4)]
 
-    def run(form):
+    def run(form, fused):
         Q.set_sparse_grad_form(form)
+        Q.set_fused_optimizer_step(fused)
         try:
             mods = nn.ModuleList([_qebt(n, D, w, grad_mode="sparse") for n, w in zip(rows, Ws)])
             opt = torch.optim.SGD([m.embedding_bag.weight for m in mods], lr=0.1)
@@ -193,14 +207,64 @@ def test_sparse_sgd_default_is_deterministic(dq):
                 torch.autograd.backward(ys, [torch.from_numpy(dys[k][t]).cuda() for t in range(len(rows))])
                 opt.step()
             assert all(m._tset.read_errors() == 0 for m in mods)
-            return [m.embedding_bag.weight.detach().clone() for m in mods]
+            return [m.embedding_bag.weight.detach().cpu().numpy().copy() for m in mods]
         finally:
             Q.set_sparse_grad_form("presummed")
+            Q.set_fused_optimizer_step(True)
 
-    a, b, ref = run("presummed"), run("presummed"), run("per_lookup")
-    for x, y, z in zip(a, b, ref):
-        assert torch.equal(x, y)
-        torch.testing.assert_close(x, z, rtol=1e-5, atol=1e-5)  # |W| reaches ~7 here (dy x 10)
+    Wo = [w.copy() for w in Ws]
+    ar = np.arange(B, dtype=np.int64)
+    for k in range(4):
+        for t in range(len(rows)):
+            O.emb_bwd_sgd(Wo[t], P[k][t], ar, dys[k][t], O.table_scale(Wo[t], 4), 0.1)
+    fused = run("presummed", True)
+    for x, z in zip(fused, Wo):
+        np.testing.assert_array_equal(x, z)
+    a, b = run("presummed", False), run("presummed", False)
+    for x, y, z in zip(a, b, Wo):
+        np.testing.assert_array_equal(x, y)
+        np.testing.assert_allclose(x, z, rtol=1e-5, atol=1e-6)  # |W| reaches ~2 here (dy x 10)
+
+
+def test_fused_optimizer_step_falls_back_when_grad_changes(dq):
+    """The fused optimizer step applies only the COO the last backward produced, as is: a
+    gradient accumulated over two backwards, a grad edited in place, or an optimizer with
+    another optimizer (Adagrad) get the optimizer's own step on the COO (the module then syncs
+    its |W| maxima)."""
+    from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
+
+    n, D, B = 300, 16, 256
+    W = G.table_weights([n], D, 3)[0]
+    P = [G.pooling_one([n], B, 70 + k)[0] for k in range(2)]
+    dy = [G.upstream_grad(1, B, D, 80 + k)[0] for k in range(2)]
+    off = torch.arange(B, device="cuda")
+
+    def step(kind):
+        m = _qebt(n, D, W, grad_mode="sparse")
+        opt = (torch.optim.Adagrad([m.embedding_bag.weight], lr=0.1) if kind == "adagrad"
+               else torch.optim.SGD([m.embedding_bag.weight], lr=0.1))
+        opt.zero_grad()
+        for k in range(2 if kind == "accumulate" else 1):
+            m(torch.from_numpy(P[k]).cuda(), off).backward(torch.from_numpy(dy[k]).cuda())
+        g = m.embedding_bag.weight.grad
+        if kind == "scaled":
+            g.mul_(0.5)
+        expect = m.embedding_bag.weight.detach().clone()
+        if kind != "adagrad":  # what SGD's add of the (accumulated / scaled) COO gives
+            expect.add_(g.coalesce(), alpha=-0.1)
+        opt.step()
+        got = m.embedding_bag.weight.detach().clone()
+        return m, got, expect
+
+    for kind in ("accumulate", "scaled"):
+        m, got, expect = step(kind)
+        torch.testing.assert_close(got, expect, rtol=0, atol=1e-6)
+        assert m._sgd_pend is None
+        y = m(torch.from_numpy(P[0]).cuda(), off)  # the next forward's scale follows the changed rows
+        assert m.eb_scaling_factor.item() == O.table_scale(got.cpu().numpy(), 4)
+    m, got, _ = step("adagrad")  # not SGD: the optimizer's own step ran (grad kept)
+    assert m.embedding_bag.weight.grad is not None
+    assert not torch.equal(got, torch.from_numpy(W).cuda())
 
 
 def test_quant_embedding_bag_two_fused_sgd(dq):

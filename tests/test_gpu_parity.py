@@ -391,6 +391,7 @@ def test_presum_understated_max_lookups_is_flagged(dq):
     idxs = [rng.integers(0, n, size=l).astype(np.int64) for n, l in zip(rows, lens)]
     offs = [np.arange(l, dtype=np.int64)[:: max(1, l // 8)][:8] for l in lens]  # 8 bags per table
     ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=5)
+    ts.scale.fill_(0.03)  # the STE's forward scale (no forward ran)
     b = to_batch(dq, idxs, offs)
     b.c.max_lookups = 100  # understated: table 0 has 3000 lookups
     dy = torch.from_numpy(G.upstream_grad(2, 8, D, 9)).cuda()
@@ -405,6 +406,7 @@ def test_presum_understated_max_lookups_is_flagged(dq):
     assert torch.equal(v[:3000], torch.zeros(3000, D, device="cuda"))
     b2 = to_batch(dq, idxs[1:], offs[1:])  # table 1 alone, through the normal path
     ts1 = ts.view(1)
+    ts1.scale.fill_(0.03)
     r1, v1 = ts1.lookup_grad(b2, dy[1:].contiguous(), presum=True)
     assert torch.equal(r[3000:] - ts.row_base[1], r1 - ts1.row_base[0])
     assert torch.equal(v[3000:], v1)

@@ -2,7 +2,7 @@
 k_table_apply, each + k_table_finalize) for N emulated ranks on
 one GPU: N different ranks' payloads (coalesce + quant-pack of N different batch slices)
 gathered into one buffer, exactly what the RCCL all-gather delivers at N GPUs.
-usage: python tools/bench_apply_ranks.py [terabyte|kaggle]   -> one JSON line per N"""
+usage: python tools/bench_apply_ranks.py [terabyte|kaggle] [flat,slot,ranges] [B per rank] -> one JSON line per N"""
 import json
 import os
 import sys
@@ -22,10 +22,13 @@ rows = [n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS] if cfg == "ter
 B = 2048
 T = len(rows)
 ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
-ex = dq.SparseGradExchange(ts, B, grad_bits=8)
 lib = L.load()
-for mode, N in [(m, n) for m in ("flat", "slot") for n in (1, 2, 4, 8)]:
-    lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT if mode == "flat" else L.DQRM_APPLY_SLOT)
+KINDS = {"flat": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT, "ranges": L.DQRM_APPLY_RANGES}
+modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["flat", "slot", "ranges"]
+B = int(sys.argv[3]) if len(sys.argv) > 3 else B
+ex = dq.SparseGradExchange(ts, B, grad_bits=8)
+for mode, N in [(m, n) for m in modes for n in (1, 2, 4, 8)]:
+    lib.dqrm_set_apply_kernel(KINDS[mode])
     gathered = torch.zeros(N, ex.payload_bytes, dtype=torch.uint8, device="cuda")
     for r in range(N):
         P = torch.stack([torch.randint(0, n, (B,), device="cuda") for n in rows])
