@@ -147,7 +147,9 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "bwd_sgd": ("k_sgd_small<{lpr}, false>", "k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "bwd_sgd_fwd": ("k_sgd_small<{lpr}, true>",),  # ... with the next batch's forward in the launch
     "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
-    "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_ranges<{lpr}>"),
+    "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_merge<{lpr}, false>", "k_apply_ranges<{lpr}>"),
+    # N > 1 at the step boundary: the apply of step i + the forward of step i+1 in one launch
+    "apply_sparse_update_fwd": ("k_apply_merge<{lpr}, true>",),
     "apply_local": "k_apply_local<{lpr},",
 }
 
@@ -208,6 +210,8 @@ def alg_bytes(phase, T, B, D, U, world=1, pool1=True, repack=False):
                                + L * (D * 4 + 8) + offs + L * D * 4 + T * 4,
         "grad_quant_pack": U * (D * 4 + 4) + U * (D + 4),
         "apply_sparse_update": world * U * (D + 4) + U * D * 8 + U * 4 + pk,
+        "apply_sparse_update_fwd": world * U * (D + 4) + U * D * 8 + U * 4 + pk + L * (D * 4 + 8) + offs
+                                   + L * D * 4 + T * 4,
         "apply_local": U * (D * 4 + 4) + U * D * 8 + U * 4 + pk,
     }[phase]
 
@@ -225,10 +229,12 @@ def timed_events(n):
     return [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
 
 
-def phase_names(mode, use_packed, fused, one_launch=False, next_fwd=False):
+def phase_names(mode, use_packed, fused, one_launch=False, next_fwd=False, coll_fwd=False):
     fwd = "emb_fwd_packed" if use_packed else "emb_fwd"
     if mode == "fwd":
         return [fwd]
+    if coll_fwd:  # N > 1: the apply of step i and the forward of step i+1 in one launch
+        return ["bwd_coalesce", "grad_quant_pack", "apply_sparse_update_fwd"]
     if mode == "sgd":
         return ["bwd_sgd_fwd"] if next_fwd else [fwd, "bwd_sgd"]
     if fused and one_launch and next_fwd:
@@ -320,7 +326,11 @@ def main():
     # kernel takes the update, config 3)
     if a.mode == "sgd" and not a.use_packed and not a.separate_forward and len(batches) > 1:
         next_fwd = ts.sgd_fwd_is_one_launch(batches[0], batches[1])  # else the forward as its own phase
-    names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd)
+    # N > 1 (or forced): the apply of step i and the forward of step i+1 in one launch when the
+    # merge kernel takes the apply (dqrm_exchange_apply_fwd / dqrm_apply_sparse_update_fwd)
+    coll_fwd = (coll and a.mode == "dp" and not a.use_packed and not a.separate_forward and len(batches) > 1
+                and ex.apply_fwd_is_one_launch(batches[1]))
+    names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd, coll_fwd)
 
     # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
     # (dqrm_exchange_grad: coalesce + both all-gathers + quantize-pack; dqrm_exchange_apply);
@@ -339,6 +349,28 @@ def main():
             if ev is not None and (only is None or only == j):
                 ev[j][k].record()
 
+        if coll_fwd:  # this batch's forward ran in the previous step's apply launch; this one runs the next's
+            nxt = batches[(i + 1) % len(batches)]
+            rf = a.scale_period <= 0 or (i + 1) % a.scale_period == 0
+            if lib_exchange and not split:
+                ex.exchange(b, dy)
+                ex.apply_forward(a.lr, nxt, out=y, bits=4, refresh_scale=rf, mode=L.DQRM_UPD_DP)
+                return
+            kern = ex.kernels
+            mark(0, 0)
+            kern.coalesce(b, dy, ex.ws, True, "tbd")
+            mark(0, 1)
+            ex._all_gather(ex.absmax_all, ex.ws.absmax)
+            mark(1, 0)
+            kern.quant_pack(ex.ws, ex.absmax_all, ex.world, a.grad_bits, ex.cap_base, ex.cap_total, ex.s_avg,
+                            ex.payload)
+            mark(1, 1)
+            ex._all_gather(ex.gathered, ex.payload)
+            mark(2, 0)
+            kern.apply_fwd(ex.cap_base, ex.cap_total, ex.gathered, ex.payload_bytes, ex.world, a.grad_bits, ex.s_avg,
+                           a.lr, L.DQRM_UPD_DP, False, nxt, y, bits=4, refresh_scale=rf, workspace=ex.apply_ws)
+            mark(2, 1)
+            return
         if next_fwd:  # this batch's forward ran in the previous step's launch; this one runs the next's
             nxt = batches[(i + 1) % len(batches)]
             rf = a.scale_period <= 0 or (i + 1) % a.scale_period == 0
@@ -399,7 +431,7 @@ def main():
                    L.DQRM_UPD_DP, repack)
         mark(3, 1)
 
-    if next_fwd:  # the first batch's forward (every later one runs inside the previous step's launch)
+    if next_fwd or coll_fwd:  # the first batch's forward (every later one runs inside the previous step's launch)
         ts.forward(batches[0], bits=4, out=y)
     for i in range(a.warmup):
         step(i)
@@ -526,6 +558,8 @@ def main():
         replicas_match = True
     n1_update = ("SGD of step i + forward of step i+1 (dqrm_emb_bwd_sgd_fwd)" if a.mode == "sgd" and next_fwd else
                  None if a.mode != "dp" or world > 1 else
+                 "coalesce + quant-pack + payload apply with the next forward (RCCL at world size 1)"
+                 if coll and coll_fwd else
                  "coalesce + quant-pack + payload apply (RCCL at world size 1)" if coll else
                  "one launch: update of step i + forward of step i+1 (dqrm_emb_bwd_apply_fwd_local)" if next_fwd else
                  "one launch (dqrm_emb_bwd_apply_local)" if one_launch else
@@ -604,7 +638,10 @@ def main():
                 else "bwd_apply_local is ONE launch (coalesce, quantize, update and the |W| hierarchy)" if one_launch
                 else "apply_local = the fused quantize + update kernel + a short k_table_finalize launch" if fused
                 else "sgd = one launch (|W| hierarchy inside)" if a.mode == "sgd"
-                else "apply_sparse_update = " + L.apply_update_form() if a.mode == "dp" else "forward only"),
+                else "apply_sparse_update_fwd = the payload merge + update of this step and the next batch's forward, "
+                "one launch (k_apply_merge<LPR, true>: each table's forward once its update and |W| maxima are final)"
+                if coll_fwd
+                else "apply_sparse_update = " + L.apply_update_form(world) if a.mode == "dp" else "forward only"),
             "weight_syncc": ({"every": sync_every, "ms_per_call": round(sync_ms, 3),
                               "amortized_us_per_step": round(sync_ms * 1e3 / sync_every, 2),
                               "in_timed_region": True} if sync_every else None),
@@ -678,7 +715,16 @@ def emulate_main(a, dev):
     y = torch.empty(T, B, D, device=dev)
     torch.cuda.synchronize()
     setup_s = time.time() - t0
-    names = ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"]
+    # the apply of step i with the forward of step i+1 in one launch (dqrm_apply_sparse_update_fwd),
+    # as bench.py's N > 1 step runs it; --separate-forward: the forward as its own launch
+    import ctypes as C
+
+    aws = torch.zeros(max(16, int(ts.lib.dqrm_apply_workspace_bytes(N, ex.cap_total))), dtype=torch.uint8, device=dev)
+    fused = not a.separate_forward and ts.lib.dqrm_apply_fwd_is_one_launch(
+        C.byref(ts.c), N, ex.cap_total, aws.numel(), C.byref(per_rank[0][1 % nb].c),
+        ts._fwd_flags(True, False, False)) == 1
+    names = (["bwd_coalesce", "grad_quant_pack", "apply_sparse_update_fwd"] if fused
+             else ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"])
 
     def step(i, ev=None):
         k = i % nb
@@ -688,20 +734,29 @@ def emulate_main(a, dev):
             if ev is not None:
                 ev[j][e].record()
 
-        mark(0, 0)
-        ts.forward(b, bits=4, out=y)
-        mark(0, 1)
-        mark(1, 0)
+        j0 = 0
+        if not fused:
+            mark(0, 0)
+            ts.forward(b, bits=4, out=y)
+            mark(0, 1)
+            j0 = 1
+        mark(j0, 0)
         kern.coalesce(b, dys[0], wss[k], True, "tbd")  # maxima -> row 0 of the "gathered" maxima
-        mark(1, 1)
-        mark(2, 0)
+        mark(j0, 1)
+        mark(j0 + 1, 0)
         kern.quant_pack(wss[k], am_all[k], N, gb, ex.cap_base, ex.cap_total, ex.s_avg, gathered[k][0])
-        mark(2, 1)
-        mark(3, 0)
-        kern.apply(ex.cap_base, ex.cap_total, gathered[k], ex.payload_bytes, N, gb, ex.s_avg, a.lr, L.DQRM_UPD_DP,
-                   False)
-        mark(3, 1)
+        mark(j0 + 1, 1)
+        mark(j0 + 2, 0)
+        if fused:  # this step's update + the next step's forward
+            kern.apply_fwd(ex.cap_base, ex.cap_total, gathered[k], ex.payload_bytes, N, gb, ex.s_avg, a.lr,
+                           L.DQRM_UPD_DP, False, per_rank[0][(i + 1) % nb], y, workspace=aws)
+        else:  # the apply alone (with the merge workspace: the AUTO choice at N > 1)
+            kern.apply_fwd(ex.cap_base, ex.cap_total, gathered[k], ex.payload_bytes, N, gb, ex.s_avg, a.lr,
+                           L.DQRM_UPD_DP, False, None, y, workspace=aws)
+        mark(j0 + 2, 1)
 
+    if fused:
+        ts.forward(per_rank[0][0], bits=4, out=y)
     for i in range(a.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -733,7 +788,8 @@ def emulate_main(a, dev):
         "alg_bytes": {n: alg_bytes(n, T, B, D, U, N, pool1=True) for n in names},
         "distinct_rows_rank0": U,
         "payload_bytes_per_rank": int(ex.payload_bytes), "maxima_bytes_per_rank": T * S * 4,
-        "apply_update_form": L.apply_update_form(),
+        "apply_update_form": L.apply_update_form(N),
+        "step_launches": 3 if fused else 4, "forward_in_apply_launch": fused,
         "device_errors": err, "setup_s": round(setup_s, 1),
     }
     print(json.dumps(line), flush=True)

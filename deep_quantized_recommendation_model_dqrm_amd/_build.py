@@ -16,7 +16,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC_DIR = os.path.join(PKG_DIR, "csrc")
 SOURCES = [os.path.join(CSRC_DIR, f) for f in ("dqrm_kernels.hip", "dqrm_coalesce.hip", "dqrm_dense.hip",
                                                 "dqrm_input.hip", "dqrm_sync.hip", "dqrm_exchange.hip", "dqrm_lookup.hip",
-                                                "dqrm_comm.hip", "dqrm_apply.hip")]
+                                                "dqrm_comm.hip", "dqrm_apply.hip", "dqrm_apply_merge.hip")]
 DEVICE_HEADER = os.path.join(CSRC_DIR, "dqrm_device.h")
 HEADER = os.path.join(REPO_DIR, "include", "dqrm.h")
 INTERNAL_HEADER = os.path.join(CSRC_DIR, "dqrm_internal.h")

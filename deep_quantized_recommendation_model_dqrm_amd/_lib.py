@@ -41,6 +41,7 @@ DQRM_APPLY_AUTO = 0
 DQRM_APPLY_FLAT = 1
 DQRM_APPLY_SLOT = 2
 DQRM_APPLY_RANGES = 3
+DQRM_APPLY_MERGE = 4
 DQRM_COALESCE_AUTO = 0
 DQRM_COALESCE_GENERAL = 1
 
@@ -75,6 +76,9 @@ EXPORTED_SYMBOLS = (
     "dqrm_emb_local_update",
     "dqrm_apply_sparse_update",
     "dqrm_apply_sparse_update_strided",
+    "dqrm_apply_sparse_update_fwd",
+    "dqrm_apply_fwd_is_one_launch",
+    "dqrm_apply_workspace_bytes",
     "dqrm_apply_local",
     "dqrm_emb_bwd_apply_local",
     "dqrm_bwd_apply_local_is_one_launch",
@@ -102,6 +106,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_comm_allgather",
     "dqrm_exchange_grad",
     "dqrm_exchange_apply",
+    "dqrm_exchange_apply_fwd",
     "dqrm_emb_bwd_lookup_grad_presum",
     "dqrm_read_errors",
     "dqrm_last_error",
@@ -194,6 +199,8 @@ class Exchange(C.Structure):
         ("payload_bytes", C.c_size_t),
         ("workspace", C.c_void_p),
         ("workspace_bytes", C.c_size_t),
+        ("apply_ws", C.c_void_p),
+        ("apply_ws_bytes", C.c_size_t),
     ]
 
 
@@ -269,6 +276,13 @@ def load(path: str | None = None) -> C.CDLL:
             C.c_int,
             [TS, P, C.c_int64, P, C.c_size_t, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P],
         ),
+        "dqrm_apply_sparse_update_fwd": (
+            C.c_int,
+            [TS, P, C.c_int64, P, C.c_size_t, C.c_size_t, C.c_int, C.c_int, P, C.c_float, C.c_int, C.c_int, P,
+             C.c_size_t, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P],
+        ),
+        "dqrm_apply_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int64]),
+        "dqrm_apply_fwd_is_one_launch": (C.c_int, [TS, C.c_int, C.c_int64, C.c_size_t, BA, C.c_uint32]),
         "dqrm_apply_local": (
             C.c_int,
             [TS, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P],
@@ -314,6 +328,10 @@ def load(path: str | None = None) -> C.CDLL:
         "dqrm_comm_allgather": (C.c_int, [P, P, P, C.c_size_t, P]),
         "dqrm_exchange_grad": (C.c_int, [C.POINTER(Exchange), BA, P, C.c_int64, C.c_int64, C.c_int, P]),
         "dqrm_exchange_apply": (C.c_int, [C.POINTER(Exchange), C.c_float, C.c_int, C.c_int, P]),
+        "dqrm_exchange_apply_fwd": (
+            C.c_int,
+            [C.POINTER(Exchange), C.c_float, C.c_int, C.c_int, BA, C.c_int, C.c_uint32, P, C.c_int64, C.c_int64, P],
+        ),
         "dqrm_emb_bwd_lookup_grad_presum": (C.c_int, [TS, BA, P, C.c_int64, C.c_int64, C.c_int, P, P, P]),
         "dqrm_read_errors": (C.c_int, [TS, C.POINTER(C.c_uint32), C.c_int, P]),
         "dqrm_last_error": (C.c_char_p, []),
@@ -341,7 +359,7 @@ def check(rc: int, what: str) -> None:
         raise DQRMError(f"{what} failed ({rc}): {msg}")
 
 
-def apply_update_form() -> str:
-    """What dqrm_apply_sparse_update launches (for bench lines): the payload decode + update
-    kernel and where the |W| hierarchy is finalized."""
+def apply_update_form(num_ranks: int = 1) -> str:
+    """What dqrm_apply_sparse_update launches under AUTO (for bench lines): the payload decode +
+    update kernel and where the |W| hierarchy is finalized."""
     return "the payload decode + update kernel (k_apply_flat) + a short k_table_finalize launch"

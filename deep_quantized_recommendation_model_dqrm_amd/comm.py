@@ -75,16 +75,47 @@ class HipExchangeKernels:
             "dqrm_grad_quant_pack",
         )
 
-    def apply(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack):
-        """gathered [N, payload_bytes] may be a column slice of a wider gathered buffer."""
+    def apply(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack,
+              workspace=None):
+        """gathered [N, payload_bytes] may be a column slice of a wider gathered buffer. workspace:
+        the merge apply's positions (dqrm_apply_workspace_bytes; allocated here when None and the
+        merge kernels would take N > 1 ranks)."""
         t = self.tables
         pitch = gathered.stride(0) if gathered.dim() == 2 else payload_bytes
+        if num_ranks > 1:
+            if workspace is None:
+                n = int(self.lib.dqrm_apply_workspace_bytes(num_ranks, cap_total))
+                workspace = torch.zeros(max(n, 16), dtype=torch.uint8, device=t.device)
+            self.apply_fwd(cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack,
+                           None, None, workspace=workspace)
+            return
         L.check(
             self.lib.dqrm_apply_sparse_update_strided(
                 C.byref(t.c), _ptr(cap_base), cap_total, _ptr(gathered), payload_bytes, pitch, num_ranks,
                 grad_bits, _ptr(s_avg), float(lr), mode, 4 if repack else 0, _stream_handle()),
             "dqrm_apply_sparse_update",
         )
+
+    def apply_fwd(self, cap_base, cap_total, gathered, payload_bytes, num_ranks, grad_bits, s_avg, lr, mode, repack,
+                  next_batch, out, bits=4, refresh_scale=True, full_precision=False, layout="tbd", workspace=None):
+        """apply() followed by the next batch's forward (dqrm_apply_sparse_update_fwd): the update
+        and the forward in one update launch when the merge kernels take the apply
+        (apply_fwd_is_one_launch; N > 1 needs `workspace`, dqrm_apply_workspace_bytes). next_batch
+        None: the apply alone, with the workspace. Returns out."""
+        t = self.tables
+        pitch = gathered.stride(0) if gathered.dim() == 2 else payload_bytes
+        nb = C.byref(next_batch.c) if next_batch is not None else None
+        B = next_batch.num_bags if next_batch is not None else 0
+        ost, osb = (B * t.D, t.D) if layout == "tbd" else (t.D, t.T * t.D)
+        L.check(
+            self.lib.dqrm_apply_sparse_update_fwd(
+                C.byref(t.c), _ptr(cap_base), cap_total, _ptr(gathered), payload_bytes, pitch, num_ranks,
+                grad_bits, _ptr(s_avg), float(lr), mode, 4 if repack else 0, _ptr(workspace),
+                workspace.numel() if workspace is not None else 0, nb, int(bits),
+                t._fwd_flags(refresh_scale, False, full_precision), _ptr(out), ost, osb, _stream_handle()),
+            "dqrm_apply_sparse_update_fwd",
+        )
+        return out
 
     def apply_local(self, ws, grad_bits, s_avg, lr, repack):
         """world size 1: quant_pack + apply fused, straight from the workspace (no payload)."""
@@ -363,6 +394,10 @@ class SparseGradExchange:
                                                           device=dev)
         self.gathered = None if shared else torch.zeros(self.world, self.payload_bytes, dtype=torch.uint8,
                                                         device=dev)
+        # the merge apply's positions (N > 1; dqrm_apply_workspace_bytes), caller-owned
+        nws = (int(L.load().dqrm_apply_workspace_bytes(self.world, self.cap_total))
+               if self.coll and isinstance(self.kernels, HipExchangeKernels) else 0)
+        self.apply_ws = torch.zeros(max(nws, 16), dtype=torch.uint8, device=dev)
         # the library-issued step (dqrm_exchange_grad / _apply): two host calls per step, the
         # collectives from C on a dqrm_comm (libdqrm's RCCL communicator, or torch.distributed
         # through a callback); only with the HIP kernels and unshared buffers
@@ -405,6 +440,7 @@ class SparseGradExchange:
         x.payload_bytes = self.payload_bytes
         w = self.tables.bwd_workspace(self.max_lookups)
         x.workspace, x.workspace_bytes = w.data_ptr(), w.numel()
+        x.apply_ws, x.apply_ws_bytes = _ptr(self.apply_ws), self.apply_ws.numel()
         return x
 
     def _check(self, rc: int, what: str) -> None:
@@ -456,8 +492,52 @@ class SparseGradExchange:
                         "dqrm_exchange_apply")
             return
         gathered = self.gathered if self.coll else self.payload.view(1, -1)
+        kw = {"workspace": self.apply_ws} if isinstance(self.kernels, HipExchangeKernels) else {}
         self.kernels.apply(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world, gb, self.s_avg,
-                           lr, mode, repack)
+                           lr, mode, repack, **kw)
+
+    def apply_fwd_is_one_launch(self, next_batch: LookupBatch) -> bool:
+        """Whether apply_forward runs the update and the next batch's forward as ONE launch
+        (dqrm_apply_fwd_is_one_launch: the merge kernel takes this exchange's apply)."""
+        t = self.tables
+        rc = t.lib.dqrm_apply_fwd_is_one_launch(C.byref(t.c), self.world if self.coll else 1, self.cap_total,
+                                                self.apply_ws.numel(), C.byref(next_batch.c),
+                                                t._fwd_flags(True, False, False))
+        if rc < 0:
+            L.check(rc, "dqrm_apply_fwd_is_one_launch")
+        return rc == 1
+
+    def apply_forward(self, lr: float, next_batch: LookupBatch, out: torch.Tensor | None = None, bits: int = 4,
+                      refresh_scale: bool = True, full_precision: bool = False, layout: str = "tbd",
+                      mode: int | None = None, repack: bool = False) -> torch.Tensor:
+        """apply(lr) followed by tables.forward(next_batch): weight_update_parallel_comm of step i
+        and apply_emb of step i+1, adjacent in the DP loop (dlrm_s_pytorch_tb_dp_one_parallel_comm.py
+        :1888-1904); the same results, one launch when the merge kernel takes the apply
+        (dqrm_apply_sparse_update_fwd / dqrm_exchange_apply_fwd). Returns the next batch's output."""
+        gb = self.grad_bits
+        if mode is None:
+            mode = L.DQRM_UPD_FP32 if gb == 32 else L.DQRM_UPD_DP
+        t = self.tables
+        B = next_batch.num_bags
+        if out is None:
+            out = torch.empty((t.T, B, t.D) if layout == "tbd" else (B, t.T, t.D), dtype=torch.float32,
+                              device=t.device)
+        if self._x is not None:
+            ost, osb = (B * t.D, t.D) if layout == "tbd" else (t.D, t.T * t.D)
+            self._check(t.lib.dqrm_exchange_apply_fwd(
+                C.byref(self._x), float(lr), int(mode), 4 if repack else 0, C.byref(next_batch.c), int(bits),
+                t._fwd_flags(refresh_scale, False, full_precision), _ptr(out), ost, osb, _stream_handle()),
+                "dqrm_exchange_apply_fwd")
+            return out
+        fwd = getattr(self.kernels, "apply_fwd", None)
+        if fwd is None:
+            self.apply(lr, mode=mode, repack=repack)
+            return t.forward(next_batch, bits=bits, refresh_scale=refresh_scale, full_precision=full_precision,
+                             out=out, layout=layout)
+        gathered = self.gathered if self.coll else self.payload.view(1, -1)
+        return fwd(self.cap_base, self.cap_total, gathered, self.payload_bytes, self.world if self.coll else 1, gb,
+                   self.s_avg, lr, mode, repack, next_batch, out, bits=bits, refresh_scale=refresh_scale,
+                   full_precision=full_precision, layout=layout, workspace=self.apply_ws)
 
     def step(self, batch: LookupBatch, dy: torch.Tensor, lr: float, ste: bool = True,
              mode: int | None = None, repack: bool = False, layout: str = "tbd") -> None:
@@ -594,7 +674,8 @@ class MultiSetExchange:
         rp = list(repack) if isinstance(repack, (list, tuple)) else [bool(repack)] * len(self.parts)
         for i, p in enumerate(self.parts):
             g = self.gathered[:, self.pl_off[i]: self.pl_off[i + 1]] if N > 1 else p.payload.view(1, -1)
-            p.kernels.apply(p.cap_base, p.cap_total, g, p.payload_bytes, N, gb, p.s_avg, lr, mode, rp[i])
+            kw = {"workspace": p.apply_ws} if isinstance(p.kernels, HipExchangeKernels) else {}
+            p.kernels.apply(p.cap_base, p.cap_total, g, p.payload_bytes, N, gb, p.s_avg, lr, mode, rp[i], **kw)
 
     @property
     def collective_bytes(self) -> tuple[int, int]:

@@ -180,9 +180,21 @@ int dqrm_exchange_apply(const dqrm_exchange* x, float lr, int mode, int repack_b
     const int rc = check_exchange(x, "dqrm_exchange_apply");
     if (rc) return rc;
     const void* g = x->comm ? x->gathered : x->payload;
-    return dqrm_apply_sparse_update_strided(x->set, x->cap_base, x->cap_total, g, x->payload_bytes,
-                                            x->payload_bytes, x->num_ranks, x->grad_bits, x->s_avg, lr, mode,
-                                            repack_bits, stream);
+    return dqrm_apply_sparse_update_fwd(x->set, x->cap_base, x->cap_total, g, x->payload_bytes, x->payload_bytes,
+                                        x->num_ranks, x->grad_bits, x->s_avg, lr, mode, repack_bits, x->apply_ws,
+                                        x->apply_ws_bytes, nullptr, 0, 0u, nullptr, 0, 0, stream);
+}
+
+int dqrm_exchange_apply_fwd(const dqrm_exchange* x, float lr, int mode, int repack_bits, const dqrm_batch* next,
+                            int fwd_bits, uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                            void* stream) {
+    const int rc = check_exchange(x, "dqrm_exchange_apply_fwd");
+    if (rc) return rc;
+    const void* g = x->comm ? x->gathered : x->payload;
+    return dqrm_apply_sparse_update_fwd(x->set, x->cap_base, x->cap_total, g, x->payload_bytes, x->payload_bytes,
+                                        x->num_ranks, x->grad_bits, x->s_avg, lr, mode, repack_bits, x->apply_ws,
+                                        x->apply_ws_bytes, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b,
+                                        stream);
 }
 
 }  // extern "C"

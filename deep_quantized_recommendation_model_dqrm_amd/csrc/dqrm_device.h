@@ -96,6 +96,16 @@ DQRM_INLINE float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_R
 DQRM_INLINE uint32_t ld_wt(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// 16 bytes another workgroup of the launch stored write-through, as two 8-B agent-scope loads
+// (global_load_dwordx2 ... sc1: past this CU's L1, tracked by the compiler's vmcnt accounting;
+// a 64-bit address, unlike a buffer load's 32-bit offset). p 16-B aligned.
+DQRM_INLINE float4 ld4_wt(const float* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                       __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
+}
 // 16-B write-through store (global_store_dwordx4 ... sc1)
 DQRM_INLINE void st4_wt(float4* p, float4 v) {
     typedef float v4f __attribute__((ext_vector_type(4)));
@@ -220,7 +230,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             sblkmax[m.sblk_base[t]] = r;
             if (flag_get_h<WT>(sdirty, m.sblk_base[t])) flag_clear(sdirty, m.sblk_base[t]);
             if (flag_get_h<WT>(bdirty, m.blk_base[t])) flag_clear(bdirty, m.blk_base[t]);
-            tmax[t] = r;
+            if constexpr (WT) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups
         }
         return;
     }
@@ -352,7 +362,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     if (threadIdx.x == 0) {
         float r = 0.0f;
         for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
-        tmax[t] = r;
+        if constexpr (WT) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups (sc1)
     }
 }
 

@@ -165,4 +165,57 @@ struct RangeApplyArgs {
 };
 hipError_t launch_apply_ranges(const RangeApplyArgs& a, hipStream_t stream);
 
+// K6 with the ranks' rows merged on chip (dqrm_apply_merge.hip, DQRM_APPLY_MERGE): k_merge_pos
+// (workgroups own block-aligned row ranges, K_t chunks per row-range slot of table t, locate every
+// entry's row in the other ranks' runs in LDS) writes the positions; k_apply_pos updates, finalizes
+// the |W| hierarchy in-launch and (fwd_idx) runs the next batch's forward behind per-table gates.
+constexpr int kMergeMaxRanks = 16;
+constexpr int kMergeMaxTables = 64;
+struct MergeApplyArgs {
+    float* W;
+    uint8_t* packed;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    uint8_t* sdirty;
+    uint8_t* bdirty;
+    float* tmax;
+    uint32_t* sync;
+    const float* pscale;
+    const int64_t* meta;
+    uint32_t* err;
+    const int64_t* cap_base;
+    int64_t cap_total;
+    const unsigned char* payloads;  // rank r's payload at payloads + r * rank_pitch
+    int64_t rank_pitch;
+    int N;
+    int T;
+    int D;
+    int bits;
+    const float* s_avg;
+    float nlr;
+    int mode;
+    int repack;
+    int32_t* pos;                     // N > 1: [N][cap_total][N] workspace (apply_workspace_bytes)
+    int gx;                           // k_apply_pos: entry chunks per (table, rank)
+    int kt[kMergeMaxTables];          // k_merge_pos: chunks per row-range slot of table t
+    int kbase[kMergeMaxTables + 1];   //   first workgroup of table t (SPLIT * kt prefix)
+    // the next batch's forward in the same launch (fwd_idx null: none): Criteo-form indices
+    // [T][fwd_B], out[t*fwd_ost_t + b*fwd_ost_b + d], dqrm_emb_fwd's bits / flags
+    // (DQRM_FWD_REFRESH_SCALE, DQRM_FWD_FULL_PRECISION); fwd_gx workgroups per table
+    const int64_t* fwd_idx;
+    int64_t fwd_B;
+    float* fwd_out;
+    int64_t fwd_ost_t, fwd_ost_b;
+    float* fwd_scale;
+    int fwd_bits;
+    uint32_t fwd_flags;
+    int fwd_gx;
+    uint32_t spin_limit;              // gate polls before a forward workgroup flags DQRM_ERRF_STALL
+    int diag;                         // DQRM_MERGE_DIAG (timing experiments only; 0 in normal use)
+};
+hipError_t launch_apply_merge(const MergeApplyArgs& a, hipStream_t stream);
+int merge_forward_gx(int64_t B);
+size_t apply_workspace_bytes(int num_ranks, int64_t cap_total);
+
 }  // namespace dqrm_internal

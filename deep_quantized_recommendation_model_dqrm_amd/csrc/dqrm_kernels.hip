@@ -3839,7 +3839,8 @@ int apply_kernel_kind() {
     if (k < 0) {
         const char* e = getenv("DQRM_APPLY");
         k = (e && !strcmp(e, "flat")) ? DQRM_APPLY_FLAT : (e && !strcmp(e, "slot")) ? DQRM_APPLY_SLOT
-            : (e && !strcmp(e, "ranges")) ? DQRM_APPLY_RANGES : DQRM_APPLY_AUTO;
+            : (e && !strcmp(e, "ranges")) ? DQRM_APPLY_RANGES : (e && !strcmp(e, "merge")) ? DQRM_APPLY_MERGE
+            : DQRM_APPLY_AUTO;
         int expect = -1;
         g_apply_kernel.compare_exchange_strong(expect, k);
         k = g_apply_kernel.load();
@@ -4017,8 +4018,9 @@ int dqrm_set_coalesce_kernel(int kind) {
 }
 
 int dqrm_set_apply_kernel(int kind) {
-    if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_RANGES)
-        return set_error(DQRM_E_INVALID, "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat), 2 (slot) or 3 (ranges)");
+    if (kind < DQRM_APPLY_AUTO || kind > DQRM_APPLY_MERGE)
+        return set_error(DQRM_E_INVALID,
+                         "dqrm_set_apply_kernel: kind must be 0 (auto), 1 (flat), 2 (slot), 3 (ranges) or 4 (merge)");
     const int prev = apply_kernel_kind();
     g_apply_kernel.store(kind);
     return prev;
@@ -4445,10 +4447,153 @@ int dqrm_emb_local_update(const dqrm_table_set* set, const dqrm_batch* batch, co
     return launch_bwd<2>(c, (hipStream_t)stream, "dqrm_emb_local_update");
 }
 
+// recover the per-rank batch B from cap_total = sum_t min(B, n_t) (host row counts), -1 without them
+static int64_t recover_batch(const dqrm_table_set* set, int64_t cap_total) {
+    const int64_t* nr = set->num_rows_host;
+    if (!nr) return -1;
+    int64_t lo = 0, hi = 0;
+    for (int t = 0; t < set->num_tables; ++t) hi = nr[t] > hi ? nr[t] : hi;
+    while (lo < hi) {  // smallest B with sum_t min(B, n_t) >= cap_total
+        const int64_t mid = (lo + hi) / 2;
+        int64_t c = 0;
+        for (int t = 0; t < set->num_tables; ++t) c += nr[t] < mid ? nr[t] : mid;
+        if (c < cap_total) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// k_apply_pos: entry chunks per (table, rank) -- one pass of 4 entries per lane group covers the
+// largest table's capacity min(B, n_t) -- at most 32768 workgroups
+static int merge_apply_gx(const dqrm_table_set* set, int64_t cap_total, int num_ranks, int D) {
+    const int64_t per = (256 / (D / 4)) * 4;  // entries per workgroup: (lane groups) x AP_INFL
+    const int64_t B = recover_batch(set, cap_total);
+    const int64_t cmax = B >= 0 ? B : cap_total;
+    int64_t gx = (cmax + per - 1) / per;
+    const int64_t lim = (32768 + (int64_t)set->num_tables * num_ranks - 1) / ((int64_t)set->num_tables * num_ranks);
+    gx = gx > lim ? lim : gx;
+    return (int)(gx < 1 ? 1 : gx);
+}
+
+// Chunks per row-range slot of each table for k_apply_merge: about DQRM_MERGE_KEYS (default 256)
+// payload entries of all ranks per workgroup, from the table's payload capacity min(B, n_t)
+// (B recovered from cap_total = sum_t min(B, n_t) and the host row counts; without those, an
+// even split), at most the slot's blocks (chunks are block-aligned) and at most 64.
+static void merge_plan(const dqrm_table_set* set, int64_t cap_total, int N, int* kt, int* kbase) {
+    static const int64_t target = [] {
+        const char* e = getenv("DQRM_MERGE_KEYS");
+        const long v = e ? atol(e) : 256;
+        return (int64_t)(v > 0 ? v : 256);
+    }();
+    const int T = set->num_tables;
+    const int64_t* nr = set->num_rows_host;
+    int64_t B = -1;
+    if (nr) {  // smallest B with sum_t min(B, n_t) >= cap_total
+        int64_t lo = 0, hi = 0;
+        for (int t = 0; t < T; ++t) hi = nr[t] > hi ? nr[t] : hi;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            int64_t c = 0;
+            for (int t = 0; t < T; ++t) c += nr[t] < mid ? nr[t] : mid;
+            if (c < cap_total) lo = mid + 1; else hi = mid;
+        }
+        B = lo;
+    }
+    kbase[0] = 0;
+    for (int t = 0; t < T; ++t) {
+        const int64_t cap_t = B >= 0 ? (nr[t] < B ? nr[t] : B) : (cap_total + T - 1) / T;
+        int64_t K = ((int64_t)N * cap_t + SPLIT * target - 1) / (SPLIT * target);
+        if (nr) {
+            const int64_t blocks_per_slot = ((nr[t] + BLK - 1) / BLK + SPLIT - 1) / SPLIT;
+            K = K < blocks_per_slot ? K : blocks_per_slot;
+        }
+        K = K < 1 ? 1 : (K > 64 ? 64 : K);
+        kt[t] = (int)K;
+        kbase[t + 1] = kbase[t] + SPLIT * (int)K;
+    }
+}
+
+static int fwd_args(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags, float* out,
+                    int64_t out_stride_t, int64_t out_stride_b, const char* who, FwdArgs* a);
+
+// the apply's kernel choice: the merge kernels (with the next batch's forward in the update's
+// launch when nf is given) when DQRM_APPLY=merge / dqrm_set_apply_kernel(DQRM_APPLY_MERGE) and
+// the positions workspace is given (N = 1 needs none). Not AUTO: measured on the TB shape
+// (profiles/r6_apply_ranks_*.txt) it is not faster than the flat kernel + finalize launch at
+// N = 1..8 (2048 per rank: 20.6 / 53.4 / 75.8 / 143 us vs 15.4 / 39.4 / 68.0 / 138.8 us).
+static bool apply_uses_merge(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t ws_bytes) {
+    const int kind = apply_kernel_kind();
+    const bool ok = num_ranks <= dqrm_internal::kMergeMaxRanks && set->num_tables <= dqrm_internal::kMergeMaxTables &&
+                    ws_bytes >= dqrm_internal::apply_workspace_bytes(num_ranks, cap_total);
+    return ok && kind == DQRM_APPLY_MERGE;
+}
+
+size_t dqrm_apply_workspace_bytes(int num_ranks, int64_t cap_total) {
+    if (num_ranks <= 0 || cap_total < 0) return 0;
+    return dqrm_internal::apply_workspace_bytes(num_ranks, cap_total);
+}
+
+// the next batch's forward inside the merge kernel's launch: a Criteo-form batch on the exact
+// FP32 rows (the INT4 packed path stays a launch of its own); DQRM_FUSED_FWD=0 turns it off
+static bool merge_fwd_fits(const dqrm_batch* next, uint32_t flags) {
+    static const bool off = [] {
+        const char* e = getenv("DQRM_FUSED_FWD");
+        return e && !strcmp(e, "0");
+    }();
+    return !off && next && (next->flags & DQRM_BATCH_POOLING_ONE) && next->num_bags > 0 &&
+           next->max_lookups >= next->num_bags && !(flags & DQRM_FWD_USE_PACKED);
+}
+
+static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total, const void* payloads,
+                        size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
+                        float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
+                        void* stream);
+
 int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
                                      const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
                                      int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
                                      void* stream) {
+    return apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
+                        lr, mode, repack_bits, nullptr, 0, nullptr, stream);
+}
+
+int dqrm_apply_sparse_update_fwd(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                                 const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
+                                 int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
+                                 void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                                 uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                                 void* stream) {
+    if (workspace && (((uintptr_t)workspace) & 15))
+        return set_error(DQRM_E_INVALID, "%s: workspace must be 16-B aligned", "dqrm_apply_sparse_update_fwd");
+    if (!next)  // the apply alone, with the workspace
+        return apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
+                            lr, mode, repack_bits, workspace, workspace_bytes, nullptr, stream);
+    FwdArgs fa;  // the forward's arguments, validated as dqrm_emb_fwd validates them
+    int rc = fwd_args(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, "dqrm_apply_sparse_update_fwd",
+                      &fa);
+    if (rc) return rc;
+    if (apply_uses_merge(set, num_ranks, cap_total, workspace_bytes) && merge_fwd_fits(next, fwd_flags))
+        return apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
+                            lr, mode, repack_bits, workspace, workspace_bytes, &fa, stream);
+    if ((rc = apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
+                           lr, mode, repack_bits, workspace, workspace_bytes, nullptr, stream)))
+        return rc;
+    return dqrm_emb_fwd(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, stream);
+}
+
+int dqrm_apply_fwd_is_one_launch(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
+                                 const dqrm_batch* next, uint32_t fwd_flags) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(next, "dqrm_apply_fwd_is_one_launch"))) return rc;
+    if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS)
+        return set_error(DQRM_E_INVALID, "%s: bad ranks (%d)", "dqrm_apply_fwd_is_one_launch", num_ranks);
+    return apply_uses_merge(set, num_ranks, cap_total, workspace_bytes) && merge_fwd_fits(next, fwd_flags) ? 1 : 0;
+}
+
+static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total, const void* payloads,
+                        size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
+                        float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
+                        void* stream) {
     int rc = check_set(set);
     if (rc) return rc;
     if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS || !payloads || !cap_base)
@@ -4474,6 +4619,36 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
     const int D = set->dim;
     const int kind = apply_kernel_kind();
     bool flat = false;
+    // MERGE (AUTO for 1 < N <= 16 ranks, T <= 64 tables): the ranks' rows merged in LDS per
+    // block-aligned row range, the hierarchy finalized in-launch (dqrm_apply_merge.hip)
+    if (apply_uses_merge(set, num_ranks, cap_total, ws_bytes)) {
+        dqrm_internal::MergeApplyArgs r{};
+        r.W = a.W; r.packed = a.packed; r.rowmax = a.rowmax; r.blkmax = a.blkmax; r.sblkmax = a.sblkmax;
+        r.sdirty = a.sdirty; r.bdirty = a.bdirty; r.tmax = a.tmax; r.sync = a.sync; r.pscale = a.pscale;
+        r.meta = a.meta; r.err = a.err; r.cap_base = cap_base; r.cap_total = cap_total; r.payloads = a.payloads;
+        r.rank_pitch = (int64_t)rank_pitch; r.N = num_ranks; r.T = a.T; r.D = D; r.bits = grad_bits; r.s_avg = s_avg;
+        r.nlr = -lr; r.mode = mode; r.repack = a.repack;
+        merge_plan(set, cap_total, num_ranks, r.kt, r.kbase);
+        r.pos = reinterpret_cast<int32_t*>(ws);
+        static const int diag = [] {  // timing experiments: phases of k_merge_pos skipped (results wrong)
+            const char* e = getenv("DQRM_MERGE_DIAG");
+            return e ? atoi(e) : 0;
+        }();
+        r.diag = diag;
+        r.gx = merge_apply_gx(set, cap_total, num_ranks, D);
+        if (nf) {  // the next batch's forward: the grid's last T * fwd_gx workgroups, behind each table's gate
+            static const uint32_t spin = [] {  // DQRM_GATE_SPIN: gate polls before a forward flags a stall
+                const char* e = getenv("DQRM_GATE_SPIN");
+                return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 20);
+            }();
+            r.fwd_idx = nf->idx; r.fwd_B = nf->B; r.fwd_out = nf->out; r.fwd_ost_t = nf->ost_t; r.fwd_ost_b = nf->ost_b;
+            r.fwd_scale = set->scale; r.fwd_bits = nf->bits; r.fwd_flags = nf->flags;
+            r.fwd_gx = dqrm_internal::merge_forward_gx(nf->B); r.spin_limit = spin;
+        }
+        HIP_TRY(dqrm_internal::launch_apply_merge(r, st));
+        return DQRM_OK;  // the |W| hierarchy is finalized inside the launch
+    }
+    if (nf) return set_error(DQRM_E_INVALID, "%s: a fused forward needs the merge kernel", "dqrm_apply_sparse_update");
     if (kind == DQRM_APPLY_RANGES) {
         // chunks per slot: the payload capacity of all ranks spread over the slots, ~48
         // entries per workgroup (at least 1, at most 64)

@@ -60,7 +60,10 @@ extern "C" {
                                   dqrm_emb_bwd_sgd_fwd;
                               10: dqrm_comm_init_external (a caller-served all-gather under the
                                   same exchange orchestration), dqrm_comm_size,
-                                  dqrm_bwd_sgd_fwd_is_one_launch */
+                                  dqrm_bwd_sgd_fwd_is_one_launch, DQRM_APPLY_MERGE,
+                                  dqrm_apply_sparse_update_fwd, dqrm_apply_fwd_is_one_launch,
+                                  dqrm_apply_workspace_bytes, dqrm_exchange.apply_ws,
+                                  dqrm_exchange_apply_fwd */
 
 /* status codes */
 #define DQRM_OK            0
@@ -370,6 +373,31 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
                                      int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
                                      void* stream);
 
+/* dqrm_apply_sparse_update_strided on the gathered payloads, then dqrm_emb_fwd(set, next,
+ * fwd_bits, fwd_flags, out, out_stride_t, out_stride_b) on the NEXT batch -- the same results as
+ * those two calls (W, the |W| hierarchy, scale[] and out bit for bit). When the apply takes the
+ * merge kernel (DQRM_APPLY_MERGE / AUTO at 1 < num_ranks <= 16) and `next` is a Criteo-form
+ * batch without DQRM_FWD_USE_PACKED, the forward runs in the apply's launch: each table's
+ * forward workgroups start once that table's update and |W| maxima are final (no finalize or
+ * forward launch). Reference: weight_update_parallel_comm (s_q_g_p_c.py:601-628) and the next
+ * apply_emb (dlrm_s_pytorch_single_gpu.py:609-674, q_m_n_q_g.py:317-398). */
+int dqrm_apply_sparse_update_fwd(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
+                                 const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
+                                 int grad_bits, const float* s_avg, float lr, int mode, int repack_bits,
+                                 void* workspace, size_t workspace_bytes, const dqrm_batch* next, int fwd_bits,
+                                 uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                                 void* stream);
+
+/* Caller workspace of the merge apply at num_ranks > 1 (the positions of every entry's row in
+ * every rank's payload: num_ranks^2 * cap_total ints; 0 at one rank). dqrm_apply_sparse_update_fwd
+ * with a smaller workspace (or NULL) runs the flat apply kernel. next == NULL: the apply alone. */
+size_t dqrm_apply_workspace_bytes(int num_ranks, int64_t cap_total);
+
+/* 1 if dqrm_apply_sparse_update_fwd would run the update of num_ranks payloads (with that
+ * workspace) and the forward of `next` with ONE update launch, 0 if not, <0 on bad arguments. */
+int dqrm_apply_fwd_is_one_launch(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
+                                 const dqrm_batch* next, uint32_t fwd_flags);
+
 /* Single-rank DP step (num_ranks == 1, mode DQRM_UPD_DP), dqrm_grad_quant_pack and
  * dqrm_apply_sparse_update fused: the table scale s = clamp(max_s ws_absmax[t*S+s], 1e-8)
  * / (2^(bits-1)-1) (-> s_avg[t]), q = quantize(v, s) per coalesced entry, and
@@ -446,6 +474,13 @@ int dqrm_bwd_apply_fwd_local_is_one_launch(const dqrm_table_set* set, const dqrm
  * the table's last workgroup re-reduces flagged superblocks -- no finalize launch
  * (DQRM_APPLY=ranges) */
 #define DQRM_APPLY_RANGES 3
+/* MERGE (opt-in, DQRM_APPLY=merge; <= 16 ranks, <= 64 tables; N > 1 needs the positions
+ * workspace of dqrm_apply_sparse_update_fwd): k_merge_pos locates every entry's row in the other
+ * ranks' payloads in LDS per block-aligned row range, k_apply_pos updates one lane group per entry
+ * with the positions read in one load and finalizes the hierarchy in-launch; with a next batch its
+ * forward runs in that launch behind per-table gates. Bit-exact with FLAT; not faster on the TB
+ * shape, hence not AUTO. */
+#define DQRM_APPLY_MERGE 4
 int dqrm_set_apply_kernel(int kind);
 
 /* Which backward kernels dqrm_emb_bwd_coalesce and dqrm_emb_bwd_sgd launch (process-wide;
@@ -643,6 +678,9 @@ typedef struct dqrm_exchange {
     size_t payload_bytes;
     void* workspace;            /* backward scratch, dqrm_bwd_workspace_bytes(T, max_lookups) */
     size_t workspace_bytes;
+    void* apply_ws;             /* the merge apply's positions, dqrm_apply_workspace_bytes(num_ranks,
+                                   cap_total); NULL / too small: the flat apply kernel */
+    size_t apply_ws_bytes;
 } dqrm_exchange;
 
 /* grad_update_parallel_comm's embedding branch for all tables (s_q_g_p_c.py:257-317 via
@@ -655,6 +693,14 @@ int dqrm_exchange_grad(const dqrm_exchange* x, const dqrm_batch* batch, const fl
 /* weight_update_parallel_comm's embedding branch (s_q_g_p_c.py:601-628): decode the gathered
  * payloads and apply (dqrm_apply_sparse_update_strided with mode / repack_bits). */
 int dqrm_exchange_apply(const dqrm_exchange* x, float lr, int mode, int repack_bits, void* stream);
+
+/* dqrm_exchange_apply followed by the NEXT batch's forward, dqrm_emb_fwd(x->set, next, fwd_bits,
+ * fwd_flags, out, out_stride_t, out_stride_b): dqrm_apply_sparse_update_fwd on the gathered
+ * payloads -- the update of step i and apply_emb of step i+1, adjacent in the DP loop
+ * (dlrm_s_pytorch_tb_dp_one_parallel_comm.py:1888-1904, then the next iteration's forward). */
+int dqrm_exchange_apply_fwd(const dqrm_exchange* x, float lr, int mode, int repack_bits, const dqrm_batch* next,
+                            int fwd_bits, uint32_t fwd_flags, float* out, int64_t out_stride_t, int64_t out_stride_b,
+                            void* stream);
 
 /* dqrm_emb_bwd_lookup_grad with duplicate rows pre-summed: same rows[], but vals[j] is the
  * sum, in lookup order, of the STE'd dy rows of every lookup of row idx[j] when j is the

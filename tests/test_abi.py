@@ -44,8 +44,8 @@ def test_struct_layouts():
     # dqrm_table_set: 2 x i32 + 3 x i64 + 15 pointers (the last a host array); dqrm_batch: 3 pointers + 2 x i64
     assert C.sizeof(L.TableSet) == 8 + 24 + 15 * 8
     assert C.sizeof(L.Batch) == 6 * 8
-    # dqrm_exchange: 2 pointers + 2 x i32 + 15 eight-byte fields
-    assert C.sizeof(L.Exchange) == 2 * 8 + 8 + 15 * 8
+    # dqrm_exchange: 2 pointers + 2 x i32 + 17 eight-byte fields
+    assert C.sizeof(L.Exchange) == 2 * 8 + 8 + 17 * 8
 
 
 def test_invalid_arguments_rejected_without_device(lib):
@@ -156,8 +156,9 @@ def test_apply_kernel_selector(lib):
     try:
         assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_SLOT
         assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_RANGES) == L.DQRM_APPLY_FLAT
-        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_RANGES
-        assert lib.dqrm_set_apply_kernel(4) == L.DQRM_E_INVALID
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_MERGE) == L.DQRM_APPLY_RANGES
+        assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT) == L.DQRM_APPLY_MERGE
+        assert lib.dqrm_set_apply_kernel(5) == L.DQRM_E_INVALID
         assert b"kind" in lib.dqrm_last_error()
         assert lib.dqrm_set_apply_kernel(L.DQRM_APPLY_AUTO) == L.DQRM_APPLY_FLAT
     finally:

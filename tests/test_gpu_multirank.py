@@ -26,7 +26,7 @@ def _free_port() -> int:
     return port
 
 
-def _rank(rank, world, port, grad_bits, out_dir, transport="torch"):
+def _rank(rank, world, port, grad_bits, out_dir, transport="torch", fused_fwd=False):
     sys.path[:0] = [HERE, os.path.join(HERE, "golden"), os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "..")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,13 +60,26 @@ def _rank(rank, world, port, grad_bits, out_dir, transport="torch"):
             with torch.no_grad():
                 dex.exchange()
                 dex.apply(0.1)
+        batches = [dq.LookupBatch.pooling_one(torch.from_numpy(np.ascontiguousarray(
+            G.pooling_one(ROWS, B_GLOBAL, 50 + k, dist="zipf" if k % 2 else "uniform")[:, sl])).cuda())
+            for k in range(STEPS + 1)]
+        y = None
         for k in range(STEPS):
-            P = G.pooling_one(ROWS, B_GLOBAL, 50 + k, dist="zipf" if k % 2 else "uniform")
             dy = G.upstream_grad(len(ROWS), B_GLOBAL, D, 60 + k)
-            b = dq.LookupBatch.pooling_one(torch.from_numpy(np.ascontiguousarray(P[:, sl])).cuda())
-            ts.forward(b)
-            ex.step(b, torch.from_numpy(np.ascontiguousarray(dy[:, sl])).cuda(), lr=0.1)
+            b = batches[k]
+            dyt = torch.from_numpy(np.ascontiguousarray(dy[:, sl])).cuda()
+            if not fused_fwd:
+                ts.forward(b)
+                ex.step(b, dyt, lr=0.1)
+                continue
+            if k == 0:
+                ts.forward(b)
+            # the update of step k with the forward of step k+1 (dqrm_exchange_apply_fwd)
+            ex.exchange(b, dyt)
+            y = ex.apply_forward(0.1, batches[k + 1])
         torch.cuda.synchronize()
+        if fused_fwd:
+            np.save(os.path.join(out_dir, f"y{rank}.npy"), y.cpu().numpy())
         assert ts.read_errors() == 0
         if transport == "torch":  # both all-gathers of every step went through the C orchestration
             assert ex.dcomm.calls == STEPS * (2 if grad_bits != 32 else 1)
@@ -79,7 +92,7 @@ def _rank(rank, world, port, grad_bits, out_dir, transport="torch"):
 
 
 @pytest.mark.parametrize("grad_bits", [8, 32])
-@pytest.mark.parametrize("transport", ["torch", "python"])
+@pytest.mark.parametrize("transport", ["torch", "python", "torch_fused_fwd"])
 def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits, transport):
     """Two processes, the global batch sliced: every rank's tables and MLP layers equal
     oracle.dp_step / dense_dp_step over the whole batch, bit for bit. transport "torch":
@@ -94,7 +107,9 @@ def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits, transport):
     from deep_quantized_recommendation_model_dqrm_amd import get_my_slice
 
     world = 2
-    mp.spawn(_rank, args=(world, _free_port(), grad_bits, str(tmp_path), transport), nprocs=world, join=True)
+    fused = transport == "torch_fused_fwd"  # + the next batch's forward in the apply's launch (merge kernel)
+    mp.spawn(_rank, args=(world, _free_port(), grad_bits, str(tmp_path), "torch" if fused else transport, fused),
+             nprocs=world, join=True)
     Ws = G.table_weights(ROWS, D, 41)
     sls = [get_my_slice(B_GLOBAL, world, r) for r in range(world)]
     for k in range(STEPS):
@@ -113,6 +128,13 @@ def test_two_ranks_hip_exchange_matches_oracle(tmp_path, grad_bits, transport):
         got = np.load(os.path.join(tmp_path, f"r{r}.npz"))
         for t in range(len(ROWS)):
             np.testing.assert_array_equal(got[f"arr_{t}"], Ws[t])
+        if fused:  # the last fused forward: the next batch on the updated tables, with their scale
+            y = np.load(os.path.join(tmp_path, f"y{r}.npy"))
+            P = G.pooling_one(ROWS, B_GLOBAL, 50 + STEPS, dist="zipf" if STEPS % 2 else "uniform")[:, sls[r]]
+            for t in range(len(ROWS)):
+                yo, _ = O.emb_fwd(Ws[t], np.ascontiguousarray(P[t]), np.arange(P.shape[1], dtype=np.int64),
+                                  O.table_scale(Ws[t], 4))
+                np.testing.assert_array_equal(y[t], yo)
         for j, (W, b) in enumerate(params):
             np.testing.assert_array_equal(got[f"W{j}"], W)
             np.testing.assert_array_equal(got[f"b{j}"], b)

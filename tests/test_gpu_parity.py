@@ -29,12 +29,13 @@ def dq():
     return d
 
 
-@pytest.fixture(params=["flat", "slot", "ranges"])
+@pytest.fixture(params=["flat", "slot", "ranges", "merge"])
 def apply_kernel(request, dq):
     """Run the test once per dqrm_apply_sparse_update kernel (the AUTO choice depends on N)."""
     L = dq._lib
     lib = L.load()
-    kind = {"flat": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT, "ranges": L.DQRM_APPLY_RANGES}[request.param]
+    kind = {"flat": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT, "ranges": L.DQRM_APPLY_RANGES,
+            "merge": L.DQRM_APPLY_MERGE}[request.param]
     prev = lib.dqrm_set_apply_kernel(kind)
     yield request.param
     lib.dqrm_set_apply_kernel(prev)
@@ -1209,3 +1210,103 @@ def test_fused_sgd_next_forward_matches_separate_calls(dq, D, B, dist, form, ref
         assert torch.equal(y0, y1), it
         for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
             assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (it, name)
+
+
+def _payloads_for_ranks(dq, ts, rank_batches, rank_dys, grad_bits):
+    """Every rank's coalesce + quantize-pack on one GPU (the all-gathers become stacking), as
+    each rank of SparseGradExchange produces them; returns (payloads [N, P], s_avg, cap_base, cap_total)."""
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels, payload_bytes
+
+    N = len(rank_batches)
+    k = HipExchangeKernels(ts)
+    max_lookups = max(b.max_lookups for b in rank_batches)
+    wss = []
+    for r in range(N):
+        ws = dq.CoalescedGrad.allocate(ts.num_rows, max_lookups, ts.D, "cuda")
+        k.coalesce(rank_batches[r], rank_dys[r], ws, True, "tbd")
+        wss.append(ws)
+    absmax_all = torch.stack([ws.absmax for ws in wss])
+    caps = dq.default_caps(ts.num_rows, max_lookups)
+    cap_base = torch.tensor(np.concatenate([[0], np.cumsum(caps)]), dtype=torch.int64, device="cuda")
+    cap_total = int(sum(caps))
+    P = payload_bytes(ts.T, cap_total, ts.D, grad_bits)
+    payloads = torch.zeros(N, P, dtype=torch.uint8, device="cuda")
+    s_avg = torch.zeros(ts.T, dtype=torch.float32, device="cuda")
+    for r in range(N):
+        k.quant_pack(wss[r], absmax_all, N, grad_bits, cap_base, cap_total, s_avg, payloads[r])
+    return payloads, s_avg, cap_base, cap_total
+
+
+@pytest.mark.parametrize("N,D,B,dist,bits", [(1, 64, 2048, "uniform", 8), (2, 64, 1024, "zipf", 8),
+                                             (4, 16, 512, "uniform", 8), (8, 64, 256, "uniform", 8),
+                                             (8, 32, 300, "zipf", 16), (3, 64, 700, "uniform", 32)])
+def test_merge_apply_with_next_forward_matches_separate_calls(dq, N, D, B, dist, bits):
+    """dqrm_apply_sparse_update_fwd -- the merge apply of N ranks' payloads (DQRM_APPLY_MERGE,
+    AUTO at 1 < N <= 16) with the NEXT batch's forward in the same launch (each table's forward
+    workgroups wait at the table's gate until its update and |W| maxima are final) -- against
+    the flat apply + k_table_finalize + dqrm_emb_fwd on a copy of the tables, bit for bit over 3
+    steps: W, the |W| hierarchy, the forward scale and the next batch's output. Then the output
+    of the last step equals the oracle's forward of the updated tables (every table), and W
+    equals oracle.dp_step over the ranks. Reference: s_q_g_p_c.py:601-628,850-890 and apply_emb
+    (dlrm_s_pytorch_single_gpu.py:609-674)."""
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
+
+    lib = L.load()
+    rows = COAL_ROWS
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 171 + N)
+    Wo = [w.copy() for w in Ws]
+    sets = [make_set(dq, Ws) for _ in range(2)]
+    mode = L.DQRM_UPD_FP32 if bits == 32 else L.DQRM_UPD_DP
+    ar = np.arange(B, dtype=np.int64)
+    Pn = [[G.pooling_one(rows, B, 181 + 10 * k + r, dist=dist) for r in range(N)] for k in range(4)]
+    rank0 = [dq.LookupBatch.pooling_one(torch.from_numpy(Pn[k][0]).cuda()) for k in range(4)]
+    ys = [ts.forward(rank0[0]) for ts in sets]
+    assert torch.equal(ys[0], ys[1])
+    for k in range(3):
+        dys = [G.upstream_grad(T, B, D, 191 + 10 * k + r) * 30 for r in range(N)]
+        rb = [dq.LookupBatch.pooling_one(torch.from_numpy(Pn[k][r]).cuda()) for r in range(N)]
+        s_fwd = sets[0].scale.cpu().numpy().copy()
+        outs = []
+        for j, ts in enumerate(sets):
+            payloads, s_avg, cap_base, cap_total = _payloads_for_ranks(
+                dq, ts, rb, [torch.from_numpy(d).cuda() for d in dys], bits)
+            kern = HipExchangeKernels(ts)
+            if j == 0:
+                prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_MERGE)
+                try:
+                    ws = torch.zeros(max(16, int(lib.dqrm_apply_workspace_bytes(N, cap_total))), dtype=torch.uint8,
+                                     device="cuda")
+                    assert lib.dqrm_apply_fwd_is_one_launch(ts.c, N, cap_total, ws.numel(), rank0[k + 1].c,
+                                                            ts._fwd_flags(True, False, False)) == 1
+                    y = torch.empty(T, B, D, device="cuda")
+                    kern.apply_fwd(cap_base, cap_total, payloads, payloads.shape[1], N, bits, s_avg, 0.5, mode, False,
+                                   rank0[k + 1], y, workspace=ws)
+                finally:
+                    lib.dqrm_set_apply_kernel(prev)
+            else:
+                prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT)
+                try:
+                    kern.apply(cap_base, cap_total, payloads, payloads.shape[1], N, bits, s_avg, 0.5, mode, False)
+                finally:
+                    lib.dqrm_set_apply_kernel(prev)
+                y = ts.forward(rank0[k + 1])
+            outs.append(y)
+        assert [ts.read_errors() for ts in sets] == [0, 0], k
+        assert torch.equal(outs[0], outs[1]), k
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (k, name)
+        O.dp_step(Wo, [[(Pn[k][r][t], ar) for t in range(T)] for r in range(N)], [[dys[r][t] for t in range(T)]
+                                                                                   for r in range(N)],
+                  list(s_fwd), 0.5, grad_bits=bits)
+    y = outs[0].cpu().numpy()
+    s = sets[0].scale.cpu().numpy()
+    for t in range(T):
+        np.testing.assert_array_equal(sets[0].table_weight(t).cpu().numpy(), Wo[t])
+        assert s[t] == O.table_scale(Wo[t], 4)
+        np.testing.assert_array_equal(y[t], O.emb_fwd(Wo[t], Pn[3][0][t], ar, s[t])[0])
+    inc = [x.clone() for x in (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)]
+    sets[0].refresh_absmax()
+    for x, z in zip(inc, (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)):
+        assert torch.equal(x, z)
