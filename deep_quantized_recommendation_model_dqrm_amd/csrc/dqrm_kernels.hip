@@ -1738,6 +1738,7 @@ DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
 }
 
 constexpr int FLAT_TPB = 256;
+constexpr int FLAT_HDR_RANKS = 32;  // k_apply_flat: ranks whose slot bounds it keeps in LDS
 #ifndef DQRM_FLAT_PRELOAD
 #define DQRM_FLAT_PRELOAD 1  // 0: an A/B build reading the superblock / table max only on growth
 #endif
@@ -1920,7 +1921,28 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     const int64_t cb = a.cap_base[t];
     const int64_t cap = a.cap_base[t + 1] - cb;
     const unsigned char* pr = a.payloads + (int64_t)r * a.payload_bytes;
-    const int cnt_r = table_entry_count(pr, t, cap);
+    // N > 1: every rank's slot bounds of table t in LDS, ONE round trip (thread j*8+q loads rank
+    // j's slot-q count; clamped prefix sums in slot order): a row's entry in rank j is then
+    // searched within its slot's run only (~3 fewer dependent steps than the whole table's list)
+    __shared__ int s_sb[FLAT_HDR_RANKS][SPLIT + 1];
+    const bool slot_search = N > 1 && N <= FLAT_HDR_RANKS;
+    if (slot_search) {
+        if ((int)threadIdx.x < N * SPLIT) {
+            const int j = threadIdx.x / SPLIT, q = threadIdx.x % SPLIT;
+            int c = reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes)[t * SPLIT + q];
+            c = c > 0 ? c : 0;
+            int inc = c;  // inclusive prefix over the rank's 8 slots (8 aligned lanes of a wave)
+#pragma unroll
+            for (int o = 1; o < SPLIT; o <<= 1) {
+                const int y = __shfl_up(inc, o, SPLIT);
+                if (q >= o) inc += y;
+            }
+            s_sb[j][q + 1] = inc < cap ? inc : (int)cap;
+            if (q == 0) s_sb[j][0] = 0;
+        }
+        __syncthreads();
+    }
+    const int cnt_r = slot_search ? s_sb[r][SPLIT] : table_entry_count(pr, t, cap);
     if ((int64_t)blockIdx.x * G >= cnt_r) return;
     // workgroups of table t that work, over all ranks' payloads (each arrives once)
     uint32_t expected = 0;
@@ -1970,22 +1992,52 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
             acc = src.load((uint32_t)e, sub);
         } else {  // where the other ranks hold row x (lane k searches ranks k, k+LPR, ...)
             bool lower = false;
+            // the slot of row x (slot s holds blocks [nblk*s/8, nblk*(s+1)/8)): its run in each rank
+            const int64_t nblk = (nrows + BLK - 1) / BLK;
+            const int xs = slot_search ? (int)((8 * ((int64_t)(x >> 8) + 1) + nblk - 1) / nblk) - 1 : 0;
             for (int j = sub; j < N; j += LPR) {
                 int p = e;
                 if (j != r) {
                     const unsigned char* pj = a.payloads + (int64_t)j * a.payload_bytes;
-                    p = find_row(reinterpret_cast<const int32_t*>(pj + pl.rows_off) + cb, table_entry_count(pj, t, cap), x);
+                    const int32_t* rows_j = reinterpret_cast<const int32_t*>(pj + pl.rows_off) + cb;
+                    if (slot_search) {
+                        const int lo = s_sb[j][xs], hi = s_sb[j][xs + 1];
+                        const int q = find_row(rows_j + lo, hi - lo, x);
+                        p = q >= 0 ? lo + q : -1;
+                    } else {
+                        p = find_row(rows_j, table_entry_count(pj, t, cap), x);
+                    }
                     lower |= (j < r) && p >= 0;
                 }
                 pos[j] = p;  // LDS, read back by the same wave below (in-order LDS within a wave)
             }
             if (__ballot(lower) & gmask) continue;  // a lower rank owns this row (group-uniform)
             // owner: rank-ordered sum of the row's entries (ranks >= r)
-            bool first = true;
             acc = make_float4(0.f, 0.f, 0.f, 0.f);
-            for (int j = r; j < N; ++j) {
-                const int p = pos[j];
-                if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
+            if (pl.elem == 1 && N <= 8) {
+                // int8 values: every rank's loaded in one round trip (absent ranks read entry 0 and
+                // add +0 to the integer sum), then summed in ascending rank order (exact)
+                uint32_t raw[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = j < N ? pos[j] : -1;
+                    const bool ok = j >= r && p >= 0;
+                    raw[j] = reinterpret_cast<const uint32_t*>(a.payloads + (int64_t)(j < N ? j : 0) * a.payload_bytes +
+                                                               pl.vals_off + (cb + (ok ? p : 0)) * D)[sub];
+                    if (!ok) raw[j] = 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t v = raw[j];
+                    acc.x += (float)(int8_t)(v & 0xFF); acc.y += (float)(int8_t)((v >> 8) & 0xFF);
+                    acc.z += (float)(int8_t)((v >> 16) & 0xFF); acc.w += (float)(int8_t)(v >> 24);
+                }
+            } else {
+                bool first = true;
+                for (int j = r; j < N; ++j) {
+                    const int p = pos[j];
+                    if (p >= 0) acc = combine<OP_SUM>(acc, src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
+                }
             }
         }
         const bool owned = own_mode && (xlo < 0 || (xlo >> 8) != (x >> 8)) && (xhi < 0 || (xhi >> 8) != (x >> 8));
