@@ -464,7 +464,8 @@ def weight_syncc(dlrm, num_gpus, group=None) -> None:
     identical replicas is computable locally: a ring all-reduce (Gloo's ring_chunked on the
     reference's CPU ranks, RCCL's ring here) adds the ranks one after another, so every
     element becomes fl(fl(...fl(x + x) + x ...) * 1/N) (dqrm_replica_mean) -- x itself for
-    N = 1, 2, 4, an ulp away for about half of the elements at N = 3 or 8. So: one
+    N = 1, 2, 4, an ulp away for about half of the elements at N = 3 or 8 (pinned against
+    real Gloo at N = 3, 5, 6, 8 by tests/golden/syncc_gloo.npz). So: one
     all-gather of per-parameter checksums (dqrm_checksum64); if every rank holds the same
     bits, that local map (skipped where it is the identity) instead of the all-reduce --
     bit-exact with the reference and a few streaming passes over HBM instead of an

@@ -119,3 +119,17 @@ def mlp_grads(shapes, seed, rank, step):
         gb = (rs.standard_normal(o) * 10.0 ** rs.uniform(-3, -1)).astype(np.float32)
         out.append((gW, gb))
     return out
+
+
+# ---------------------------------------------------------------- weight_syncc replicas
+def replica_values(n, seed):
+    """f32 parameter values for the identical-replica weight_syncc fixtures: significands
+    uniform over all 2^23 mantissas, exponents over the f32 normal range a world of 8 can
+    sum without overflow, plus zeros, subnormals and values that overflow at 3..8 ranks."""
+    rs = np.random.RandomState(seed)
+    mant = rs.randint(0, 1 << 23, n).astype(np.uint32)
+    expo = rs.randint(1, 250, n).astype(np.uint32)  # up to 2^122
+    sign = rs.randint(0, 2, n).astype(np.uint32) << 31
+    x = (sign | (expo << 23) | mant).view(np.float32).copy()
+    x[:8] = np.array([0.0, -0.0, 1e-45, -3e-39, 1.0, 1.5, 3.0e38, -1.2e38], np.float32)
+    return x

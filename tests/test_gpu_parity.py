@@ -1310,3 +1310,23 @@ def test_merge_apply_with_next_forward_matches_separate_calls(dq, N, D, B, dist,
     sets[0].refresh_absmax()
     for x, z in zip(inc, (sets[0].rowmax, sets[0].blkmax, sets[0].sblkmax, sets[0].tmax)):
         assert torch.equal(x, z)
+
+
+@pytest.mark.parametrize("N", [3, 5, 6, 8])
+def test_replica_mean_matches_gloo_fixture(dq, golden_dir, N):
+    """dqrm_replica_mean (weight_syncc on identical replicas, s_q_g_p_c.py:963-970) = real
+    Gloo's all_reduce(SUM) * 1/N at N = 3, 5, 6, 8 (syncc_gloo.npz: every mantissa, exponents
+    up to 2^122, zeros, subnormals, overflow to inf), bit for bit, incl. a 1 Mi-element vector
+    (its checksum) and a length that is not a multiple of the kernel's vector width."""
+    lib = dq._lib.load()
+    fx = load(golden_dir, "syncc_gloo.npz")
+    inv = float(np.float32(1.0 / N))
+    for i, tag in enumerate(("small", "large")):
+        x = G.replica_values(int(fx["sizes"][i]), int(fx["seeds"][i]))
+        t = torch.from_numpy(x).cuda()
+        dq._lib.check(lib.dqrm_replica_mean(t.data_ptr(), t.numel(), N, inv, None), "dqrm_replica_mean")
+        got = t.cpu().numpy()
+        if tag == "small":
+            np.testing.assert_array_equal(got.view(np.uint32), fx[f"small_n{N}"].view(np.uint32))
+        else:
+            assert G.checksum(got) == str(fx[f"large_n{N}_checksum"])
