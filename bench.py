@@ -148,8 +148,10 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "bwd_sgd_fwd": ("k_sgd_small<{lpr}, true>",),  # ... with the next batch's forward in the launch
     "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
     "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_merge<{lpr}, false>", "k_apply_ranges<{lpr}>"),
-    # N > 1 at the step boundary: the apply of step i + the forward of step i+1 in one launch
-    "apply_sparse_update_fwd": ("k_apply_merge<{lpr}, true>",),
+    # N > 1 at the step boundary: the apply of step i + the forward of step i+1 in one launch (merge)
+    "apply_sparse_update_fwd": ("k_apply_pos<{lpr}, true>",),
+    # ... or the flat apply, then its finalize + the forward in one launch: a list = both kernels' sum
+    "apply_sparse_update_fwd_fin": ["k_apply_flat<{lpr},", "k_finalize_fwd<{lpr},"],
     "apply_local": "k_apply_local<{lpr},",
 }
 
@@ -167,15 +169,24 @@ def pmc_traffic(path, phase, D, workload=None):
     if workload is not None and summ.get("workload") != workload:
         return None
     sym = KERNEL_SYMBOL[phase]
-    prefixes = tuple(p.format(lpr=D // 4) for p in (sym if isinstance(sym, tuple) else (sym,)))
     kernels = summ["kernels"]
-    for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
-        if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
-            return {"bytes": round(v["hbm_bytes_per_launch"]), "correction": summ.get("correction"),
-                    "profiled_avg_us": round(v["avg_us"], 2),
-                    "profiled_median_us": round(v["median_us"], 2) if v.get("median_us") else None,
-                    "source": os.path.relpath(path, ROOT)}
-    return None
+
+    def one(alts):  # the first kernel matching one of the alternative prefixes
+        prefixes = tuple(p.format(lpr=D // 4) for p in alts)
+        for name, v in sorted(kernels.items(), key=lambda kv: [kv[0].startswith(p) for p in prefixes], reverse=True):
+            if name.startswith(prefixes) and v.get("hbm_bytes_per_launch") is not None:
+                return v
+        return None
+
+    # a list: the phase is several launches, their bytes and times summed; a tuple: alternatives
+    parts = [one((p,)) for p in sym] if isinstance(sym, list) else [one(sym if isinstance(sym, tuple) else (sym,))]
+    if any(v is None for v in parts):
+        return None
+    med = [v.get("median_us") for v in parts]
+    return {"bytes": round(sum(v["hbm_bytes_per_launch"] for v in parts)), "correction": summ.get("correction"),
+            "profiled_avg_us": round(sum(v["avg_us"] for v in parts), 2),
+            "profiled_median_us": round(sum(med), 2) if all(med) else None,
+            "source": os.path.relpath(path, ROOT)}
 
 
 def latest_profile(tag):
@@ -326,10 +337,12 @@ def main():
     # kernel takes the update, config 3)
     if a.mode == "sgd" and not a.use_packed and not a.separate_forward and len(batches) > 1:
         next_fwd = ts.sgd_fwd_is_one_launch(batches[0], batches[1])  # else the forward as its own phase
-    # N > 1 (or forced): the apply of step i and the forward of step i+1 in one launch when the
-    # merge kernel takes the apply (dqrm_exchange_apply_fwd / dqrm_apply_sparse_update_fwd)
-    coll_fwd = (coll and a.mode == "dp" and not a.use_packed and not a.separate_forward and len(batches) > 1
-                and ex.apply_fwd_is_one_launch(batches[1]))
+    # N > 1 (or forced): the apply of step i and the forward of step i+1 through one call
+    # (dqrm_exchange_apply_fwd / dqrm_apply_sparse_update_fwd) when it saves a launch: the merge
+    # kernel runs both in one launch, the flat kernel's finalize shares a launch with the forward
+    coll_form = (ex.apply_fwd_form(batches[1]) if coll and a.mode == "dp" and not a.use_packed
+                 and not a.separate_forward and len(batches) > 1 else "separate")
+    coll_fwd = coll_form != "separate"
     names = phase_names(a.mode, a.use_packed, fused, one_launch, next_fwd, coll_fwd)
 
     # N > 1 (or forced) over RCCL: the exchange is issued by libdqrm in two calls per step
@@ -568,7 +581,8 @@ def main():
                 "index_dist": a.index_dist}
     # (the forced-collectives N > 1 form is profiled under its own tag, e.g. r5_tbforced)
     prof = a.traffic_profile or latest_profile(PROFILE_TAG[a.config] + ("forced" if coll and world == 1 else ""))
-    traffic = pmc_traffic(prof, dom, D, workload)
+    traffic = pmc_traffic(prof, dom + ("_fin" if dom == "apply_sparse_update_fwd" and coll_form == "fin_fwd" else ""),
+                          D, workload)
     med_us = traffic["profiled_median_us"] if traffic else None
     if rank == 0:
         value = B_global * a.steps / elapsed
@@ -639,8 +653,12 @@ def main():
                 else "apply_local = the fused quantize + update kernel + a short k_table_finalize launch" if fused
                 else "sgd = one launch (|W| hierarchy inside)" if a.mode == "sgd"
                 else "apply_sparse_update_fwd = the payload merge + update of this step and the next batch's forward, "
-                "one launch (k_apply_merge<LPR, true>: each table's forward once its update and |W| maxima are final)"
-                if coll_fwd
+                "one launch (k_apply_pos<LPR, true>: each table's forward once its update and |W| maxima are final)"
+                if coll_form == "one_launch"
+                else "apply_sparse_update_fwd = the payload decode + update (k_apply_flat), then the |W| finalize and "
+                "the next batch's forward in one launch (k_finalize_fwd: each table's scale once its finalize "
+                "workgroup opened the table's gate)"
+                if coll_form == "fin_fwd"
                 else "apply_sparse_update = " + L.apply_update_form(world) if a.mode == "dp" else "forward only"),
             "weight_syncc": ({"every": sync_every, "ms_per_call": round(sync_ms, 3),
                               "amortized_us_per_step": round(sync_ms * 1e3 / sync_every, 2),
@@ -720,9 +738,9 @@ def emulate_main(a, dev):
     import ctypes as C
 
     aws = torch.zeros(max(16, int(ts.lib.dqrm_apply_workspace_bytes(N, ex.cap_total))), dtype=torch.uint8, device=dev)
-    fused = not a.separate_forward and ts.lib.dqrm_apply_fwd_is_one_launch(
-        C.byref(ts.c), N, ex.cap_total, aws.numel(), C.byref(per_rank[0][1 % nb].c),
-        ts._fwd_flags(True, False, False)) == 1
+    form = ts.lib.dqrm_apply_fwd_form(C.byref(ts.c), N, ex.cap_total, aws.numel(), C.byref(per_rank[0][1 % nb].c),
+                                      ts._fwd_flags(True, False, False))
+    fused = not a.separate_forward and form in (L.DQRM_APPLY_FWD_ONE_LAUNCH, L.DQRM_APPLY_FWD_FIN_FWD)
     names = (["bwd_coalesce", "grad_quant_pack", "apply_sparse_update_fwd"] if fused
              else ["emb_fwd", "bwd_coalesce", "grad_quant_pack", "apply_sparse_update"])
 
@@ -789,7 +807,11 @@ def emulate_main(a, dev):
         "distinct_rows_rank0": U,
         "payload_bytes_per_rank": int(ex.payload_bytes), "maxima_bytes_per_rank": T * S * 4,
         "apply_update_form": L.apply_update_form(N),
-        "step_launches": 3 if fused else 4, "forward_in_apply_launch": fused,
+        # coalesce, quantize-pack, then: merge (k_merge_pos at N > 1 + k_apply_pos with the forward) /
+        # flat (k_apply_flat + k_finalize_fwd) / separate (forward + k_apply_flat + k_table_finalize)
+        "step_launches": (4 if form == L.DQRM_APPLY_FWD_FIN_FWD or N > 1 else 3) if fused else 5,
+        "forward_in_apply_launch": fused and form == L.DQRM_APPLY_FWD_ONE_LAUNCH,
+        "forward_in_finalize_launch": fused and form == L.DQRM_APPLY_FWD_FIN_FWD,
         "device_errors": err, "setup_s": round(setup_s, 1),
     }
     print(json.dumps(line), flush=True)

@@ -42,6 +42,9 @@ DQRM_APPLY_FLAT = 1
 DQRM_APPLY_SLOT = 2
 DQRM_APPLY_RANGES = 3
 DQRM_APPLY_MERGE = 4
+DQRM_APPLY_FWD_SEPARATE = 0
+DQRM_APPLY_FWD_ONE_LAUNCH = 1
+DQRM_APPLY_FWD_FIN_FWD = 2
 DQRM_COALESCE_AUTO = 0
 DQRM_COALESCE_GENERAL = 1
 
@@ -53,7 +56,7 @@ DQRM_WIRE_F16 = 1
 DQRM_WIRE_I32 = 2
 DQRM_WIRE_F32 = 3
 
-DQRM_ABI_VERSION = 10  # include/dqrm.h
+DQRM_ABI_VERSION = 11  # include/dqrm.h
 DQRM_PRESUM_MAX_LOOKUPS = 2048
 
 # every symbol include/dqrm.h declares (checked by tests/test_abi.py)
@@ -78,6 +81,7 @@ EXPORTED_SYMBOLS = (
     "dqrm_apply_sparse_update_strided",
     "dqrm_apply_sparse_update_fwd",
     "dqrm_apply_fwd_is_one_launch",
+    "dqrm_apply_fwd_form",
     "dqrm_apply_workspace_bytes",
     "dqrm_apply_local",
     "dqrm_emb_bwd_apply_local",
@@ -283,6 +287,7 @@ def load(path: str | None = None) -> C.CDLL:
         ),
         "dqrm_apply_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int64]),
         "dqrm_apply_fwd_is_one_launch": (C.c_int, [TS, C.c_int, C.c_int64, C.c_size_t, BA, C.c_uint32]),
+        "dqrm_apply_fwd_form": (C.c_int, [TS, C.c_int, C.c_int64, C.c_size_t, BA, C.c_uint32]),
         "dqrm_apply_local": (
             C.c_int,
             [TS, P, C.c_int64, P, P, P, P, C.c_int, P, C.c_float, C.c_int, P],

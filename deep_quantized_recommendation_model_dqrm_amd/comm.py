@@ -507,6 +507,17 @@ class SparseGradExchange:
             L.check(rc, "dqrm_apply_fwd_is_one_launch")
         return rc == 1
 
+    def apply_fwd_form(self, next_batch: LookupBatch) -> str:
+        """The launches apply_forward issues (dqrm_apply_fwd_form): "one_launch" (the merge kernel:
+        update and forward together), "fin_fwd" (the flat apply, then its finalize and the forward in
+        one launch) or "separate" (the apply's launches, then the forward's)."""
+        t = self.tables
+        rc = t.lib.dqrm_apply_fwd_form(C.byref(t.c), self.world if self.coll else 1, self.cap_total,
+                                       self.apply_ws.numel(), C.byref(next_batch.c), t._fwd_flags(True, False, False))
+        if rc < 0:
+            L.check(rc, "dqrm_apply_fwd_form")
+        return {L.DQRM_APPLY_FWD_ONE_LAUNCH: "one_launch", L.DQRM_APPLY_FWD_FIN_FWD: "fin_fwd"}.get(rc, "separate")
+
     def apply_forward(self, lr: float, next_batch: LookupBatch, out: torch.Tensor | None = None, bits: int = 4,
                       refresh_scale: bool = True, full_precision: bool = False, layout: str = "tbd",
                       mode: int | None = None, repack: bool = False) -> torch.Tensor:

@@ -40,7 +40,6 @@ namespace {
 
 constexpr int SPLIT = DQRM_TABLE_SPLIT;
 constexpr int AM_TPB = 256;
-constexpr int AM_NW = AM_TPB / WAVE;
 constexpr int AM_MAXN = dqrm_internal::kMergeMaxRanks;  // ranks
 constexpr int AM_KEYS = 4096;     // a chunk's rows of all ranks held in LDS (else searched in HBM)
 constexpr int AM_MAP = 16384;     // dense-range map entries (int16): row span x ranks

@@ -192,7 +192,9 @@ DQRM_INLINE void pack4_row(const float4 w, uint8_t* __restrict__ prow, int idx4,
 // superblocks. Narrow tables (<= 256 rows, dimension-split in the slot kernels) get their
 // rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats),
 // unless rebuild_narrow is false (the updating kernel kept them exact like any table's).
-template <bool WT>
+// WTS: the table max is stored write-through (read by other workgroups of the launch); U4:
+// loads in flight per thread in the flag and superblock scans.
+template <bool WT, bool WTS = WT, int U4 = 4>
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
@@ -230,7 +232,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             sblkmax[m.sblk_base[t]] = r;
             if (flag_get_h<WT>(sdirty, m.sblk_base[t])) flag_clear(sdirty, m.sblk_base[t]);
             if (flag_get_h<WT>(bdirty, m.blk_base[t])) flag_clear(bdirty, m.blk_base[t]);
-            if constexpr (WT) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups
+            if constexpr (WTS) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups
         }
         return;
     }
@@ -238,7 +240,6 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     const int64_t ns = ceil_div(nblk, SBLK_BLOCKS);
     const int64_t sbb = m.sblk_base[t], bb = m.blk_base[t];
     const int lane = threadIdx.x % WAVE, w = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    constexpr int U4 = 4;  // loads in flight per thread
     // tracked (flat apply kernels): tmax already holds every grown row max (atomicMax), so
     // the table-wide rescan is needed only if a rescanned superblock held the table max
     const float tmax0 = tracked ? ld_h<WT>(tmax + t) : 0.0f;
@@ -362,7 +363,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     if (threadIdx.x == 0) {
         float r = 0.0f;
         for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
-        if constexpr (WT) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups (sc1)
+        if constexpr (WTS) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups (sc1)
     }
 }
 

@@ -240,19 +240,48 @@ struct FwdArgs {
     int bits;
     uint32_t flags;
     int pool1;  // DQRM_BATCH_POOLING_ONE: bag b of every table is lookup b (offsets unread)
+    uint32_t* sync;     // k_finalize_fwd: the tables' sync words (gate, arrivals)
+    uint32_t spin;      //   gate polls before a forward workgroup flags a stall
 };
 
+// k_finalize_fwd's per-table sync words (apart from the merge apply's 8/9 and the one-launch
+// step's 3-5 / 32+): the gate (1 = the table's |W| maxima are final) and its forward arrivals
+constexpr int FINFWD_GATE_WORD = 10;
+constexpr int FINFWD_CNT_WORD = 11;
+
+// wave-uniform bounded wait for a table's gate (a gate that never opens is flagged, not a hang)
+DQRM_INLINE void wait_gate(const uint32_t* gate, uint32_t spin, uint32_t* err) {
+    uint32_t n = 0;
+    while (ld_wt(gate) == 0u) {
+        if (++n > spin) {
+            flag_error(err, DQRM_ERRF_STALL);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 // Table t's bags, workgroup bx of gx (the body of k_emb_fwd; WT: the table max was just
-// written by this workgroup -- k_fwd_after_update -- and is read write-through)
-template <int LPR, int UNR, bool WT>
+// written by this workgroup -- k_fwd_after_update -- and is read write-through). GATE
+// (k_finalize_fwd): the table max is final only once the table's finalize workgroup opened its
+// gate, so the scale is taken after the first pass's index and row loads are in flight (W
+// itself is final at launch start), and every workgroup passes the gate once.
+template <int LPR, int UNR, bool WT, bool GATE = false>
 __device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t bx, int64_t gx) {
     const bool full_precision = (a.flags & DQRM_FWD_FULL_PRECISION) != 0;
     const bool refresh = (a.flags & DQRM_FWD_REFRESH_SCALE) != 0;
     const bool use_packed = (a.flags & DQRM_FWD_USE_PACKED) != 0 && !full_precision;
-    float s = 1.0f;
-    if (!full_precision) s = refresh ? sym_scale(WT ? ld_wt(a.tmax + t) : a.tmax[t], a.bits) : a.scale[t];
-    const float r = 1.0f / s;
-    if (refresh && !full_precision && bx == 0 && threadIdx.x == 0) a.scale[t] = s;
+    float s = 1.0f, r = 1.0f;
+    const bool gated = GATE && refresh && !full_precision;  // a frozen scale needs no final max
+    bool waited = !gated;   // the scale is taken
+    bool passed = false;    // GATE: this workgroup passed the gate
+    uint32_t* gate = GATE ? a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FINFWD_GATE_WORD : nullptr;
+    auto take_scale = [&]() {
+        if (!full_precision) s = refresh ? sym_scale((WT || GATE) ? ld_wt(a.tmax + t) : a.tmax[t], a.bits) : a.scale[t];
+        r = 1.0f / s;
+        if (refresh && !full_precision && bx == 0 && threadIdx.x == 0) a.scale[t] = s;
+    };
+    if (!gated) take_scale();
     const int64_t rowbase = a.meta[t], nrows = a.meta[a.T + t];
     // Criteo form: table t's lookups are idx[t*B, (t+1)*B) -- no idx_base round trip in front of the index loads
     const int64_t ibase = a.pool1 ? (int64_t)t * a.B : a.idx_base[t];
@@ -344,6 +373,11 @@ __device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t b
                     pk[k] = 0x8888u;
                 }
         }
+        if (!waited) {  // GATE: the first pass's loads are in flight; now the table's final max
+            wait_gate(gate, a.spin, a.err);
+            waited = passed = true;
+            take_scale();
+        }
         // phase 4: pooled sums for multi-lookup bags (bag order, FP32), quantize, store
 #pragma unroll
         for (int k = 0; k < UNR; ++k) {
@@ -380,6 +414,19 @@ __device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t b
             }
             const int64_t b = b0 + k * G + grp;
             reinterpret_cast<float4*>(out + b * a.ost_b)[lane] = y;
+        }
+    }
+    if constexpr (GATE) {
+        // every forward workgroup of the table passes the gate once (also one without bags), so
+        // when the last one arrives here none still polls: it re-arms the gate for the next launch
+        if (!passed) wait_gate(gate, a.spin, a.err);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t* cnt = a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FINFWD_CNT_WORD;
+            if (atomicAdd(cnt, 1u) + 1u == (uint32_t)gx) {
+                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -1167,6 +1214,54 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
         if (threadIdx.x == 0) *fw = 0u;
     }
     finalize_table<false>(m, t, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0, flagged == 0);
+}
+
+// The flat apply's finalize and the next batch's forward in ONE launch (dqrm_apply_sparse_update_fwd
+// / dqrm_exchange_apply_fwd with the flat apply kernel: weight_update_parallel_comm, s_q_g_p_c.py:601-628,
+// then the next apply_emb, single_gpu.py:609-674). Workgroups 0..T-1 finalize one table each as
+// k_table_finalize does (256 threads, 16 loads in flight per thread in the scans), store the table max
+// write-through and open the table's gate; the forward workgroups behind them (k_emb_fwd's grid, table
+// by table) issue their index and row loads at once -- W is final at launch start, only the
+// maxima may still move -- and take the scale from the table max once the gate is open. The gates
+// are opened by lower-numbered workgroups, which are dispatched first, so they are resident before
+// any forward workgroup polls (bounded polls: DQRM_ERRF_STALL, no hang).
+struct FinArgs {
+    const float* W;
+    float* rowmax;
+    float* blkmax;
+    float* sblkmax;
+    uint8_t* sdirty;
+    uint8_t* bdirty;
+    float* tmax;
+    int D;
+    int tracked, flagged;
+};
+
+template <int LPR, int UNR>
+__global__ void __launch_bounds__(256) k_finalize_fwd(FwdArgs a, FinArgs f, int gx) {
+    const int T = a.T;
+    if ((int)blockIdx.x < T) {
+        const int t = blockIdx.x;
+        bool fin = true;
+        if (f.flagged) {
+            uint32_t* fw = a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FLAG_WORD;
+            fin = *fw != 0u;  // uniform
+            __syncthreads();  // every thread has read the word before it is cleared
+            if (fin && threadIdx.x == 0) *fw = 0u;
+        }
+        if (fin)
+            finalize_table<false, true, 16>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
+                                            f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through table max has landed
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FINFWD_GATE_WORD, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int id = (int)blockIdx.x - T;
+    const int t = id / gx;
+    emb_fwd_table<LPR, UNR, false, true>(a, t, id - t * gx, gx);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -3652,13 +3747,17 @@ int check_set(const dqrm_table_set* s) {
 // tracked: the preceding kernel raised tmax for every grown row (the flat apply kernels)
 // flagged: after the flat apply kernels (k_apply_flat / k_apply_local), which mark the tables
 // they flagged (FLAG_WORD) and keep narrow tables' maxima themselves
-int launch_finalize(const dqrm_table_set* set, hipStream_t st, bool tracked = false, bool flagged = false) {
-    static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
-    static const bool no_skip = [] {  // DQRM_FIN_FLAGGED=0: finalize every table (A/B)
+static bool fin_flagged_skip() {  // DQRM_FIN_FLAGGED=0: finalize every table (A/B)
+    static const bool no_skip = [] {
         const char* e = getenv("DQRM_FIN_FLAGGED");
         return e && !strcmp(e, "0");
     }();
-    if (no_skip) flagged = false;
+    return !no_skip;
+}
+
+int launch_finalize(const dqrm_table_set* set, hipStream_t st, bool tracked = false, bool flagged = false) {
+    static_assert(BLK <= 1024, "finalize: one thread per row of a narrow table");
+    if (!fin_flagged_skip()) flagged = false;
     hipLaunchKernelGGL(k_table_finalize, dim3(set->num_tables), dim3(1024), 0, st, set->W, set->rowmax,
                        set->blkmax, set->sblkmax, set->sdirty, set->bdirty, set->tmax, set->meta, set->num_tables,
                        set->dim, tracked ? 1 : 0, set->sync, flagged ? 1 : 0);
@@ -4567,6 +4666,39 @@ static void merge_plan(const dqrm_table_set* set, int64_t cap_total, int N, int*
 static int fwd_args(const dqrm_table_set* set, const dqrm_batch* batch, int bits, uint32_t flags, float* out,
                     int64_t out_stride_t, int64_t out_stride_b, const char* who, FwdArgs* a);
 
+// the flat apply's finalize launch together with the next forward (k_finalize_fwd): the exact
+// FP32-row forward (the INT4 packed gather stays a launch of its own); DQRM_FIN_FWD=0 turns it off
+static bool finfwd_fits(const dqrm_table_set* set, const dqrm_batch* next, uint32_t flags) {
+    static const bool off = [] {
+        const char* e = getenv("DQRM_FIN_FWD");
+        return e && !strcmp(e, "0");
+    }();
+    const bool packed_path = (flags & DQRM_FWD_USE_PACKED) && !(flags & DQRM_FWD_FULL_PRECISION) && set->dim >= 8;
+    return !off && next && next->num_bags > 0 && !packed_path;
+}
+
+static int launch_finalize_fwd(const dqrm_table_set* set, FwdArgs fa, hipStream_t st) {
+    static const uint32_t spin = [] {  // DQRM_GATE_SPIN: gate polls before a forward flags a stall
+        const char* e = getenv("DQRM_GATE_SPIN");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 20);
+    }();
+    fa.sync = set->sync;
+    fa.spin = spin;
+    FinArgs f{set->W, set->rowmax, set->blkmax, set->sblkmax, set->sdirty, set->bdirty, set->tmax, set->dim,
+              1, fin_flagged_skip() ? 1 : 0};
+    DISPATCH_LPR(set->dim, {
+        constexpr int UNR = 4;
+        constexpr int BAGS_PER_WG = (256 / LPR) * UNR;
+        int64_t bx = (fa.B + BAGS_PER_WG - 1) / BAGS_PER_WG;
+        const int64_t cap = (8192 + fa.T - 1) / fa.T;  // as dqrm_emb_fwd: ~8k forward workgroups, grid-stride beyond
+        if (bx > cap) bx = cap;
+        const int64_t grid = (int64_t)fa.T * (1 + bx);
+        hipLaunchKernelGGL((k_finalize_fwd<LPR, UNR>), dim3((unsigned)grid), dim3(256), 0, st, fa, f, (int)bx);
+    });
+    LAUNCH_CHECK();
+    return DQRM_OK;
+}
+
 // the apply's kernel choice: the merge kernels (with the next batch's forward in the update's
 // launch when nf is given) when DQRM_APPLY=merge / dqrm_set_apply_kernel(DQRM_APPLY_MERGE) and
 // the positions workspace is given (N = 1 needs none). Not AUTO: measured on the TB shape
@@ -4577,6 +4709,14 @@ static bool apply_uses_merge(const dqrm_table_set* set, int num_ranks, int64_t c
     const bool ok = num_ranks <= dqrm_internal::kMergeMaxRanks && set->num_tables <= dqrm_internal::kMergeMaxTables &&
                     ws_bytes >= dqrm_internal::apply_workspace_bytes(num_ranks, cap_total);
     return ok && kind == DQRM_APPLY_MERGE;
+}
+
+// the flat kernel takes the apply (the choice apply_update_ex makes below)
+static bool apply_takes_flat(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t ws_bytes) {
+    if (apply_uses_merge(set, num_ranks, cap_total, ws_bytes)) return false;
+    const int kind = apply_kernel_kind();
+    if (kind == DQRM_APPLY_RANGES) return false;
+    return !(kind == DQRM_APPLY_SLOT || (kind == DQRM_APPLY_AUTO && num_ranks > 1 && num_ranks >= set->dim / 4));
 }
 
 size_t dqrm_apply_workspace_bytes(int num_ranks, int64_t cap_total) {
@@ -4599,6 +4739,10 @@ static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int6
                         size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
                         float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
                         void* stream);
+static int apply_update_ex(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total, const void* payloads,
+                           size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
+                           float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
+                           bool* fin_deferred, void* stream);
 
 int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
                                      const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
@@ -4626,26 +4770,53 @@ int dqrm_apply_sparse_update_fwd(const dqrm_table_set* set, const int64_t* cap_b
     if (apply_uses_merge(set, num_ranks, cap_total, workspace_bytes) && merge_fwd_fits(next, fwd_flags))
         return apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
                             lr, mode, repack_bits, workspace, workspace_bytes, &fa, stream);
-    if ((rc = apply_update(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
-                           lr, mode, repack_bits, workspace, workspace_bytes, nullptr, stream)))
+    // the flat apply: its finalize and the forward in one launch when the forward takes the exact rows
+    const bool fin_fwd = finfwd_fits(set, next, fwd_flags);
+    bool deferred = false;
+    if ((rc = apply_update_ex(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits,
+                              s_avg, lr, mode, repack_bits, workspace, workspace_bytes, nullptr,
+                              fin_fwd ? &deferred : nullptr, stream)))
         return rc;
+    if (deferred) return launch_finalize_fwd(set, fa, (hipStream_t)stream);
     return dqrm_emb_fwd(set, next, fwd_bits, fwd_flags, out, out_stride_t, out_stride_b, stream);
+}
+
+int dqrm_apply_fwd_form(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
+                        const dqrm_batch* next, uint32_t fwd_flags) {
+    int rc = check_set(set);
+    if (rc) return rc;
+    if ((rc = check_batch(next, "dqrm_apply_fwd_form"))) return rc;
+    if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS)
+        return set_error(DQRM_E_INVALID, "%s: bad ranks (%d)", "dqrm_apply_fwd_form", num_ranks);
+    if (apply_uses_merge(set, num_ranks, cap_total, workspace_bytes) && merge_fwd_fits(next, fwd_flags))
+        return DQRM_APPLY_FWD_ONE_LAUNCH;
+    if (apply_takes_flat(set, num_ranks, cap_total, workspace_bytes) && finalize_launch_flat() &&
+        finfwd_fits(set, next, fwd_flags))
+        return DQRM_APPLY_FWD_FIN_FWD;
+    return DQRM_APPLY_FWD_SEPARATE;
 }
 
 int dqrm_apply_fwd_is_one_launch(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
                                  const dqrm_batch* next, uint32_t fwd_flags) {
-    int rc = check_set(set);
-    if (rc) return rc;
-    if ((rc = check_batch(next, "dqrm_apply_fwd_is_one_launch"))) return rc;
-    if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS)
-        return set_error(DQRM_E_INVALID, "%s: bad ranks (%d)", "dqrm_apply_fwd_is_one_launch", num_ranks);
-    return apply_uses_merge(set, num_ranks, cap_total, workspace_bytes) && merge_fwd_fits(next, fwd_flags) ? 1 : 0;
+    const int f = dqrm_apply_fwd_form(set, num_ranks, cap_total, workspace_bytes, next, fwd_flags);
+    return f < 0 ? f : (f == DQRM_APPLY_FWD_ONE_LAUNCH ? 1 : 0);
 }
 
 static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total, const void* payloads,
                         size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
                         float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
                         void* stream) {
+    return apply_update_ex(set, cap_base, cap_total, payloads, payload_bytes, rank_pitch, num_ranks, grad_bits, s_avg,
+                           lr, mode, repack_bits, ws, ws_bytes, nf, nullptr, stream);
+}
+
+// fin_deferred (non-null): a flat apply's finalize launch is left to the caller (*fin_deferred = true),
+// which runs it together with the next forward (k_finalize_fwd)
+static int apply_update_ex(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total, const void* payloads,
+                           size_t payload_bytes, size_t rank_pitch, int num_ranks, int grad_bits, const float* s_avg,
+                           float lr, int mode, int repack_bits, void* ws, size_t ws_bytes, const FwdArgs* nf,
+                           bool* fin_deferred, void* stream) {
+    if (fin_deferred) *fin_deferred = false;
     int rc = check_set(set);
     if (rc) return rc;
     if (num_ranks <= 0 || num_ranks > DQRM_MAX_RANKS || !payloads || !cap_base)
@@ -4716,7 +4887,7 @@ static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int6
     }
     // AUTO: flat while each lane of a row's group searches at most one other rank
     // (num_ranks < D/4), slot beyond (tools/bench_apply_ranks.py)
-    if (kind == DQRM_APPLY_SLOT || (kind == DQRM_APPLY_AUTO && num_ranks > 1 && num_ranks >= D / 4)) {
+    if (!apply_takes_flat(set, num_ranks, cap_total, ws_bytes)) {  // SLOT, or AUTO at num_ranks >= D/4
         DISPATCH_LPR(D, {
             if ((rc = allow_lds(k_table_apply<LPR>, SLOT_LDS))) return rc;
             hipLaunchKernelGGL(k_table_apply<LPR>, dim3(a.T * SPLIT), dim3(TWG), SLOT_LDS, st, a);
@@ -4743,6 +4914,10 @@ static int apply_update(const dqrm_table_set* set, const int64_t* cap_base, int6
         });
     }
     LAUNCH_CHECK();  // both kernels finalize the |W| hierarchy inside the launch
+    if (a.fin_launch && flat && fin_deferred) {
+        *fin_deferred = true;
+        return DQRM_OK;
+    }
     if (a.fin_launch) return launch_finalize(set, st, flat, flat);
     return DQRM_OK;
 }

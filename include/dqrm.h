@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define DQRM_ABI_VERSION 10 /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
+#define DQRM_ABI_VERSION 11 /* 2: dqrm_table_set.bdirty, dqrm_set_apply_kernel, dqrm_apply_local;
                                3: backward workspace (dqrm_bwd_workspace_bytes), no per-slot key cap;
                                4: dqrm_table_set.sync (in-launch hierarchy finalize), padded flags;
                                5: dqrm_emb_bwd_apply_local (coalesce + local update, one launch);
@@ -63,7 +63,9 @@ extern "C" {
                                   dqrm_bwd_sgd_fwd_is_one_launch, DQRM_APPLY_MERGE,
                                   dqrm_apply_sparse_update_fwd, dqrm_apply_fwd_is_one_launch,
                                   dqrm_apply_workspace_bytes, dqrm_exchange.apply_ws,
-                                  dqrm_exchange_apply_fwd */
+                                  dqrm_exchange_apply_fwd;
+                              11: the flat apply's finalize and the next forward in one launch
+                                  (dqrm_apply_sparse_update_fwd), dqrm_apply_fwd_form */
 
 /* status codes */
 #define DQRM_OK            0
@@ -379,7 +381,10 @@ int dqrm_apply_sparse_update_strided(const dqrm_table_set* set, const int64_t* c
  * merge kernel (DQRM_APPLY_MERGE / AUTO at 1 < num_ranks <= 16) and `next` is a Criteo-form
  * batch without DQRM_FWD_USE_PACKED, the forward runs in the apply's launch: each table's
  * forward workgroups start once that table's update and |W| maxima are final (no finalize or
- * forward launch). Reference: weight_update_parallel_comm (s_q_g_p_c.py:601-628) and the next
+ * forward launch). When the flat apply kernel takes it (AUTO at num_ranks < dim/4) and the
+ * forward reads the exact FP32 rows, the flat kernel's finalize and the forward share ONE launch
+ * after it (the forward's index and row loads in flight while the table's maxima are finalized;
+ * each table's scale taken once its finalize workgroup opened the table's gate). Reference: weight_update_parallel_comm (s_q_g_p_c.py:601-628) and the next
  * apply_emb (dlrm_s_pytorch_single_gpu.py:609-674, q_m_n_q_g.py:317-398). */
 int dqrm_apply_sparse_update_fwd(const dqrm_table_set* set, const int64_t* cap_base, int64_t cap_total,
                                  const void* payloads, size_t payload_bytes, size_t rank_pitch, int num_ranks,
@@ -397,6 +402,16 @@ size_t dqrm_apply_workspace_bytes(int num_ranks, int64_t cap_total);
  * workspace) and the forward of `next` with ONE update launch, 0 if not, <0 on bad arguments. */
 int dqrm_apply_fwd_is_one_launch(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
                                  const dqrm_batch* next, uint32_t fwd_flags);
+
+/* The launches dqrm_apply_sparse_update_fwd would issue for these arguments: DQRM_APPLY_FWD_SEPARATE
+ * (the apply's launches, then the forward's), DQRM_APPLY_FWD_ONE_LAUNCH (update and forward in one
+ * launch: the merge kernel) or DQRM_APPLY_FWD_FIN_FWD (the flat apply, then its finalize and the
+ * forward in one launch); <0 on bad arguments. */
+#define DQRM_APPLY_FWD_SEPARATE   0
+#define DQRM_APPLY_FWD_ONE_LAUNCH 1
+#define DQRM_APPLY_FWD_FIN_FWD    2
+int dqrm_apply_fwd_form(const dqrm_table_set* set, int num_ranks, int64_t cap_total, size_t workspace_bytes,
+                        const dqrm_batch* next, uint32_t fwd_flags);
 
 /* Single-rank DP step (num_ranks == 1, mode DQRM_UPD_DP), dqrm_grad_quant_pack and
  * dqrm_apply_sparse_update fused: the table scale s = clamp(max_s ws_absmax[t*S+s], 1e-8)

@@ -76,12 +76,24 @@ def test_fwd_after_update_flags_bad_rows(dq):
     assert ts.read_errors() & dq._lib.DQRM_ERRF_INDEX
 
 
-def test_module_sparse_steps_keep_exact_hierarchy(dq):
+@pytest.mark.parametrize("fused_step", [False, True])
+def test_module_sparse_steps_keep_exact_hierarchy(dq, fused_step):
     """A list of modules, grad_mode "sparse" + torch.optim.SGD for 4 steps (the unchanged
-    single-GPU driver): after every fused sync-and-forward each table's |W| hierarchy equals
-    a full rebuild from its W, and the output equals a plain refreshing forward on that W."""
+    single-GPU driver): after every step's next forward each table's |W| hierarchy equals a
+    full rebuild from its W, and the output equals a plain refreshing forward on that W.
+    fused_step False: the optimizer adds the COO and the module syncs the changed rows in its
+    next forward (dqrm_emb_fwd_after_update); True (default): the optimizer's step runs as the
+    module's own SGD kernel, so no rows are left to sync."""
     from deep_quantized_recommendation_model_dqrm_amd import quant_modules_not_quantize_grad as Q
 
+    Q.set_fused_optimizer_step(fused_step)
+    try:
+        _module_sparse_steps(dq, Q, fused_step)
+    finally:
+        Q.set_fused_optimizer_step(True)
+
+
+def _module_sparse_steps(dq, Q, fused_step):
     rows, D, B = [3, 61, 1500, 20000], 16, 128
     g = torch.Generator(device="cuda").manual_seed(5)
     mods = torch.nn.ModuleList([Q.QuantEmbeddingBagTwo(n, D, 4, grad_mode="sparse", init="device", device="cuda")
@@ -92,7 +104,7 @@ def test_module_sparse_steps_keep_exact_hierarchy(dq):
         P = [torch.randint(0, n, (B,), generator=g, device="cuda") for n in rows]
         dys = [torch.randn(B, D, generator=g, device="cuda") * 0.1 for _ in rows]
         pending = [bool(m._ext_rows) for m in mods]
-        assert all(pending) == (step > 0)
+        assert all(pending) == (step > 0 and not fused_step) and (any(pending) == all(pending))
         ly = [mods[t](P[t], off) for t in range(len(rows))]
         for t, m in enumerate(mods):
             ts = m._tset

@@ -1240,11 +1240,14 @@ def _payloads_for_ranks(dq, ts, rank_batches, rank_dys, grad_bits):
 @pytest.mark.parametrize("N,D,B,dist,bits", [(1, 64, 2048, "uniform", 8), (2, 64, 1024, "zipf", 8),
                                              (4, 16, 512, "uniform", 8), (8, 64, 256, "uniform", 8),
                                              (8, 32, 300, "zipf", 16), (3, 64, 700, "uniform", 32)])
-def test_merge_apply_with_next_forward_matches_separate_calls(dq, N, D, B, dist, bits):
-    """dqrm_apply_sparse_update_fwd -- the merge apply of N ranks' payloads (DQRM_APPLY_MERGE,
-    AUTO at 1 < N <= 16) with the NEXT batch's forward in the same launch (each table's forward
-    workgroups wait at the table's gate until its update and |W| maxima are final) -- against
-    the flat apply + k_table_finalize + dqrm_emb_fwd on a copy of the tables, bit for bit over 3
+@pytest.mark.parametrize("fused", ["merge", "flat"])
+def test_merge_apply_with_next_forward_matches_separate_calls(dq, N, D, B, dist, bits, fused):
+    """dqrm_apply_sparse_update_fwd -- merge: the merge apply of N ranks' payloads
+    (DQRM_APPLY_MERGE) with the NEXT batch's forward in the same launch (each table's forward
+    workgroups wait at the table's gate until its update and |W| maxima are final); flat: the
+    flat apply, then its finalize and the next forward in ONE launch (k_finalize_fwd: the
+    forward workgroups wait at the gate their table's finalize workgroup opens) -- against the
+    flat apply + k_table_finalize + dqrm_emb_fwd on a copy of the tables, bit for bit over 3
     steps: W, the |W| hierarchy, the forward scale and the next batch's output. Then the output
     of the last step equals the oracle's forward of the updated tables (every table), and W
     equals oracle.dp_step over the ranks. Reference: s_q_g_p_c.py:601-628,850-890 and apply_emb
@@ -1274,12 +1277,12 @@ def test_merge_apply_with_next_forward_matches_separate_calls(dq, N, D, B, dist,
                 dq, ts, rb, [torch.from_numpy(d).cuda() for d in dys], bits)
             kern = HipExchangeKernels(ts)
             if j == 0:
-                prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_MERGE)
+                prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_MERGE if fused == "merge" else L.DQRM_APPLY_FLAT)
                 try:
                     ws = torch.zeros(max(16, int(lib.dqrm_apply_workspace_bytes(N, cap_total))), dtype=torch.uint8,
                                      device="cuda")
                     assert lib.dqrm_apply_fwd_is_one_launch(ts.c, N, cap_total, ws.numel(), rank0[k + 1].c,
-                                                            ts._fwd_flags(True, False, False)) == 1
+                                                            ts._fwd_flags(True, False, False)) == (fused == "merge")
                     y = torch.empty(T, B, D, device="cuda")
                     kern.apply_fwd(cap_base, cap_total, payloads, payloads.shape[1], N, bits, s_avg, 0.5, mode, False,
                                    rank0[k + 1], y, workspace=ws)
@@ -1330,3 +1333,65 @@ def test_replica_mean_matches_gloo_fixture(dq, golden_dir, N):
             np.testing.assert_array_equal(got.view(np.uint32), fx[f"small_n{N}"].view(np.uint32))
         else:
             assert G.checksum(got) == str(fx[f"large_n{N}_checksum"])
+
+
+@pytest.mark.parametrize("refresh,full_precision,layout", [(True, False, "tbd"), (False, False, "tbd"),
+                                                           (True, True, "btd"), (True, False, "btd")])
+def test_flat_finalize_forward_bag_batches(dq, refresh, full_precision, layout):
+    """k_finalize_fwd with a bag-form next batch (offsets, multi-lookup bags, an empty bag), a
+    frozen scale, full precision and both output layouts: dqrm_apply_sparse_update_fwd on the
+    flat apply = the flat apply + k_table_finalize + dqrm_emb_fwd on a copy, bit for bit (W, the
+    |W| hierarchy, the scale, the output); the output = oracle.emb_fwd of the updated tables."""
+    import ctypes as C
+    from deep_quantized_recommendation_model_dqrm_amd import _lib as L
+    from deep_quantized_recommendation_model_dqrm_amd.comm import HipExchangeKernels
+
+    lib = L.load()
+    rows, D, B, N, bits = COAL_ROWS, 32, 384, 2, 8
+    T = len(rows)
+    Ws = G.table_weights(rows, D, 977)
+    sets = [make_set(dq, Ws) for _ in range(2)]
+    for k in range(2):
+        rb = [dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, B, 983 + 10 * k + r)).cuda())
+              for r in range(N)]
+        dys = [torch.from_numpy(G.upstream_grad(T, B, D, 991 + 10 * k + r) * 30).cuda() for r in range(N)]
+        idxs, offs = G.random_bags(rows, 200, 997 + 10 * k, num_indices_per_lookup=3)
+        for o in offs:
+            o[7] = o[8]  # an empty bag
+        nb = to_batch(dq, idxs, offs)
+        outs = []
+        prev = lib.dqrm_set_apply_kernel(L.DQRM_APPLY_FLAT)
+        try:
+            for j, ts in enumerate(sets):
+                payloads, s_avg, cap_base, cap_total = _payloads_for_ranks(dq, ts, rb, dys, bits)
+                kern = HipExchangeKernels(ts)
+                shape = (T, 200, D) if layout == "tbd" else (200, T, D)
+                y = torch.full(shape, float("nan"), device="cuda")
+                if j == 0:
+                    kern.apply_fwd(cap_base, cap_total, payloads, payloads.shape[1], N, bits, s_avg, 0.5,
+                                   L.DQRM_UPD_DP, False, nb, y, refresh_scale=refresh, full_precision=full_precision,
+                                   layout=layout)
+                else:
+                    kern.apply(cap_base, cap_total, payloads, payloads.shape[1], N, bits, s_avg, 0.5, L.DQRM_UPD_DP,
+                               False)
+                    ost, osb = (200 * D, D) if layout == "tbd" else (D, T * D)
+                    L.check(lib.dqrm_emb_fwd(C.byref(ts.c), C.byref(nb.c), 4,
+                                             ts._fwd_flags(refresh, False, full_precision), y.data_ptr(), ost, osb,
+                                             None), "dqrm_emb_fwd")
+                outs.append(y)
+        finally:
+            lib.dqrm_set_apply_kernel(prev)
+        torch.cuda.synchronize()
+        assert [ts.read_errors() for ts in sets] == [0, 0], k
+        assert torch.equal(outs[0], outs[1]), k
+        for name in ("W", "rowmax", "blkmax", "sblkmax", "tmax", "scale"):
+            assert torch.equal(getattr(sets[0], name), getattr(sets[1], name)), (k, name)
+        y = outs[0].cpu().numpy()
+        s = sets[0].scale.cpu().numpy()
+        for t in range(T):
+            Wt = sets[0].table_weight(t).cpu().numpy()
+            if refresh and not full_precision:
+                assert s[t] == O.table_scale(Wt, 4)
+            ref = O.emb_fwd(Wt, idxs[t], offs[t], s[t], full_precision=full_precision)[0]
+            yt = y[t] if layout == "tbd" else y[:, t]
+            np.testing.assert_array_equal(yt, ref)
