@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "../../include/dqrm.h"
@@ -193,12 +194,18 @@ DQRM_INLINE void pack4_row(const float4 w, uint8_t* __restrict__ prow, int idx4,
 // rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats),
 // unless rebuild_narrow is false (the updating kernel kept them exact like any table's).
 // WTS: the table max is stored write-through (read by other workgroups of the launch); U4:
-// loads in flight per thread in the flag and superblock scans.
-template <bool WT, bool WTS = WT, int U4 = 4>
+// loads in flight per thread in the flag and superblock scans. on_final() is called once by every
+// thread of the workgroup as soon as the table max is final: with `tracked`, right after the flag
+// scan when no flagged superblock held the table max (the rest only fixes lower levels), else at
+// the end (k_finalize_fwd opens the table's forward gate there).
+struct NoFinal {
+    DQRM_INLINE void operator()() const {}
+};
+template <bool WT, bool WTS = WT, int U4 = 4, class OnFinal = NoFinal>
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
-                               int D, bool tracked, bool rebuild_narrow = true) {
+                               int D, bool tracked, bool rebuild_narrow = true, OnFinal on_final = OnFinal()) {
     // Every load below is an sc1 (write-through) load: this runs either as its own launch or
     // in the table's last workgroup of the updating kernel (arrive_last), whose producers
     // stored the hierarchy write-through.
@@ -234,6 +241,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             if (flag_get_h<WT>(bdirty, m.blk_base[t])) flag_clear(bdirty, m.blk_base[t]);
             if constexpr (WTS) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups
         }
+        on_final();
         return;
     }
     const int64_t nblk = ceil_div(m.num_rows[t], BLK);
@@ -311,6 +319,8 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     constexpr int FIN_LIST = 128;
     __shared__ int s_dl[FIN_LIST];
     __shared__ int s_dn;
+    bool early = false;  // on_final() already called
+    bool first = true;
     for (;;) {
         if (threadIdx.x == 0) s_dn = 0;
         __syncthreads();
@@ -338,6 +348,15 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
         }
         __syncthreads();
         const int nd = s_dn;
+        if (!std::is_same<OnFinal, NoFinal>::value && tracked && first && nd <= FIN_LIST) {  // can the table max shrink?
+            int hit = 0;
+            for (int i = threadIdx.x; i < nd; i += blockDim.x) hit |= ld_h<WT>(sblkmax + sbb + s_dl[i]) >= tmax0;
+            if (!__syncthreads_or(hit)) {
+                on_final();
+                early = true;
+            }
+        }
+        first = false;
         for (int i = w; i < nd && i < FIN_LIST; i += nw) fix_superblock(s_dl[i]);
         if (nd <= FIN_LIST) break;  // uniform
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cleared flags land before the next scan
@@ -345,7 +364,10 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the new superblock maxima reach L2 first
     __syncthreads();
-    if (!s_rescan) return;  // uniform: tmax is exact already
+    if (!s_rescan) {  // uniform: tmax is exact already
+        if (!early) on_final();
+        return;
+    }
     float v = 0.0f;
     for (int64_t k0 = threadIdx.x; k0 < ns; k0 += (int64_t)blockDim.x * U4) {
         float x[U4];
@@ -365,6 +387,7 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
         for (int k = 0; k < nw; ++k) r = fmaxf(r, red[k]);
         if constexpr (WTS) st_wt(tmax + t, r); else tmax[t] = r;  // WT: read by other workgroups (sc1)
     }
+    if (!early) on_final();
 }
 
 // One rank's wire payload: [counts i32 T*SPLIT][rows i32 cap][values cap x D], 16-B aligned

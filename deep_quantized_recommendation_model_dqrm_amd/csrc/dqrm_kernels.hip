@@ -1249,14 +1249,17 @@ __global__ void __launch_bounds__(256) k_finalize_fwd(FwdArgs a, FinArgs f, int 
             __syncthreads();  // every thread has read the word before it is cleared
             if (fin && threadIdx.x == 0) *fw = 0u;
         }
-        if (fin)
+        uint32_t* gate = a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FINFWD_GATE_WORD;
+        auto open_gate = [gate]() {  // the table max is final (and, if it moved, stored write-through)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        if (fin)  // the gate opens as soon as the table max is known final, the lower levels after it
             finalize_table<false, true, 16>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
-                                            f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-through table max has landed
-        __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(a.sync + (int64_t)t * DQRM_SYNC_STRIDE + FINFWD_GATE_WORD, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+                                            f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0, open_gate);
+        else
+            open_gate();
         return;
     }
     const int id = (int)blockIdx.x - T;

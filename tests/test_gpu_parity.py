@@ -1351,6 +1351,8 @@ def test_flat_finalize_forward_bag_batches(dq, refresh, full_precision, layout):
     T = len(rows)
     Ws = G.table_weights(rows, D, 977)
     sets = [make_set(dq, Ws) for _ in range(2)]
+    for ts in sets:  # the frozen scale of the refresh=False case (a held periodic-refresh scale)
+        ts.scale.copy_(torch.from_numpy(np.array([O.table_scale(w, 4) for w in Ws], np.float32)))
     for k in range(2):
         rb = [dq.LookupBatch.pooling_one(torch.from_numpy(G.pooling_one(rows, B, 983 + 10 * k + r)).cuda())
               for r in range(N)]

@@ -68,7 +68,22 @@ def main(src: str, tag: str) -> None:
             rd_exact[k] = sum(mean.get(f"TCC_EA0_RDREQ_{n}B_sum", 0.0) * n for n in (32, 64, 128))
     except OSError:
         pass
+    # write requests by size and L2 atomics (optional pass): where WRITE_SIZE goes
+    wrq = {}
+    try:
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(f"{src}_wrreq/tb_counter_collection.csv")):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, d in acc.items():
+            mean = {c: sum(x) / len(x) for c, x in d.items()}
+            n64 = mean.get("TCC_EA0_WRREQ_64B_sum", 0.0)
+            wrq[k] = {"write_requests_64B": n64, "write_requests_32B": mean.get("TCC_EA0_WRREQ_sum", 0.0) - n64,
+                      "atomic_requests": mean.get("TCC_EA0_ATOMIC_sum")}
+    except OSError:
+        pass
     for k, v in out.items():
+        if k in wrq:
+            v.update(wrq[k])
         fe = counters["FETCH_SIZE"].get(k)
         wr = counters["WRITE_SIZE"].get(k)
         v["fetch_size_bytes"] = fe
