@@ -1837,6 +1837,7 @@ DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
 
 constexpr int FLAT_TPB = 256;
 constexpr int FLAT_HDR_RANKS = 32;  // k_apply_flat: ranks whose slot bounds it keeps in LDS
+constexpr int FLAT_RUN_MAX = 4096;  // k_apply_flat: other ranks' rows of a pass's slots staged in LDS
 #ifndef DQRM_FLAT_PRELOAD
 #define DQRM_FLAT_PRELOAD 1  // 0: an A/B build reading the superblock / table max only on growth
 #endif
@@ -1847,19 +1848,35 @@ constexpr int FLAT_HDR_RANKS = 32;  // k_apply_flat: ranks whose slot bounds it 
 // flags the block (bdirty) and its superblock (sdirty) for finalize's re-reduction. Rows
 // of one call are distinct, so a concurrent grower either raised old_blk before this row
 // read it (then the block max is that grower's current value) or the holder is flagged.
+// the row and its maxima, loaded before the update's value is known (so they share its round trip)
+struct FlatPre {
+    float4 w0;
+    float old_blk, old_sb, old_tm;
+};
 template <int LPR>
-DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
-                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub,
-                                 bool owned, const OwnQueue* oq) {
+DQRM_INLINE FlatPre flat_row_preload(const ApplyArgs& a, int t, int64_t grow, int64_t x, int64_t bb, int64_t sbb,
+                                     int sub) {
     constexpr int D = LPR * 4;
     const int64_t blk = x >> 8;
-    const float4 w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
-    const float old_blk = a.blkmax[bb + blk];
+    FlatPre p;
+    p.w0 = reinterpret_cast<const float4*>(a.W + grow * D)[sub];
+    p.old_blk = a.blkmax[bb + blk];
     // the superblock and table maxima with the row (DQRM_FLAT_PRELOAD): no dependent round trips
     // on growth, which early in training is every row of a big table; a stale-low value only
     // costs a redundant atomicMax (within the launch they only grow)
-    const float old_sb = DQRM_FLAT_PRELOAD ? a.sblkmax[sbb + (blk >> 8)] : 0.0f;
-    const float old_tm = DQRM_FLAT_PRELOAD ? a.tmax[t] : 0.0f;
+    p.old_sb = DQRM_FLAT_PRELOAD ? a.sblkmax[sbb + (blk >> 8)] : 0.0f;
+    p.old_tm = DQRM_FLAT_PRELOAD ? a.tmax[t] : 0.0f;
+    return p;
+}
+
+template <int LPR>
+DQRM_INLINE void flat_row_apply(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
+                                int64_t nrows, int64_t bb, int64_t sbb, const FlatPre& pre, float4 acc, float r_pack,
+                                int sub, bool owned, const OwnQueue* oq) {
+    constexpr int D = LPR * 4;
+    const int64_t blk = x >> 8;
+    const float4 w0 = pre.w0;
+    const float old_blk = pre.old_blk, old_sb = pre.old_sb, old_tm = pre.old_tm;
     float4 w;
     w.x = update(w0.x, acc.x); w.y = update(w0.y, acc.y);
     w.z = update(w0.z, acc.z); w.w = update(w0.w, acc.w);
@@ -1894,6 +1911,14 @@ DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, 
             }
         }
     }
+}
+
+template <int LPR>
+DQRM_INLINE void flat_row_update(const ApplyArgs& a, const ApplyUpdate& update, int t, int64_t grow, int64_t x,
+                                 int64_t nrows, int64_t bb, int64_t sbb, float4 acc, float r_pack, int sub,
+                                 bool owned, const OwnQueue* oq) {
+    flat_row_apply<LPR>(a, update, t, grow, x, nrows, bb, sbb, flat_row_preload<LPR>(a, t, grow, x, bb, sbb, sub), acc,
+                        r_pack, sub, owned, oq);
 }
 
 // Single-rank DP step, quantize-pack and apply fused (dqrm_apply_local): grid (entry
@@ -2076,29 +2101,87 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
         if (threadIdx.x == 0) s_oq_n = 0;
         __syncthreads();
     }
-    for (int e = blockIdx.x * G + grp; e < cnt_r; e += gridDim.x * G) {
-        const int32_t x = rows_r[e];
-        const int c0 = e - grp;  // the chunk's first entry
+    // N > 1: the other ranks' rows of the slots this pass's G entries fall in are staged in LDS
+    // (one round trip, issued with the entries' own row loads), so each entry's positions are
+    // found by LDS searches instead of dependent HBM round trips; runs longer than FLAT_RUN_MAX
+    // rows in total are searched in HBM as before
+    __shared__ int32_t s_run[FLAT_RUN_MAX];
+    __shared__ int s_roff[FLAT_HDR_RANKS];
+    for (int e0 = blockIdx.x * G; e0 < cnt_r; e0 += gridDim.x * G) {  // uniform passes
+        const int e = e0 + grp;
+        const bool valid = e < cnt_r;
+        const int32_t x = valid ? rows_r[e] : -1;
+        const int c0 = e0;  // the chunk's first entry
         const int32_t xlo = (own_mode && c0 > 0) ? rows_r[c0 - 1] : -1;
         const int32_t xhi = (own_mode && c0 + G < cnt_r) ? rows_r[c0 + G] : -1;
+        int qa = 0, qb = -1;
+        bool staged = false;
+        if (slot_search) {
+            const int elast = (e0 + G < cnt_r ? e0 + G : cnt_r) - 1;
+            while (qa < SPLIT - 1 && s_sb[r][qa + 1] <= e0) ++qa;  // rank r's slot of its entry e0
+            qb = qa;
+            while (qb < SPLIT - 1 && s_sb[r][qb + 1] <= elast) ++qb;
+            int tot = 0;
+            for (int j = 0; j < N; ++j)
+                if (j != r) tot += s_sb[j][qb + 1] - s_sb[j][qa];
+            staged = tot <= FLAT_RUN_MAX;  // uniform
+            if (staged) {
+                __syncthreads();  // the previous pass's searches are done with s_run
+                constexpr int PT = FLAT_RUN_MAX / FLAT_TPB;
+                int32_t v[PT];
+                int dst[PT];
+#pragma unroll
+                for (int k = 0; k < PT; ++k) dst[k] = -1;
+                int off = 0;
+                for (int j = 0; j < N; ++j) {  // every load in flight, then the LDS stores
+                    if (j == r) continue;
+                    const int lo = s_sb[j][qa], len = s_sb[j][qb + 1] - lo;
+                    if (threadIdx.x == 0) s_roff[j] = off;
+                    const int32_t* rj = reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes +
+                                                                         pl.rows_off) + cb + lo;
+#pragma unroll
+                    for (int k = 0; k < PT; ++k) {
+                        const int i = (int)threadIdx.x + k * FLAT_TPB;
+                        if (i >= off && i < off + len) {
+                            v[k] = rj[i - off];
+                            dst[k] = i;
+                        }
+                    }
+                    off += len;
+                }
+#pragma unroll
+                for (int k = 0; k < PT; ++k)
+                    if (dst[k] >= 0) s_run[dst[k]] = v[k];
+                __syncthreads();
+            }
+        }
+        if (!valid) continue;
         if (x < 0 || x >= nrows) {  // cannot happen for payloads this library packed
             if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
             continue;
         }
+        const int64_t grow = rb + x;
         float4 acc;
+        FlatPre pre;
         if (N == 1) {
+            pre = flat_row_preload<LPR>(a, t, grow, x, bb, sbb, sub);  // with the value: one round trip
             acc = src.load((uint32_t)e, sub);
         } else {  // where the other ranks hold row x (lane k searches ranks k, k+LPR, ...)
             bool lower = false;
             // the slot of row x (slot s holds blocks [nblk*s/8, nblk*(s+1)/8)): its run in each rank
             const int64_t nblk = (nrows + BLK - 1) / BLK;
             const int xs = slot_search ? (int)((8 * ((int64_t)(x >> 8) + 1) + nblk - 1) / nblk) - 1 : 0;
+            const bool in_lds = staged && xs >= qa && xs <= qb;
             for (int j = sub; j < N; j += LPR) {
                 int p = e;
                 if (j != r) {
                     const unsigned char* pj = a.payloads + (int64_t)j * a.payload_bytes;
                     const int32_t* rows_j = reinterpret_cast<const int32_t*>(pj + pl.rows_off) + cb;
-                    if (slot_search) {
+                    if (in_lds) {
+                        const int lo = s_sb[j][xs];
+                        const int q = find_row(s_run + s_roff[j] + (lo - s_sb[j][qa]), s_sb[j][xs + 1] - lo, x);
+                        p = q >= 0 ? lo + q : -1;
+                    } else if (slot_search) {
                         const int lo = s_sb[j][xs], hi = s_sb[j][xs + 1];
                         const int q = find_row(rows_j + lo, hi - lo, x);
                         p = q >= 0 ? lo + q : -1;
@@ -2110,6 +2193,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
                 pos[j] = p;  // LDS, read back by the same wave below (in-order LDS within a wave)
             }
             if (__ballot(lower) & gmask) continue;  // a lower rank owns this row (group-uniform)
+            pre = flat_row_preload<LPR>(a, t, grow, x, bb, sbb, sub);  // in flight with the values
             // owner: rank-ordered sum of the row's entries (ranks >= r)
             acc = make_float4(0.f, 0.f, 0.f, 0.f);
             if (pl.elem == 1 && N <= 8) {
@@ -2139,7 +2223,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
             }
         }
         const bool owned = own_mode && (xlo < 0 || (xlo >> 8) != (x >> 8)) && (xhi < 0 || (xhi >> 8) != (x >> 8));
-        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub, owned, own_mode ? &oq : nullptr);
+        flat_row_apply<LPR>(a, update, t, grow, x, nrows, bb, sbb, pre, acc, r_pack, sub, owned, own_mode ? &oq : nullptr);
     }
     if (own_mode) {  // owned blocks whose max holder shrank: re-reduce their 256 row maxima
         __syncthreads();

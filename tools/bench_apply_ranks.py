@@ -2,7 +2,7 @@
 k_table_apply, each + k_table_finalize) for N emulated ranks on
 one GPU: N different ranks' payloads (coalesce + quant-pack of N different batch slices)
 gathered into one buffer, exactly what the RCCL all-gather delivers at N GPUs.
-usage: python tools/bench_apply_ranks.py [terabyte|kaggle] [flat,slot,ranges,merge] [B per rank] [N list, e.g. 1,2,4,8] -> one JSON line per N"""
+usage: python tools/bench_apply_ranks.py [terabyte|tbsmall|kaggle] [flat,slot,ranges,merge] [B per rank] [N list, e.g. 1,2,4,8] -> one JSON line per N"""
 import json
 import os
 import sys
@@ -17,8 +17,10 @@ from deep_quantized_recommendation_model_dqrm_amd import _lib as L  # noqa: E402
 import gen_inputs as G  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "terabyte"
-D = 64 if cfg == "terabyte" else 16
-rows = [n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS] if cfg == "terabyte" else G.KAGGLE_ROWS
+D = 64 if cfg.startswith("tb") or cfg == "terabyte" else 16
+rows = [n * 16 if n >= 1_000_000 else n for n in G.TERABYTE_ROWS] if D == 64 else G.KAGGLE_ROWS
+if cfg == "tbsmall":  # the TB shape with every table capped at 2 M rows (~2 GB of W): the same entries, few TLB misses
+    rows = [min(n, 2_000_000) for n in rows]
 B = 2048
 T = len(rows)
 ts = dq.EmbeddingTableSet(rows, D, device="cuda", init="uniform", seed=3)
