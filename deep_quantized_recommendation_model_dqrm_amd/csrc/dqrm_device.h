@@ -258,59 +258,100 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     const uint32_t* sdw = flag_word(sdirty, sbb, &sh0);
     sh0 /= 8;
     const int64_t nwords = (ns + sh0 + 3) / 4;
-    // one superblock whose max holder shrank, by one wave: re-reduce its flagged blocks' 256
-    // rowmax (the owning lane keeps the new block max in a register), then the superblock
-    auto fix_superblock = [&](int64_t sb) {
-        const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
-        float nv[SBLK_BLOCKS / WAVE];
-        bool dq[SBLK_BLOCKS / WAVE];
-        const float old_sb = ld_h<WT>(sblkmax + sbb + sb);  // with the flags and block maxima: one round trip
+    // up to FB listed superblocks whose max holder shrank (list entries i0, i0 + nw, ...), by one
+    // wave, all their loads in flight together: their flags and block maxima (one round trip),
+    // then their flagged blocks' 256 rowmax DB blocks at a time (the owning lane keeps the new
+    // block max in a register), then the superblocks
+    constexpr int FB = 4, Q = SBLK_BLOCKS / WAVE, DB = 8;
+    __shared__ int s_fx[16][2 * DB];  // per wave: the dirty blocks of a pass (combo f*Q+q, lane)
+    __shared__ uint64_t s_dm[16][FB * Q];  // per wave: each combo's dirty-lane ballot
+    auto fix_batch = [&](const int* lst, int i0, int n) {
+        int64_t b0[FB];
+        float nv[FB][Q], old_sb[FB];
+        bool dq[FB][Q];
 #pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-            const int64_t b = b0 + lane + q * WAVE;
-            dq[q] = b < b1 && flag_get_h<WT>(bdirty, bb + b);
-            nv[q] = b < b1 ? ld_h<WT>(blkmax + bb + b) : 0.0f;
+        for (int f = 0; f < FB; ++f) {
+            const int i = i0 + f * nw;
+            const bool act = i < n;
+            const int64_t sb = act ? lst[i] : 0;
+            b0[f] = sb * SBLK_BLOCKS;
+            const int64_t b1 = act ? (b0[f] + SBLK_BLOCKS < nblk ? b0[f] + SBLK_BLOCKS : nblk) : b0[f];
+            old_sb[f] = act ? ld_h<WT>(sblkmax + sbb + sb) : 0.0f;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int64_t b = b0[f] + lane + q * WAVE;
+                dq[f][q] = b < b1 && flag_get_h<WT>(bdirty, bb + b);
+                nv[f][q] = b < b1 ? ld_h<WT>(blkmax + bb + b) : 0.0f;
+            }
         }
+        int* fx = s_fx[w];
+        auto flush = [&](int cnt) {  // cnt (wave-uniform) dirty blocks listed in fx
+            float x[DB];
 #pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
-            uint64_t dm = __ballot(dq[q]);
-            while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
-                constexpr int DB = 8;
-                int dl[DB];
-                float x[DB];
+            for (int i = 0; i < DB; ++i) {
+                x[i] = 0.0f;
+                if (i >= cnt) continue;
+                const int c = fx[2 * i], l = fx[2 * i + 1];
+                int64_t base = 0;
 #pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
-                    dm &= dm ? dm - 1 : 0;
-                }
+                for (int f = 0; f < FB; ++f)
+                    if (c / Q == f) base = b0[f];
+                const int64_t blk = base + (c % Q) * WAVE + l;
 #pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    x[i] = 0.0f;
-                    if (dl[i] < 0) continue;
-                    const int64_t blk = b0 + q * WAVE + dl[i];
-#pragma unroll
-                    for (int k = 0; k < BLK / WAVE; ++k) {
-                        const int64_t rr = blk * BLK + lane + k * WAVE;
-                        if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], ld_h<WT>(rowmax + m.row_base[t] + rr));
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < DB; ++i) {
-                    if (dl[i] < 0) continue;
-                    const float y = wave_max(x[i]);
-                    if (lane == dl[i]) nv[q] = y;
+                for (int k = 0; k < BLK / WAVE; ++k) {
+                    const int64_t rr = blk * BLK + lane + k * WAVE;
+                    if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], ld_h<WT>(rowmax + m.row_base[t] + rr));
                 }
             }
-            if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; flag_clear(bdirty, b0 + lane + q * WAVE + bb); }
-        }
-        float v = 0.0f;
 #pragma unroll
-        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
-        v = wave_max(v);
-        if (lane == 0) {
-            sblkmax[sbb + sb] = v;
-            flag_clear(sdirty, sbb + sb);
-            if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
+            for (int i = 0; i < DB; ++i) {
+                if (i >= cnt) continue;
+                const float y = wave_max(x[i]);
+                const int c = fx[2 * i], l = fx[2 * i + 1];
+#pragma unroll
+                for (int f = 0; f < FB; ++f)
+#pragma unroll
+                    for (int q = 0; q < Q; ++q)
+                        if (c == f * Q + q && lane == l) nv[f][q] = y;
+            }
+        };
+        uint64_t* dms = s_dm[w];
+#pragma unroll
+        for (int f = 0; f < FB; ++f)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) dms[f * Q + q] = __ballot(dq[f][q]);  // every lane: the same word
+        int cnt = 0;
+#pragma unroll 1
+        for (int c = 0; c < FB * Q; ++c) {
+            uint64_t dm = dms[c];
+            while (dm) {  // wave-uniform
+                fx[2 * cnt] = c;
+                fx[2 * cnt + 1] = __ffsll((long long)dm) - 1;
+                dm &= dm - 1;
+                if (++cnt == DB) {
+                    flush(DB);
+                    cnt = 0;
+                }
+            }
+        }
+        if (cnt) flush(cnt);
+#pragma unroll
+        for (int f = 0; f < FB; ++f) {
+            if (i0 + f * nw >= n) break;  // uniform
+            float v = 0.0f;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int64_t b = b0[f] + lane + q * WAVE;
+                if (dq[f][q]) { blkmax[b + bb] = nv[f][q]; flag_clear(bdirty, b + bb); }
+                v = fmaxf(v, nv[f][q]);
+            }
+            v = wave_max(v);
+            if (lane == 0) {
+                const int64_t sb = b0[f] / SBLK_BLOCKS;
+                sblkmax[sbb + sb] = v;
+                flag_clear(sdirty, sbb + sb);
+                if (v < old_sb[f] && old_sb[f] >= tmax0) s_rescan = 1;  // the table max may have shrunk
+            }
         }
     };
     // 1. list the flagged superblocks in LDS (one scan of the flag words); 2. one wave per
@@ -357,7 +398,8 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
             }
         }
         first = false;
-        for (int i = w; i < nd && i < FIN_LIST; i += nw) fix_superblock(s_dl[i]);
+        const int nl = nd < FIN_LIST ? nd : FIN_LIST;
+        for (int i0 = w; i0 < nl; i0 += nw * FB) fix_batch(s_dl, i0, nl);
         if (nd <= FIN_LIST) break;  // uniform
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cleared flags land before the next scan
         __syncthreads();

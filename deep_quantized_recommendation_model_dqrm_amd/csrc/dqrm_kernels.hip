@@ -1837,8 +1837,6 @@ DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
 
 constexpr int FLAT_TPB = 256;
 constexpr int FLAT_HDR_RANKS = 32;  // k_apply_flat: ranks whose slot bounds it keeps in LDS
-constexpr int QW_RANKS = 8;  // k_apply_flat: ranks whose rows are found by quantile windows (more: binary searches)
-constexpr int QW = 4;        //   window entries per lane (QW x LPR per rank)
 #ifndef DQRM_FLAT_PRELOAD
 #define DQRM_FLAT_PRELOAD 1  // 0: an A/B build reading the superblock / table max only on growth
 #endif
@@ -2102,88 +2100,23 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
         if (threadIdx.x == 0) s_oq_n = 0;
         __syncthreads();
     }
-    for (int e0 = blockIdx.x * G; e0 < cnt_r; e0 += gridDim.x * G) {
-        const int e = e0 + grp;
-        const bool valid = e < cnt_r;
-        const int32_t x = valid ? rows_r[e] : -1;
-        const int c0 = e0;  // the chunk's first entry
+    for (int e = blockIdx.x * G + grp; e < cnt_r; e += gridDim.x * G) {
+        const int32_t x = rows_r[e];
+        const int c0 = e - grp;  // the chunk's first entry
         const int32_t xlo = (own_mode && c0 > 0) ? rows_r[c0 - 1] : -1;
         const int32_t xhi = (own_mode && c0 + G < cnt_r) ? rows_r[c0 + G] : -1;
-        if (!valid) continue;
         if (x < 0 || x >= nrows) {  // cannot happen for payloads this library packed
             if (sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);
             continue;
         }
-        const int64_t grow = rb + x;
         float4 acc;
-        FlatPre pre;
         if (N == 1) {
-            pre = flat_row_preload<LPR>(a, t, grow, x, bb, sbb, sub);  // with the value: one round trip
             acc = src.load((uint32_t)e, sub);
         } else {  // where the other ranks hold row x (lane k searches ranks k, k+LPR, ...)
             bool lower = false;
             // the slot of row x (slot s holds blocks [nblk*s/8, nblk*(s+1)/8)): its run in each rank
             const int64_t nblk = (nrows + BLK - 1) / BLK;
             const int xs = slot_search ? (int)((8 * ((int64_t)(x >> 8) + 1) + nblk - 1) / nblk) - 1 : 0;
-            if (slot_search && N <= QW_RANKS) {
-                // quantile window: x is rank r's entry er of nr in slot xs, and rank j's entry of the same
-                // row (if any) sits near the same quantile of its nj entries (both are ascending samples of
-                // the slot's rows): the group loads QW * LPR entries of rank j around that position, every
-                // rank's window in ONE round trip, and matches them by ballot; a row outside its window
-                // (rare) is searched in the rest of the run
-                const int lr = s_sb[r][xs], nr = s_sb[r][xs + 1] - lr, er = e - lr;
-                constexpr int W = QW * LPR;
-                int32_t cand[QW_RANKS][QW];
-                int wlo[QW_RANKS], wn[QW_RANKS];
-#pragma unroll
-                for (int j = 0; j < QW_RANKS; ++j) {
-                    const bool act = j < N && j != r;
-                    const int lo = act ? s_sb[j][xs] : 0;
-                    const int nj = act ? s_sb[j][xs + 1] - lo : 0;
-                    int ws = nr > 0 ? (int)(((int64_t)(2 * er + 1) * nj) / (2 * (int64_t)nr)) - W / 2 : 0;
-                    ws = ws > nj - W ? nj - W : ws;
-                    ws = ws < 0 ? 0 : ws;
-                    wlo[j] = ws;
-                    wn[j] = nj - ws < W ? nj - ws : W;
-                    const int32_t* rj = reinterpret_cast<const int32_t*>(a.payloads + (int64_t)(act ? j : 0) * a.payload_bytes +
-                                                                         pl.rows_off) + cb + lo + ws;
-#pragma unroll
-                    for (int m = 0; m < QW; ++m) {
-                        const int i = sub + m * LPR;
-                        cand[j][m] = (act && i < wn[j]) ? rj[i] : 0;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < QW_RANKS; ++j) {
-                    if (j >= N) break;
-                    int p = e;
-                    if (j != r) {
-                        const int lo = s_sb[j][xs], nj = s_sb[j][xs + 1] - lo;
-                        p = -1;
-                        int below = 0;  // window entries < x
-#pragma unroll
-                        for (int m = 0; m < QW; ++m) {
-                            const bool in = sub + m * LPR < wn[j];
-                            const uint64_t hit = __ballot(in && cand[j][m] == x) & gmask;
-                            if (hit) p = lo + wlo[j] + (__ffsll((long long)(hit >> gbase)) - 1) + m * LPR;
-                            below += __popcll(__ballot(in && cand[j][m] < x) & gmask);
-                        }
-                        if (p < 0) {  // not in the window: absent unless x lies beyond one of its ends
-                            int flo = -1, fhi = -1;  // the rest of the run to search
-                            if (below == 0 && wlo[j] > 0) { flo = 0; fhi = wlo[j]; }
-                            else if (below == wn[j] && wlo[j] + wn[j] < nj) { flo = wlo[j] + wn[j]; fhi = nj; }
-                            if (flo >= 0) {
-                                const int32_t* rows_j = reinterpret_cast<const int32_t*>(
-                                    a.payloads + (int64_t)j * a.payload_bytes + pl.rows_off) + cb + lo;
-                                const int q = find_row(rows_j + flo, fhi - flo, x);
-                                p = q >= 0 ? lo + flo + q : -1;
-                            }
-                        }
-                        lower |= (j < r) && p >= 0;
-                    }
-                    if (sub == 0) pos[j] = p;  // LDS, read back by the group's wave below
-                }
-            } else {
             for (int j = sub; j < N; j += LPR) {
                 int p = e;
                 if (j != r) {
@@ -2200,9 +2133,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
                 }
                 pos[j] = p;  // LDS, read back by the same wave below (in-order LDS within a wave)
             }
-            }
             if (__ballot(lower) & gmask) continue;  // a lower rank owns this row (group-uniform)
-            pre = flat_row_preload<LPR>(a, t, grow, x, bb, sbb, sub);  // in flight with the values
             // owner: rank-ordered sum of the row's entries (ranks >= r)
             acc = make_float4(0.f, 0.f, 0.f, 0.f);
             if (pl.elem == 1 && N <= 8) {
@@ -2232,7 +2163,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
             }
         }
         const bool owned = own_mode && (xlo < 0 || (xlo >> 8) != (x >> 8)) && (xhi < 0 || (xhi >> 8) != (x >> 8));
-        flat_row_apply<LPR>(a, update, t, grow, x, nrows, bb, sbb, pre, acc, r_pack, sub, owned, own_mode ? &oq : nullptr);
+        flat_row_update<LPR>(a, update, t, rb + x, x, nrows, bb, sbb, acc, r_pack, sub, owned, own_mode ? &oq : nullptr);
     }
     if (own_mode) {  // owned blocks whose max holder shrank: re-reduce their 256 row maxima
         __syncthreads();
