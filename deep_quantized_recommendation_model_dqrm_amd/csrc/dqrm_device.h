@@ -194,14 +194,15 @@ DQRM_INLINE void pack4_row(const float4 w, uint8_t* __restrict__ prow, int idx4,
 // rowmax, block, superblock and table maxima rebuilt from W here (<= 256 rows x D floats),
 // unless rebuild_narrow is false (the updating kernel kept them exact like any table's).
 // WTS: the table max is stored write-through (read by other workgroups of the launch); U4:
-// loads in flight per thread in the flag and superblock scans. on_final() is called once by every
+// loads in flight per thread in the flag and superblock scans; FB: flagged superblocks a wave
+// fixes at once (> 1: 3 KiB more LDS, for the finalize launches, not the in-launch finalizes). on_final() is called once by every
 // thread of the workgroup as soon as the table max is final: with `tracked`, right after the flag
 // scan when no flagged superblock held the table max (the rest only fixes lower levels), else at
 // the end (k_finalize_fwd opens the table's forward gate there).
 struct NoFinal {
     DQRM_INLINE void operator()() const {}
 };
-template <bool WT, bool WTS = WT, int U4 = 4, class OnFinal = NoFinal>
+template <bool WT, bool WTS = WT, int U4 = 4, int FB = 1, class OnFinal = NoFinal>
 DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ W, float* __restrict__ rowmax,
                                float* __restrict__ blkmax, float* __restrict__ sblkmax,
                                uint8_t* __restrict__ sdirty, uint8_t* __restrict__ bdirty, float* __restrict__ tmax,
@@ -258,13 +259,68 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
     const uint32_t* sdw = flag_word(sdirty, sbb, &sh0);
     sh0 /= 8;
     const int64_t nwords = (ns + sh0 + 3) / 4;
+    // one superblock whose max holder shrank, by one wave: re-reduce its flagged blocks' 256
+    // rowmax (the owning lane keeps the new block max in a register), then the superblock
+    auto fix_superblock = [&](int64_t sb) {
+        const int64_t b0 = sb * SBLK_BLOCKS, b1 = b0 + SBLK_BLOCKS < nblk ? b0 + SBLK_BLOCKS : nblk;
+        float nv[SBLK_BLOCKS / WAVE];
+        bool dq[SBLK_BLOCKS / WAVE];
+        const float old_sb = ld_h<WT>(sblkmax + sbb + sb);  // with the flags and block maxima: one round trip
+#pragma unroll
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+            const int64_t b = b0 + lane + q * WAVE;
+            dq[q] = b < b1 && flag_get_h<WT>(bdirty, bb + b);
+            nv[q] = b < b1 ? ld_h<WT>(blkmax + bb + b) : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) {
+            uint64_t dm = __ballot(dq[q]);
+            while (dm) {  // up to DB dirty blocks per pass, all their loads in flight
+                constexpr int DB = 8;
+                int dl[DB];
+                float x[DB];
+#pragma unroll
+                for (int i = 0; i < DB; ++i) {
+                    dl[i] = dm ? __ffsll((long long)dm) - 1 : -1;  // wave-uniform
+                    dm &= dm ? dm - 1 : 0;
+                }
+#pragma unroll
+                for (int i = 0; i < DB; ++i) {
+                    x[i] = 0.0f;
+                    if (dl[i] < 0) continue;
+                    const int64_t blk = b0 + q * WAVE + dl[i];
+#pragma unroll
+                    for (int k = 0; k < BLK / WAVE; ++k) {
+                        const int64_t rr = blk * BLK + lane + k * WAVE;
+                        if (rr < m.num_rows[t]) x[i] = fmaxf(x[i], ld_h<WT>(rowmax + m.row_base[t] + rr));
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < DB; ++i) {
+                    if (dl[i] < 0) continue;
+                    const float y = wave_max(x[i]);
+                    if (lane == dl[i]) nv[q] = y;
+                }
+            }
+            if (dq[q]) { blkmax[b0 + lane + q * WAVE + bb] = nv[q]; flag_clear(bdirty, b0 + lane + q * WAVE + bb); }
+        }
+        float v = 0.0f;
+#pragma unroll
+        for (int q = 0; q < SBLK_BLOCKS / WAVE; ++q) v = fmaxf(v, nv[q]);
+        v = wave_max(v);
+        if (lane == 0) {
+            sblkmax[sbb + sb] = v;
+            flag_clear(sdirty, sbb + sb);
+            if (v < old_sb && old_sb >= tmax0) s_rescan = 1;  // the table max may have shrunk
+        }
+    };
     // up to FB listed superblocks whose max holder shrank (list entries i0, i0 + nw, ...), by one
     // wave, all their loads in flight together: their flags and block maxima (one round trip),
     // then their flagged blocks' 256 rowmax DB blocks at a time (the owning lane keeps the new
     // block max in a register), then the superblocks
-    constexpr int FB = 4, Q = SBLK_BLOCKS / WAVE, DB = 8;
-    __shared__ int s_fx[16][2 * DB];  // per wave: the dirty blocks of a pass (combo f*Q+q, lane)
-    __shared__ uint64_t s_dm[16][FB * Q];  // per wave: each combo's dirty-lane ballot
+    constexpr int Q = SBLK_BLOCKS / WAVE, DB = 8;
+    __shared__ int s_fx[FB > 1 ? 16 : 1][2 * DB];  // per wave: the dirty blocks of a pass (combo f*Q+q, lane)
+    __shared__ uint64_t s_dm[FB > 1 ? 16 : 1][FB * Q];  // per wave: each combo's dirty-lane ballot
     auto fix_batch = [&](const int* lst, int i0, int n) {
         int64_t b0[FB];
         float nv[FB][Q], old_sb[FB];
@@ -399,7 +455,11 @@ DQRM_INLINE void finalize_table(const Meta& m, int t, const float* __restrict__ 
         }
         first = false;
         const int nl = nd < FIN_LIST ? nd : FIN_LIST;
-        for (int i0 = w; i0 < nl; i0 += nw * FB) fix_batch(s_dl, i0, nl);
+        if constexpr (FB > 1) {
+            for (int i0 = w; i0 < nl; i0 += nw * FB) fix_batch(s_dl, i0, nl);
+        } else {
+            for (int i = w; i < nl; i += nw) fix_superblock(s_dl[i]);
+        }
         if (nd <= FIN_LIST) break;  // uniform
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cleared flags land before the next scan
         __syncthreads();

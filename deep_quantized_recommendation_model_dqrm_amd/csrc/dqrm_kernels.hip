@@ -1213,7 +1213,8 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
         __syncthreads();  // every thread has read the word before it is cleared
         if (threadIdx.x == 0) *fw = 0u;
     }
-    finalize_table<false>(m, t, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0, flagged == 0);
+    finalize_table<false, false, 4, 4>(m, t, W, rowmax, blkmax, sblkmax, sdirty, bdirty, tmax, D, tracked != 0,
+                                       flagged == 0);
 }
 
 // The flat apply's finalize and the next batch's forward in ONE launch (dqrm_apply_sparse_update_fwd
@@ -1256,7 +1257,7 @@ __global__ void __launch_bounds__(256) k_finalize_fwd(FwdArgs a, FinArgs f, int 
             if (threadIdx.x == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         };
         if (fin)  // the gate opens as soon as the table max is known final, the lower levels after it
-            finalize_table<false, true, 16>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
+            finalize_table<false, true, 16, 4>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
                                             f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0, open_gate);
         else
             open_gate();
