@@ -135,5 +135,8 @@ def test_bench_launcher_rccl_world1():
     assert line["value"] is not None and line["device_errors"] == 0
     assert line["collectives"]["backend"] == "nccl" and line["collectives"]["per_step"] == 2
     assert line["collectives"]["issued_by"].startswith("libdqrm")
-    assert line["config"]["n1_update"] == "coalesce + quant-pack + payload apply (RCCL at world size 1)"
+    assert line["config"]["n1_update"] in ("coalesce + quant-pack + payload apply (RCCL at world size 1)",
+                                           "coalesce + quant-pack + payload apply with the next forward "
+                                           "(RCCL at world size 1)")
+    assert line["kernels_ms"].get("apply_sparse_update_fwd") or line["kernels_ms"].get("apply_sparse_update")
     assert line["mlp_grad_exchange"]["collectives"] == 2
