@@ -266,7 +266,7 @@ DQRM_INLINE void wait_gate(const uint32_t* gate, uint32_t spin, uint32_t* err) {
 // (k_finalize_fwd): the table max is final only once the table's finalize workgroup opened its
 // gate, so the scale is taken after the first pass's index and row loads are in flight (W
 // itself is final at launch start), and every workgroup passes the gate once.
-template <int LPR, int UNR, bool WT, bool GATE = false>
+template <int LPR, int UNR, bool WT, bool GATE = false, int TPB = 256>
 __device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t bx, int64_t gx) {
     const bool full_precision = (a.flags & DQRM_FWD_FULL_PRECISION) != 0;
     const bool refresh = (a.flags & DQRM_FWD_REFRESH_SCALE) != 0;
@@ -293,7 +293,7 @@ __device__ __forceinline__ void emb_fwd_table(const FwdArgs& a, int t, int64_t b
 
     const float qlo = -(float)(1 << (a.bits - 1));
     const float qhi = (float)((1 << (a.bits - 1)) - 1);
-    constexpr int G = 256 / LPR;  // bags per workgroup pass
+    constexpr int G = TPB / LPR;  // bags per workgroup pass
     const int lane = threadIdx.x % LPR;
     const int grp = threadIdx.x / LPR;
     const int D = LPR * 4;
@@ -1220,7 +1220,7 @@ __global__ void __launch_bounds__(1024) k_table_finalize(const float* __restrict
 // The flat apply's finalize and the next batch's forward in ONE launch (dqrm_apply_sparse_update_fwd
 // / dqrm_exchange_apply_fwd with the flat apply kernel: weight_update_parallel_comm, s_q_g_p_c.py:601-628,
 // then the next apply_emb, single_gpu.py:609-674). Workgroups 0..T-1 finalize one table each as
-// k_table_finalize does (256 threads, 16 loads in flight per thread in the scans), store the table max
+// k_table_finalize does (1024 threads), store the table max
 // write-through and open the table's gate; the forward workgroups behind them (k_emb_fwd's grid, table
 // by table) issue their index and row loads at once -- W is final at launch start, only the
 // maxima may still move -- and take the scale from the table max once the gate is open. The gates
@@ -1238,8 +1238,10 @@ struct FinArgs {
     int tracked, flagged;
 };
 
+constexpr int FINFWD_TPB = 1024;  // the finalize's 16 waves (as k_table_finalize); the forward's bag passes alike
+
 template <int LPR, int UNR>
-__global__ void __launch_bounds__(256) k_finalize_fwd(FwdArgs a, FinArgs f, int gx) {
+__global__ void __launch_bounds__(FINFWD_TPB) k_finalize_fwd(FwdArgs a, FinArgs f, int gx) {
     const int T = a.T;
     if ((int)blockIdx.x < T) {
         const int t = blockIdx.x;
@@ -1257,15 +1259,15 @@ __global__ void __launch_bounds__(256) k_finalize_fwd(FwdArgs a, FinArgs f, int 
             if (threadIdx.x == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         };
         if (fin)  // the gate opens as soon as the table max is known final, the lower levels after it
-            finalize_table<false, true, 16, 4>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
-                                            f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0, open_gate);
+            finalize_table<false, true, 4, 1>(make_meta(a.meta, T), t, f.W, f.rowmax, f.blkmax, f.sblkmax, f.sdirty,
+                                              f.bdirty, f.tmax, f.D, f.tracked != 0, f.flagged == 0, open_gate);
         else
             open_gate();
         return;
     }
     const int id = (int)blockIdx.x - T;
     const int t = id / gx;
-    emb_fwd_table<LPR, UNR, false, true>(a, t, id - t * gx, gx);
+    emb_fwd_table<LPR, UNR, false, true, FINFWD_TPB>(a, t, id - t * gx, gx);
 }
 
 // gather the lookups of table t whose row falls in [r0, r1) as keys (row << 32 | bag);
@@ -4716,12 +4718,12 @@ static int launch_finalize_fwd(const dqrm_table_set* set, FwdArgs fa, hipStream_
               1, fin_flagged_skip() ? 1 : 0};
     DISPATCH_LPR(set->dim, {
         constexpr int UNR = 4;
-        constexpr int BAGS_PER_WG = (256 / LPR) * UNR;
+        constexpr int BAGS_PER_WG = (FINFWD_TPB / LPR) * UNR;
         int64_t bx = (fa.B + BAGS_PER_WG - 1) / BAGS_PER_WG;
-        const int64_t cap = (8192 + fa.T - 1) / fa.T;  // as dqrm_emb_fwd: ~8k forward workgroups, grid-stride beyond
+        const int64_t cap = (2048 + fa.T - 1) / fa.T;  // ~2k forward workgroups of 1024 threads, grid-stride beyond
         if (bx > cap) bx = cap;
         const int64_t grid = (int64_t)fa.T * (1 + bx);
-        hipLaunchKernelGGL((k_finalize_fwd<LPR, UNR>), dim3((unsigned)grid), dim3(256), 0, st, fa, f, (int)bx);
+        hipLaunchKernelGGL((k_finalize_fwd<LPR, UNR>), dim3((unsigned)grid), dim3(FINFWD_TPB), 0, st, fa, f, (int)bx);
     });
     LAUNCH_CHECK();
     return DQRM_OK;
