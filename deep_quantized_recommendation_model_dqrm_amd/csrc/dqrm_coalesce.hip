@@ -1675,7 +1675,7 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             __syncthreads();
         }
         if (s_fin) {
-            if constexpr (FWD) {
+            if (FWD && !la.late_pub) {
                 // the table's final max is published as soon as it is known (usually right after the
                 // flag scan: no flagged superblock held it), not after the block re-reductions, so
                 // the table's forward shares start while this workgroup finishes the lower levels
