@@ -1675,12 +1675,13 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             __syncthreads();
         }
         if (s_fin) {
-            if (FWD && !la.late_pub) {
+            if constexpr (FWD) {
                 // the table's final max is published as soon as it is known (usually right after the
                 // flag scan: no flagged superblock held it), not after the block re-reductions, so
                 // the table's forward shares start while this workgroup finishes the lower levels
                 uint64_t* fw = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
                 auto publish = [&]() {
+                    if (la.late_pub) return;  // (A/B: published after the finalize, below)
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a rescanned table max has landed
                     __syncthreads();
                     if (tid == 0) {
