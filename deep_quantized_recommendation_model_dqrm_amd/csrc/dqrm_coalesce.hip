@@ -1674,32 +1674,9 @@ __global__ void __launch_bounds__(TPB) k_coalesce_p1(dqrm_internal::CoalesceArgs
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
-        if (s_fin) {
-            if constexpr (FWD) {
-                // the table's final max is published as soon as it is known (usually right after the
-                // flag scan: no flagged superblock held it), not after the block re-reductions, so
-                // the table's forward shares start while this workgroup finishes the lower levels
-                uint64_t* fw = reinterpret_cast<uint64_t*>(la.sync + (int64_t)t * DQRM_SYNC_STRIDE + FWD_WORD);
-                auto publish = [&]() {
-                    if (la.late_pub) return;  // (A/B: published after the finalize, below)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a rescanned table max has landed
-                    __syncthreads();
-                    if (tid == 0) {
-                        const float tm = ld_wt(la.tmax + t);
-                        s_ftm = tm;
-                        s_fok = 1;
-                        s_pub = 1;
-                        __hip_atomic_store(fw, gr_make(tm, 0, epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    __syncthreads();
-                };
-                finalize_table<true, true, 4, 1>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax,
-                                                 la.sdirty, la.bdirty, la.tmax, a.D, true, false, publish);
-            } else {
-                finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
-                                     la.bdirty, la.tmax, a.D, true, false);
-            }
-        }
+        if (s_fin)
+            finalize_table<true>(make_meta(a.meta, a.T), t, la.W, la.rowmax, la.blkmax, la.sblkmax, la.sdirty,
+                                 la.bdirty, la.tmax, a.D, true, false);
         CDIAG_W(13);
         // 9. the NEXT batch's forward (dqrm_emb_bwd_apply_fwd_local): emb_fwd_table's
         //    arithmetic for pooling 1, y[b] = fake-quant(W[row_b]) with the scale of the updated

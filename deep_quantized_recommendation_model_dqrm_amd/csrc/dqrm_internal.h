@@ -68,7 +68,6 @@ struct LocalApplyArgs {
     float* fwd_scale;           // [T] the forward scale: written (refresh) or read (held)
     int fwd_bits;
     uint32_t fwd_flags;
-    int late_pub;               // 1: publish the table max after the whole finalize (DQRM_EARLY_PUB=0, A/B)
 };
 constexpr int kSubTables = 32;  // LocalApplyArgs::sub_table entries
 

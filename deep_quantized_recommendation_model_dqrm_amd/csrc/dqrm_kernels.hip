@@ -5127,11 +5127,6 @@ static int bwd_apply_local(const dqrm_table_set* set, const dqrm_batch* batch, c
         if (fused_fwd) {
             la.fwd_idx = ff->next->idx; la.fwd_out = ff->out; la.fwd_ost_t = ff->ost_t; la.fwd_ost_b = ff->ost_b;
             la.fwd_scale = set->scale; la.fwd_bits = ff->bits; la.fwd_flags = ff->flags;
-            static const int late = [] {
-                const char* e = getenv("DQRM_EARLY_PUB");
-                return e && !strcmp(e, "0") ? 1 : 0;
-            }();
-            la.late_pub = late;
         }
         const hipError_t e = dqrm_internal::launch_coalesce_pool1(ca, &la, (hipStream_t)stream);
         if (e != hipSuccess)
