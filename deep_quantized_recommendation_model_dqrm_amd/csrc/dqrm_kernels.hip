@@ -1828,14 +1828,17 @@ DQRM_INLINE int table_entry_count(const unsigned char* payload, int t, int64_t c
     return c < cap ? c : (int)cap;
 }
 
-// position of row x in an ascending row list of n entries, or -1
+// position of row x in an ascending list of n distinct rows, or -1. A present row is probed on
+// the way (the lower bound ends where a probe set hi = its position), so no load after the loop
 DQRM_INLINE int find_row(const int32_t* rows, int n, int32_t x) {
-    int lo = 0, hi = n;
+    int lo = 0, hi = n, found = -1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (rows[mid] < x) lo = mid + 1; else hi = mid;
+        const int32_t v = rows[mid];
+        if (v == x) found = mid;
+        if (v < x) lo = mid + 1; else hi = mid;
     }
-    return (lo < n && rows[lo] == x) ? lo : -1;
+    return found;
 }
 
 constexpr int FLAT_TPB = 256;
