@@ -2204,6 +2204,156 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     }
 }
 
+// two binary searches (find_row's) interleaved: their dependent loads share round trips
+DQRM_INLINE void find_row2(const int32_t* ra, int na, int32_t xa, const int32_t* rb2, int nb, int32_t xb, int* pa,
+                           int* pb) {
+    int loa = 0, hia = na, lob = 0, hib = nb, fa = -1, fb = -1;
+    while (loa < hia || lob < hib) {
+        const bool ga = loa < hia, gb = lob < hib;
+        const int ma = (loa + hia) >> 1, mb = (lob + hib) >> 1;
+        const int32_t va = ga ? ra[ma] : 0;
+        const int32_t vb = gb ? rb2[mb] : 0;
+        if (ga) {
+            if (va == xa) fa = ma;
+            if (va < xa) loa = ma + 1; else hia = ma;
+        }
+        if (gb) {
+            if (vb == xb) fb = mb;
+            if (vb < xb) lob = mb + 1; else hib = mb;
+        }
+    }
+    *pa = fa;
+    *pb = fb;
+}
+
+// k_apply_flat for 1 < N <= FLAT_HDR_RANKS ranks with the finalize launch after it (the default):
+// each lane group takes TWO entries of rank r's payload (e and e + G), whose searches in the other
+// ranks' slot runs, value loads and row loads share their round trips -- twice the entries in
+// flight per wave at nearly the same registers. Same arithmetic, ownership and |W| upkeep.
+// DQRM_FLAT_DUAL=0: k_apply_flat (A/B).
+template <int LPR>
+__global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
+    constexpr int D = LPR * 4;
+    constexpr int G = FLAT_TPB / LPR;
+    __shared__ int s_pos[2][G][DQRM_MAX_RANKS];
+    __shared__ int s_sb[FLAT_HDR_RANKS][SPLIT + 1];
+    const int t = blockIdx.y, r = blockIdx.z;
+    const int T = a.T, N = a.N;
+    const Meta m = make_meta(a.meta, T);
+    const PayloadLayout pl = payload_layout(T, a.cap_total, D, a.bits);
+    const int64_t cb = a.cap_base[t];
+    const int64_t cap = a.cap_base[t + 1] - cb;
+    const unsigned char* pr = a.payloads + (int64_t)r * a.payload_bytes;
+    if ((int)threadIdx.x < N * SPLIT) {  // every rank's slot bounds of table t (as k_apply_flat)
+        const int j = threadIdx.x / SPLIT, q = threadIdx.x % SPLIT;
+        int c = reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes)[t * SPLIT + q];
+        c = c > 0 ? c : 0;
+        int inc = c;
+#pragma unroll
+        for (int o = 1; o < SPLIT; o <<= 1) {
+            const int y = __shfl_up(inc, o, SPLIT);
+            if (q >= o) inc += y;
+        }
+        s_sb[j][q + 1] = inc < cap ? inc : (int)cap;
+        if (q == 0) s_sb[j][0] = 0;
+    }
+    __syncthreads();
+    const int cnt_r = s_sb[r][SPLIT];
+    if ((int64_t)blockIdx.x * 2 * G >= cnt_r) return;
+    const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
+    const int64_t nblk = (nrows + BLK - 1) / BLK;
+    const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
+    const ApplyUpdate update{a.mode, (float)(1.0 / (double)N), sc, (float)((double)sc / (double)N), a.nlr};
+    const float r_pack = a.repack ? 1.0f / a.pscale[t] : 0.0f;
+    const PayloadSource<LPR> src{a.payloads, a.payload_bytes, pl, cb, 0};
+    const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+    const int gbase = (threadIdx.x % WAVE) - sub;
+    const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
+    const int32_t* rows_r = reinterpret_cast<const int32_t*>(pr + pl.rows_off) + cb;
+    for (int e0 = blockIdx.x * 2 * G + grp; e0 < cnt_r; e0 += gridDim.x * 2 * G) {
+        int ee[2], xs[2];
+        int32_t xx[2];
+        bool ok[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            ee[k] = e0 + k * G;
+            const bool has = ee[k] < cnt_r;
+            xx[k] = has ? rows_r[ee[k]] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool has = ee[k] < cnt_r;
+            ok[k] = has && xx[k] >= 0 && xx[k] < nrows;
+            if (has && !ok[k] && sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);  // (never for packed payloads)
+            xs[k] = ok[k] ? (int)((8 * ((int64_t)(xx[k] >> 8) + 1) + nblk - 1) / nblk) - 1 : 0;
+        }
+        bool lower[2] = {false, false};
+        for (int j = sub; j < N; j += LPR) {  // lane k searches ranks k, k+LPR, ... for both entries
+            int p0 = ee[0], p1 = ee[1];
+            if (j != r) {
+                const int32_t* rows_j =
+                    reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes + pl.rows_off) + cb;
+                const int lo0 = s_sb[j][xs[0]], lo1 = s_sb[j][xs[1]];
+                const int n0 = ok[0] ? s_sb[j][xs[0] + 1] - lo0 : 0, n1 = ok[1] ? s_sb[j][xs[1] + 1] - lo1 : 0;
+                int q0, q1;
+                find_row2(rows_j + lo0, n0, xx[0], rows_j + lo1, n1, xx[1], &q0, &q1);
+                p0 = q0 >= 0 ? lo0 + q0 : -1;
+                p1 = q1 >= 0 ? lo1 + q1 : -1;
+                lower[0] |= (j < r) && p0 >= 0;
+                lower[1] |= (j < r) && p1 >= 0;
+            }
+            s_pos[0][grp][j] = p0;  // LDS, read back by the same wave below
+            s_pos[1][grp][j] = p1;
+        }
+        bool own[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) own[k] = ok[k] && !(__ballot(lower[k]) & gmask);  // lowest holding rank owns it
+        FlatPre pre[2];
+        float4 acc[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (own[k]) pre[k] = flat_row_preload<LPR>(a, t, rb + xx[k], xx[k], bb, sbb, sub);
+        }
+        if (pl.elem == 1 && N <= 8) {  // int8: both entries' values of every rank in one round trip
+            uint32_t raw[2][8];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = j < N ? s_pos[k][grp][j] : -1;
+                    const bool v = own[k] && j >= r && p >= 0;
+                    raw[k][j] = reinterpret_cast<const uint32_t*>(a.payloads + (int64_t)(j < N ? j : 0) * a.payload_bytes +
+                                                                  pl.vals_off + (cb + (v ? p : 0)) * D)[sub];
+                    if (!v) raw[k][j] = 0u;
+                }
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {  // ascending rank order (integers: exact)
+                    const uint32_t v = raw[k][j];
+                    acc[k].x += (float)(int8_t)(v & 0xFF); acc[k].y += (float)(int8_t)((v >> 8) & 0xFF);
+                    acc[k].z += (float)(int8_t)((v >> 16) & 0xFF); acc[k].w += (float)(int8_t)(v >> 24);
+                }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!own[k]) continue;
+                bool first = true;
+                for (int j = r; j < N; ++j) {
+                    const int p = s_pos[k][grp][j];
+                    if (p >= 0) acc[k] = combine<OP_SUM>(acc[k], src.load(((uint32_t)j << 24) | (uint32_t)p, sub), first, 0.0f);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (own[k])
+                flat_row_apply<LPR>(a, update, t, rb + xx[k], xx[k], nrows, bb, sbb, pre[k], acc[k], r_pack, sub, false,
+                                    nullptr);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Sort and gather helpers of the fused backward (K4, below): a workgroup of SORT_TPB threads
 // sorts one slot's (row << 32 | position) keys in LDS or in the caller's workspace.
@@ -4938,7 +5088,14 @@ static int apply_update_ex(const dqrm_table_set* set, const int64_t* cap_base, i
             const int64_t lim = (32768 + (int64_t)a.T * num_ranks - 1) / ((int64_t)a.T * num_ranks);
             if (gx > lim) gx = lim;
             if (gx < 1) gx = 1;
-            if (a.fin_launch)
+            static const bool dual = [] {  // DQRM_FLAT_DUAL=0: one entry per lane group (A/B)
+                const char* e = getenv("DQRM_FLAT_DUAL");
+                return !(e && !strcmp(e, "0"));
+            }();
+            if (a.fin_launch && dual && num_ranks > 1 && num_ranks <= FLAT_HDR_RANKS)
+                hipLaunchKernelGGL((k_apply_flat2<LPR>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
+                                   dim3(FLAT_TPB), 0, st, a);
+            else if (a.fin_launch)
                 hipLaunchKernelGGL((k_apply_flat<LPR, false>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
                                    dim3(FLAT_TPB), 0, st, a);
             else
