@@ -2230,7 +2230,7 @@ DQRM_INLINE void find_row2(const int32_t* ra, int na, int32_t xa, const int32_t*
 // each lane group takes TWO entries of rank r's payload (e and e + G), whose searches in the other
 // ranks' slot runs, value loads and row loads share their round trips -- twice the entries in
 // flight per wave at nearly the same registers. Same arithmetic, ownership and |W| upkeep.
-// DQRM_FLAT_DUAL=0: k_apply_flat (A/B).
+// Taken when the tables average >= 512 entries (apply_update_ex); DQRM_FLAT_DUAL=0/1 forces it.
 template <int LPR>
 __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
     constexpr int D = LPR * 4;
@@ -5088,10 +5088,12 @@ static int apply_update_ex(const dqrm_table_set* set, const int64_t* cap_base, i
             const int64_t lim = (32768 + (int64_t)a.T * num_ranks - 1) / ((int64_t)a.T * num_ranks);
             if (gx > lim) gx = lim;
             if (gx < 1) gx = 1;
-            static const bool dual = [] {  // DQRM_FLAT_DUAL=0: one entry per lane group (A/B)
-                const char* e = getenv("DQRM_FLAT_DUAL");
-                return !(e && !strcmp(e, "0"));
-            }();
+            // two entries per lane group when the tables hold enough entries to keep the chip busy
+            // at half the workgroups (same box, TB: 2048 per rank 129 vs 142 us at N = 8, 44 vs 48 at
+            // N = 2; 256 per rank slower: 20 vs 14 us at N = 2); DQRM_FLAT_DUAL=0/1 forces it
+            const char* dual_e = getenv("DQRM_FLAT_DUAL");  // read per call (tests switch it)
+            const int dual_env = dual_e ? atoi(dual_e) : -1;
+            const bool dual = dual_env >= 0 ? dual_env != 0 : cap_total >= (int64_t)512 * a.T;
             if (a.fin_launch && dual && num_ranks > 1 && num_ranks <= FLAT_HDR_RANKS)
                 hipLaunchKernelGGL((k_apply_flat2<LPR>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
                                    dim3(FLAT_TPB), 0, st, a);
