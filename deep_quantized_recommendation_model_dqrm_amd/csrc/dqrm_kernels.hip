@@ -2204,26 +2204,32 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat(ApplyArgs a) {
     }
 }
 
-// two binary searches (find_row's) interleaved: their dependent loads share round trips
-DQRM_INLINE void find_row2(const int32_t* ra, int na, int32_t xa, const int32_t* rb2, int nb, int32_t xb, int* pa,
-                           int* pb) {
-    int loa = 0, hia = na, lob = 0, hib = nb, fa = -1, fb = -1;
-    while (loa < hia || lob < hib) {
-        const bool ga = loa < hia, gb = lob < hib;
-        const int ma = (loa + hia) >> 1, mb = (lob + hib) >> 1;
-        const int32_t va = ga ? ra[ma] : 0;
-        const int32_t vb = gb ? rb2[mb] : 0;
-        if (ga) {
-            if (va == xa) fa = ma;
-            if (va < xa) loa = ma + 1; else hia = ma;
-        }
-        if (gb) {
-            if (vb == xb) fb = mb;
-            if (vb < xb) lob = mb + 1; else hib = mb;
+// E binary searches (find_row's) interleaved: their dependent loads share round trips
+template <int E>
+DQRM_INLINE void find_rows(const int32_t* const* rs, const int* ns, const int32_t* xs, int* found) {
+    int lo[E], hi[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        lo[k] = 0;
+        hi[k] = ns[k];
+        found[k] = -1;
+    }
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < E; ++k) any |= lo[k] < hi[k];
+        if (!any) break;
+        int32_t v[E];
+#pragma unroll
+        for (int k = 0; k < E; ++k) v[k] = lo[k] < hi[k] ? rs[k][(lo[k] + hi[k]) >> 1] : 0;
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            if (lo[k] >= hi[k]) continue;
+            const int mid = (lo[k] + hi[k]) >> 1;
+            if (v[k] == xs[k]) found[k] = mid;
+            if (v[k] < xs[k]) lo[k] = mid + 1; else hi[k] = mid;
         }
     }
-    *pa = fa;
-    *pb = fb;
 }
 
 // k_apply_flat for 1 < N <= FLAT_HDR_RANKS ranks with the finalize launch after it (the default):
@@ -2231,11 +2237,11 @@ DQRM_INLINE void find_row2(const int32_t* ra, int na, int32_t xa, const int32_t*
 // ranks' slot runs, value loads and row loads share their round trips -- twice the entries in
 // flight per wave at nearly the same registers. Same arithmetic, ownership and |W| upkeep.
 // Taken when the tables average >= 512 entries (apply_update_ex); DQRM_FLAT_DUAL=0/1 forces it.
-template <int LPR>
+template <int LPR, int E>
 __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
     constexpr int D = LPR * 4;
     constexpr int G = FLAT_TPB / LPR;
-    __shared__ int s_pos[2][G][DQRM_MAX_RANKS];
+    __shared__ int s_pos[E][G][DQRM_MAX_RANKS];
     __shared__ int s_sb[FLAT_HDR_RANKS][SPLIT + 1];
     const int t = blockIdx.y, r = blockIdx.z;
     const int T = a.T, N = a.N;
@@ -2259,7 +2265,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
     }
     __syncthreads();
     const int cnt_r = s_sb[r][SPLIT];
-    if ((int64_t)blockIdx.x * 2 * G >= cnt_r) return;
+    if ((int64_t)blockIdx.x * E * G >= cnt_r) return;
     const int64_t nrows = m.num_rows[t], rb = m.row_base[t], bb = m.blk_base[t], sbb = m.sblk_base[t];
     const int64_t nblk = (nrows + BLK - 1) / BLK;
     const float sc = (a.mode == DQRM_UPD_FP32) ? 1.0f : a.s_avg[t];
@@ -2270,55 +2276,66 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
     const int gbase = (threadIdx.x % WAVE) - sub;
     const uint64_t gmask = (LPR >= WAVE ? ~0ull : ((1ull << LPR) - 1ull)) << gbase;
     const int32_t* rows_r = reinterpret_cast<const int32_t*>(pr + pl.rows_off) + cb;
-    for (int e0 = blockIdx.x * 2 * G + grp; e0 < cnt_r; e0 += gridDim.x * 2 * G) {
-        int ee[2], xs[2];
-        int32_t xx[2];
-        bool ok[2];
+    for (int e0 = blockIdx.x * E * G + grp; e0 < cnt_r; e0 += gridDim.x * E * G) {
+        int ee[E], xs[E];
+        int32_t xx[E];
+        bool ok[E];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < E; ++k) {
             ee[k] = e0 + k * G;
             const bool has = ee[k] < cnt_r;
             xx[k] = has ? rows_r[ee[k]] : -1;
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < E; ++k) {
             const bool has = ee[k] < cnt_r;
             ok[k] = has && xx[k] >= 0 && xx[k] < nrows;
             if (has && !ok[k] && sub == 0) flag_error(a.err, DQRM_ERRF_INDEX);  // (never for packed payloads)
             xs[k] = ok[k] ? (int)((8 * ((int64_t)(xx[k] >> 8) + 1) + nblk - 1) / nblk) - 1 : 0;
         }
-        bool lower[2] = {false, false};
-        for (int j = sub; j < N; j += LPR) {  // lane k searches ranks k, k+LPR, ... for both entries
-            int p0 = ee[0], p1 = ee[1];
+        bool lower[E];
+#pragma unroll
+        for (int k = 0; k < E; ++k) lower[k] = false;
+        for (int j = sub; j < N; j += LPR) {  // lane k searches ranks k, k+LPR, ... for all E entries
+            int p[E];
             if (j != r) {
                 const int32_t* rows_j =
                     reinterpret_cast<const int32_t*>(a.payloads + (int64_t)j * a.payload_bytes + pl.rows_off) + cb;
-                const int lo0 = s_sb[j][xs[0]], lo1 = s_sb[j][xs[1]];
-                const int n0 = ok[0] ? s_sb[j][xs[0] + 1] - lo0 : 0, n1 = ok[1] ? s_sb[j][xs[1] + 1] - lo1 : 0;
-                int q0, q1;
-                find_row2(rows_j + lo0, n0, xx[0], rows_j + lo1, n1, xx[1], &q0, &q1);
-                p0 = q0 >= 0 ? lo0 + q0 : -1;
-                p1 = q1 >= 0 ? lo1 + q1 : -1;
-                lower[0] |= (j < r) && p0 >= 0;
-                lower[1] |= (j < r) && p1 >= 0;
+                const int32_t* rs[E];
+                int lo[E], nn[E], q[E];
+#pragma unroll
+                for (int k = 0; k < E; ++k) {
+                    lo[k] = s_sb[j][xs[k]];
+                    nn[k] = ok[k] ? s_sb[j][xs[k] + 1] - lo[k] : 0;
+                    rs[k] = rows_j + lo[k];
+                }
+                find_rows<E>(rs, nn, xx, q);
+#pragma unroll
+                for (int k = 0; k < E; ++k) {
+                    p[k] = q[k] >= 0 ? lo[k] + q[k] : -1;
+                    lower[k] |= (j < r) && p[k] >= 0;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < E; ++k) p[k] = ee[k];
             }
-            s_pos[0][grp][j] = p0;  // LDS, read back by the same wave below
-            s_pos[1][grp][j] = p1;
+#pragma unroll
+            for (int k = 0; k < E; ++k) s_pos[k][grp][j] = p[k];  // LDS, read back by the same wave below
         }
-        bool own[2];
+        bool own[E];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) own[k] = ok[k] && !(__ballot(lower[k]) & gmask);  // lowest holding rank owns it
-        FlatPre pre[2];
-        float4 acc[2];
+        for (int k = 0; k < E; ++k) own[k] = ok[k] && !(__ballot(lower[k]) & gmask);  // lowest holding rank owns it
+        FlatPre pre[E];
+        float4 acc[E];
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < E; ++k) {
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (own[k]) pre[k] = flat_row_preload<LPR>(a, t, rb + xx[k], xx[k], bb, sbb, sub);
         }
         if (pl.elem == 1 && N <= 8) {  // int8: both entries' values of every rank in one round trip
-            uint32_t raw[2][8];
+            uint32_t raw[E][8];
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < E; ++k)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const int p = j < N ? s_pos[k][grp][j] : -1;
@@ -2328,7 +2345,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
                     if (!v) raw[k][j] = 0u;
                 }
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < E; ++k)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {  // ascending rank order (integers: exact)
                     const uint32_t v = raw[k][j];
@@ -2337,7 +2354,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
                 }
         } else {
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < E; ++k) {
                 if (!own[k]) continue;
                 bool first = true;
                 for (int j = r; j < N; ++j) {
@@ -2347,7 +2364,7 @@ __global__ void __launch_bounds__(FLAT_TPB) k_apply_flat2(ApplyArgs a) {
             }
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < E; ++k)
             if (own[k])
                 flat_row_apply<LPR>(a, update, t, rb + xx[k], xx[k], nrows, bb, sbb, pre[k], acc[k], r_pack, sub, false,
                                     nullptr);
@@ -5094,8 +5111,11 @@ static int apply_update_ex(const dqrm_table_set* set, const int64_t* cap_base, i
             const char* dual_e = getenv("DQRM_FLAT_DUAL");  // read per call (tests switch it)
             const int dual_env = dual_e ? atoi(dual_e) : -1;
             const bool dual = dual_env >= 0 ? dual_env != 0 : cap_total >= (int64_t)512 * a.T;
-            if (a.fin_launch && dual && num_ranks > 1 && num_ranks <= FLAT_HDR_RANKS)
-                hipLaunchKernelGGL((k_apply_flat2<LPR>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
+            if (a.fin_launch && dual && num_ranks > 1 && num_ranks <= FLAT_HDR_RANKS && dual_env == 4)
+                hipLaunchKernelGGL((k_apply_flat2<LPR, (LPR >= 4 ? 4 : 2)>), dim3((unsigned)gx, (unsigned)a.T,
+                                   (unsigned)num_ranks), dim3(FLAT_TPB), 0, st, a);  // (LDS: E = 4 needs LPR >= 4)
+            else if (a.fin_launch && dual && num_ranks > 1 && num_ranks <= FLAT_HDR_RANKS)
+                hipLaunchKernelGGL((k_apply_flat2<LPR, 2>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),
                                    dim3(FLAT_TPB), 0, st, a);
             else if (a.fin_launch)
                 hipLaunchKernelGGL((k_apply_flat<LPR, false>), dim3((unsigned)gx, (unsigned)a.T, (unsigned)num_ranks),

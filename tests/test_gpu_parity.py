@@ -29,17 +29,17 @@ def dq():
     return d
 
 
-@pytest.fixture(params=["flat", "flat2", "slot", "ranges", "merge"])
+@pytest.fixture(params=["flat", "flat2", "flat4", "slot", "ranges", "merge"])
 def apply_kernel(request, dq):
     """Run the test once per dqrm_apply_sparse_update kernel (the AUTO choice depends on N);
-    flat2: the flat kernel's two-entries-per-lane-group form (k_apply_flat2, N > 1), forced."""
+    flat2 / flat4: the flat kernel with two / four entries per lane group (k_apply_flat2, N > 1), forced."""
     L = dq._lib
     lib = L.load()
-    kind = {"flat": L.DQRM_APPLY_FLAT, "flat2": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT,
+    kind = {"flat": L.DQRM_APPLY_FLAT, "flat2": L.DQRM_APPLY_FLAT, "flat4": L.DQRM_APPLY_FLAT, "slot": L.DQRM_APPLY_SLOT,
             "ranges": L.DQRM_APPLY_RANGES, "merge": L.DQRM_APPLY_MERGE}[request.param]
     prev = lib.dqrm_set_apply_kernel(kind)
     old = os.environ.get("DQRM_FLAT_DUAL")
-    os.environ["DQRM_FLAT_DUAL"] = "1" if request.param == "flat2" else "0"
+    os.environ["DQRM_FLAT_DUAL"] = {"flat2": "2", "flat4": "4"}.get(request.param, "0")
     yield request.param
     if old is None:
         os.environ.pop("DQRM_FLAT_DUAL", None)
