@@ -147,11 +147,12 @@ KERNEL_SYMBOL = {  # bench phase -> libdqrm kernel (as named in the rocprofv3 su
     "bwd_sgd": ("k_sgd_small<{lpr}, false>", "k_sgd_small<{lpr}>", "k_bwd_fused<{lpr}, 0>"),  # small batches / general
     "bwd_sgd_fwd": ("k_sgd_small<{lpr}, true>",),  # ... with the next batch's forward in the launch
     "grad_quant_pack": ("k_qpack<{lpr}>", "k_quant_pack<{lpr}>"),
-    "apply_sparse_update": ("k_apply_flat<{lpr},", "k_apply_merge<{lpr}, false>", "k_apply_ranges<{lpr}>"),
+    "apply_sparse_update": ("k_apply_flat2<{lpr},", "k_apply_flat<{lpr},", "k_apply_pos<{lpr}, false>",
+                            "k_apply_ranges<{lpr}>"),
     # N > 1 at the step boundary: the apply of step i + the forward of step i+1 in one launch (merge)
     "apply_sparse_update_fwd": ("k_apply_pos<{lpr}, true>",),
     # ... or the flat apply, then its finalize + the forward in one launch: a list = both kernels' sum
-    "apply_sparse_update_fwd_fin": ["k_apply_flat<{lpr},", "k_finalize_fwd<{lpr},"],
+    "apply_sparse_update_fwd_fin": [("k_apply_flat2<{lpr},", "k_apply_flat<{lpr},"), "k_finalize_fwd<{lpr},"],
     "apply_local": "k_apply_local<{lpr},",
 }
 
@@ -179,7 +180,8 @@ def pmc_traffic(path, phase, D, workload=None):
         return None
 
     # a list: the phase is several launches, their bytes and times summed; a tuple: alternatives
-    parts = [one((p,)) for p in sym] if isinstance(sym, list) else [one(sym if isinstance(sym, tuple) else (sym,))]
+    parts = ([one(p if isinstance(p, tuple) else (p,)) for p in sym] if isinstance(sym, list)
+             else [one(sym if isinstance(sym, tuple) else (sym,))])
     if any(v is None for v in parts):
         return None
     med = [v.get("median_us") for v in parts]

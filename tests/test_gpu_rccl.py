@@ -140,3 +140,25 @@ def test_bench_launcher_rccl_world1():
                                            "(RCCL at world size 1)")
     assert line["kernels_ms"].get("apply_sparse_update_fwd") or line["kernels_ms"].get("apply_sparse_update")
     assert line["mlp_grad_exchange"]["collectives"] == 2
+
+
+def test_bench_two_ranks_gloo_on_one_gpu():
+    """bench.py's N > 1 step end to end: two ranks under torch.distributed.run sharing the GPU over
+    Gloo (the functional rehearsal of the multi-GPU driver run): the exchange's all-gathers served
+    by torch.distributed through the library's callback, the flat apply (two entries per lane
+    group at this size) then the finalize + next forward launch; both ranks' tables and maxima
+    end bit-identical (the line's replica check) with no device error."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--config", "kaggle", "--steps", "10", "--warmup", "3",
+           "--cpu-baseline", "0", "--gather-batch", "0", "--mlp-iters", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] is not None and line["device_errors"] == 0
+    assert line["replicas_bit_identical"] is True
+    assert line["collectives"]["world_size"] == 2 and line["collectives"]["per_step"] == 2
+    assert "apply_sparse_update_fwd" in line["kernels_ms"]
